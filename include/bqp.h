@@ -1,0 +1,172 @@
+/*
+ * bqp.h — C ABI of the MI355X batched MPC QP solver (libbqp.so).
+ *
+ * Drop-in boundary for the per-step optimal-control solve of bevanda/Learning-Based-MPC.
+ * The reference issues that solve through two MATLAB call surfaces; each entry point below
+ * names the one it replaces:
+ *
+ *   fmincon(COSTFUN, opt_var, [],[],[],[],[],[], CONSFUN, options)
+ *       matlab/LBMPC/functions/ocpLMPC.m:20-24      (LMPC, form F1)
+ *       matlab/LBMPC/functions/ocpLBMPC.m:157-161    (LBMPC QP sub-problem, form F3)
+ *       matlab/trackingMPC/RunExample.m:134-136      (tracking MPC, form F5)
+ *   solver('x0',..,'lbx',..,'ubx',..,'lbg',..,'ubg',..)  (CasADi nlpsol/IPOPT)
+ *       matlab/LBMPC/examples/DMS_tracking_LMPC_casadi.m:163-167  (form F2)
+ *       matlab/LBMPC/examples/DSS_tracking_LMPC_casadi.m:155-160
+ *
+ * Two solver entry points:
+ *   bqp_solve_ocp_batched   structured stage-wise OCP (the fast path; Riccati KKT on GPU)
+ *   bqp_quadprog_batched    MATLAB quadprog semantics on dense per-instance (H,f,A,b,Aeq,beq,lb,ub)
+ * and *_device variants taking device pointers + a hipStream_t (passed as void*).
+ *
+ * Conventions
+ *   - all matrices are column-major (MATLAB layout), fp64;
+ *   - every input array carries an element stride between instances; stride 0 = one copy shared
+ *     by the whole batch (broadcast);
+ *   - return code: BQP_OK (0) or a negative BQP_E_* (API error: bad dims, HIP failure, missing
+ *     GPU); per-instance status is exitflag[] with quadprog meanings:
+ *       1 converged, 0 iteration limit, -2 primal infeasible, -3 dual infeasible/unbounded,
+ *       -6 non-convex, -8 numerical failure;
+ *   - thread safety: one bqp_handle per host thread / stream; no global mutable state.
+ */
+#ifndef BQP_H
+#define BQP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BQP_OK 0
+#define BQP_E_ARG (-1)       /* invalid dimensions / NULL required pointer */
+#define BQP_E_HIP (-2)       /* HIP runtime error (allocation, launch, copy) */
+#define BQP_E_NODEV (-3)     /* no usable gfx950 device */
+#define BQP_E_UNSUPPORTED (-4) /* dimensions outside the compiled kernel set */
+
+typedef struct bqp_handle_s* bqp_handle;
+
+typedef struct {
+    int max_iter;      /* default 50 */
+    double tol_stat;   /* stationarity inf-norm (absolute), default 1e-10 */
+    double tol_feas;   /* primal residual inf-norm (absolute), default 1e-10 */
+    double tol_comp;   /* average complementarity mu, default 1e-12 */
+    double tau;        /* fraction-to-boundary, default 0.995 */
+    int precision;     /* 0 = fp64 (default) */
+    int want_duals;    /* 1: fill the multiplier outputs (structured API) */
+} bqp_options;
+
+typedef struct {
+    int iterations;
+    double constrviolation;  /* max(primal eq, primal ineq) at exit */
+    double firstorderopt;    /* stationarity inf-norm at exit */
+    double mu;               /* average complementarity at exit */
+    double kkt[4];           /* stationarity, primal eq, primal ineq, complementarity (inf) */
+} bqp_output;
+
+/* ------------------------------------------------------------------------------------------
+ * Structured OCP (form F1/F2/F4/F5 after the host shim's change of variables):
+ *
+ *   x_{k+1} = A x_k + B u_k + c              k = 0..N-1,   x_0 = x0 (fixed)
+ *   theta  in R^np  (global steady-state parameter, free)
+ *   min  sum_{k=0}^{N} 0.5 v_k' W_k v_k + w_k' v_k,  v_k = [x_k; u_k; theta]  (nv = nx+nu+np;
+ *        for k = N the u block of W_N / w_N is ignored)
+ *   s.t. xlb_k <= x_k <= xub_k (k = 1..N),  ulb_k <= u_k <= uub_k (k = 0..N-1)  (+-INFINITY ok)
+ *        Fp [x_kp; u_kp; theta] <= hp     (n_poly rows, polytope at stage kp = poly_stage)
+ *
+ * Reference mapping: costLMPC.m:20-45 / constraintsLMPC.m:15-41 (F1),
+ * DMS_tracking_LMPC_casadi.m:223-287 (F2), trackingMPC/costFunction.m:20-39 /
+ * constraintsFunction.m:20-38 (F5); the terminal polytope is term_set.mat's F_w_N (616x5).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    int nx, nu, np, N;
+    int n_poly;      /* rows of the polytope block (>= 0) */
+    int poly_stage;  /* stage the polytope acts on, 0..N */
+} bqp_ocp_dims;
+
+typedef struct {
+    const double* A;    /* nx*nx                                  stride sA  */
+    const double* B;    /* nx*nu                                  stride sB  */
+    const double* c;    /* nx, NULL = 0                           stride sc  */
+    const double* W;    /* (N+1) blocks nv*nv                     stride sW  */
+    const double* w;    /* (N+1)*nv, NULL = 0                     stride sw  */
+    const double* xlb;  /* (N+1)*nx, NULL = -inf (stage 0 unused) stride sxb */
+    const double* xub;  /* (N+1)*nx, NULL = +inf                  stride sxb */
+    const double* ulb;  /* N*nu, NULL = -inf                      stride sub */
+    const double* uub;  /* N*nu, NULL = +inf                      stride sub */
+    const double* Fp;   /* n_poly*nv (column-major, n_poly rows)  stride sFp */
+    const double* hp;   /* n_poly                                 stride shp */
+    const double* x0;   /* nx                                     stride sx0 */
+    int64_t sA, sB, sc, sW, sw, sxb, sub, sFp, shp, sx0;
+} bqp_ocp_data;
+
+/* Optional multiplier outputs of the structured solve (NULL members are skipped). */
+typedef struct {
+    double* pi;     /* batch*N*nx: dynamics multipliers for x_{k+1} = A x_k + B u_k + c   */
+    double* lam_x;  /* batch*(N+1)*nx*2: [lower, upper] per stage (0 for absent bounds) */
+    double* lam_u;  /* batch*N*nu*2                                                    */
+    double* lam_p;  /* batch*n_poly                                                    */
+} bqp_ocp_duals;
+
+/* Lifecycle.  device < 0 selects the current HIP device. */
+int bqp_create(bqp_handle* h, int device);
+int bqp_destroy(bqp_handle h);
+void bqp_default_options(bqp_options* opt);
+const char* bqp_version(void);
+
+/* Host-pointer structured solve.  Outputs (host): x batch*(N+1)*nx, u batch*N*nu,
+ * theta batch*np, fval batch, exitflag batch, out batch (out/fval/duals may be NULL). */
+int bqp_solve_ocp_batched(bqp_handle h, const bqp_ocp_dims* dims, int batch,
+                          const bqp_ocp_data* data, const bqp_options* opt,
+                          double* x, double* u, double* theta, double* fval, int* exitflag,
+                          bqp_output* out, const bqp_ocp_duals* duals);
+
+/* Device-pointer structured solve (all data/output pointers are device memory owned by the
+ * caller; stream is a hipStream_t, NULL = default stream).  Asynchronous: returns after the
+ * launch; synchronise the stream before reading outputs. */
+int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* dims, int batch,
+                                 const bqp_ocp_data* data, const bqp_options* opt,
+                                 double* x, double* u, double* theta, double* fval,
+                                 int* exitflag, bqp_output* out, const bqp_ocp_duals* duals,
+                                 void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * quadprog-compatible dense batched solve:
+ *   [x,fval,exitflag,output,lambda] = quadprog(H,f,A,b,Aeq,beq,lb,ub,x0,options)
+ *   min 0.5 x'Hx + f'x  s.t.  A x <= b, Aeq x = beq, lb <= x <= ub.
+ * H n*n, f n, A m*n, b m, Aeq me*n, beq me, lb/ub n (NULL = unbounded), x0 ignored (IPM).
+ * lambda outputs follow quadprog: H x + f + A'l_ineqlin + Aeq'l_eqlin - l_lower + l_upper = 0.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    int n;   /* variables */
+    int m;   /* inequality rows */
+    int me;  /* equality rows */
+} bqp_dims;
+
+typedef struct {
+    int64_t sH, sf, sA, sb, sAeq, sbeq, slb, sub;  /* element strides, 0 = shared */
+} bqp_strides;
+
+int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_strides* st,
+                         const double* H, const double* f, const double* A, const double* b,
+                         const double* Aeq, const double* beq, const double* lb,
+                         const double* ub, const double* x0, const bqp_options* opt,
+                         double* x, double* fval, int* exitflag, double* lam_ineqlin,
+                         double* lam_eqlin, double* lam_lower, double* lam_upper,
+                         bqp_output* out);
+
+int bqp_quadprog_batched_device(bqp_handle h, const bqp_dims* d, int batch,
+                                const bqp_strides* st, const double* H, const double* f,
+                                const double* A, const double* b, const double* Aeq,
+                                const double* beq, const double* lb, const double* ub,
+                                const bqp_options* opt, double* x, double* fval, int* exitflag,
+                                double* lam_ineqlin, double* lam_eqlin, double* lam_lower,
+                                double* lam_upper, bqp_output* out, void* stream);
+
+/* Timing of the most recent solve on this handle: kernel time measured with hipEvents on the
+ * launch stream (ms), and the number of kernel launches it covered. */
+int bqp_last_kernel_ms(bqp_handle h, double* ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BQP_H */

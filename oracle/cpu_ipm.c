@@ -1,0 +1,735 @@
+/*
+ * TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): C restatement of the structured Mehrotra
+ * predictor-corrector IPM specified in oracle/ocp_ipm.py, written in the same restructured
+ * (closed-loop) form as the HIP kernel learning-based-mpc_amd/csrc/bqp_ocp.hip so that GPU
+ * iterates can be compared to it at round-off level.  It is also the timed CPU baseline of
+ * bench.py (cpu_baseline.kind = "port": one instance per OpenMP thread, fp64, -O3).
+ *
+ * It consumes the same bqp_ocp_dims/bqp_ocp_data description as include/bqp.h.  The reference
+ * itself (MATLAB fmincon-sqp / CasADi-IPOPT) cannot run here.
+ *
+ * Build: make -C oracle   ->  oracle/_build/libcpu_ipm.so
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#include "../include/bqp.h"
+
+#define MAXNS 8
+#define MAXNU 4
+#define MAXNV 12
+
+typedef struct {
+    int nx, nu, np, ns, nv, N, mp, kp;
+    double Abar[MAXNS][MAXNS], Bbar[MAXNS][MAXNU], cbar[MAXNS];
+    const double* H;   /* (N+1)*nv*nv internal order [x th u], row-major [i][j] */
+    const double* Fp;  /* mp*nv internal order row-major                        */
+} prob_t;
+
+typedef struct {
+    double *s, *u, *pi;                  /* (N+1)*ns, N*nu, (N+1)*ns                 */
+    double *g;                           /* (N+1)*nv linear term, internal order     */
+    double *xlb, *xub, *ulb, *uub, *hp;  /* bounds (inf allowed)                      */
+    double *tx, *lx, *tu, *lu, *tp, *lp; /* x rows: (N+1)*nx*2 [upper,lower]; u: N*nu*2 */
+    /* work */
+    double *rs, *ru, *re, *rix, *riu, *rip;
+    double *ds, *du, *dpi, *dtx, *dlx, *dtu, *dlu, *dtp, *dlp;
+    double *Ptab, *Ktab, *Rinv, *p, *qs, *qu, *wv, *qt, *kff, *f;
+    double *Dx, *Du, *FD;
+    double P0inv[MAXNS * MAXNS];
+} work_t;
+
+static int perm_of(const prob_t* P, int i) {
+    /* internal index i -> external [x; u; th] index */
+    if (i < P->nx) return i;
+    if (i < P->ns) return P->nx + P->nu + (i - P->nx);
+    return P->nx + (i - P->ns);
+}
+
+/* ---------------- small dense helpers ---------------- */
+static int chol_inv(int n, const double* M, double* Minv) {
+    /* Minv = M^{-1} for SPD n x n (n <= MAXNS) via Cholesky */
+    double L[MAXNS * MAXNS];
+    memset(L, 0, sizeof(L));
+    for (int j = 0; j < n; ++j) {
+        double d = M[j * n + j];
+        for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+        if (!(d > 0)) return -1;
+        d = sqrt(d);
+        L[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double v = M[i * n + j];
+            for (int k = 0; k < j; ++k) v -= L[i * n + k] * L[j * n + k];
+            L[i * n + j] = v / d;
+        }
+    }
+    /* inverse of L, then Minv = L^-T L^-1 */
+    double Li[MAXNS * MAXNS];
+    memset(Li, 0, sizeof(Li));
+    for (int i = 0; i < n; ++i) {
+        Li[i * n + i] = 1.0 / L[i * n + i];
+        for (int j = 0; j < i; ++j) {
+            double v = 0;
+            for (int k = j; k < i; ++k) v -= L[i * n + k] * Li[k * n + j];
+            Li[i * n + j] = v / L[i * n + i];
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double v = 0;
+            for (int k = (i > j ? i : j); k < n; ++k) v += Li[k * n + i] * Li[k * n + j];
+            Minv[i * n + j] = v;
+        }
+    return 0;
+}
+
+/* ---------------- residuals ---------------- */
+static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, double* musum,
+                      int* mcount) {
+    const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv;
+    double st = 0, fe = 0, cs = 0;
+    int mc = 0;
+    for (int k = 0; k <= N; ++k) {
+        const double* H = P->H + (size_t)k * nv * nv;
+        double v[MAXNV];
+        for (int i = 0; i < ns; ++i) v[i] = W->s[k * ns + i];
+        for (int i = 0; i < nu; ++i) v[ns + i] = (k < N) ? W->u[k * nu + i] : 0.0;
+        int nvk = (k < N) ? nv : ns;
+        double gv[MAXNV];
+        for (int i = 0; i < nvk; ++i) {
+            double a = W->g[k * nv + i];
+            for (int j = 0; j < nvk; ++j) a += H[i * nv + j] * v[j];
+            gv[i] = a;
+        }
+        for (int i = 0; i < ns; ++i) {
+            double a = gv[i];
+            if (k < N)
+                for (int j = 0; j < ns; ++j) a += P->Abar[j][i] * W->pi[(k + 1) * ns + j];
+            if (k > 0) a -= W->pi[k * ns + i];
+            W->rs[k * ns + i] = a;
+        }
+        if (k < N)
+            for (int i = 0; i < nu; ++i) {
+                double a = gv[ns + i];
+                for (int j = 0; j < ns; ++j) a += P->Bbar[j][i] * W->pi[(k + 1) * ns + j];
+                W->ru[k * nu + i] = a;
+            }
+        /* box rows */
+        for (int i = 0; i < nx; ++i) {
+            double xi = W->s[k * ns + i];
+            int o = (k * nx + i) * 2;
+            double ri_u = 0, ri_l = 0;
+            if (k > 0 && isfinite(W->xub[k * nx + i])) {
+                W->rs[k * ns + i] += W->lx[o];
+                ri_u = xi + W->tx[o] - W->xub[k * nx + i];
+                cs += W->tx[o] * W->lx[o]; ++mc;
+            }
+            if (k > 0 && isfinite(W->xlb[k * nx + i])) {
+                W->rs[k * ns + i] -= W->lx[o + 1];
+                ri_l = -xi + W->tx[o + 1] + W->xlb[k * nx + i];
+                cs += W->tx[o + 1] * W->lx[o + 1]; ++mc;
+            }
+            W->rix[o] = ri_u; W->rix[o + 1] = ri_l;
+        }
+        if (k < N)
+            for (int i = 0; i < nu; ++i) {
+                double ui = W->u[k * nu + i];
+                int o = (k * nu + i) * 2;
+                double ri_u = 0, ri_l = 0;
+                if (isfinite(W->uub[k * nu + i])) {
+                    W->ru[k * nu + i] += W->lu[o];
+                    ri_u = ui + W->tu[o] - W->uub[k * nu + i];
+                    cs += W->tu[o] * W->lu[o]; ++mc;
+                }
+                if (isfinite(W->ulb[k * nu + i])) {
+                    W->ru[k * nu + i] -= W->lu[o + 1];
+                    ri_l = -ui + W->tu[o + 1] + W->ulb[k * nu + i];
+                    cs += W->tu[o + 1] * W->lu[o + 1]; ++mc;
+                }
+                W->riu[o] = ri_u; W->riu[o + 1] = ri_l;
+            }
+        if (k < N)
+            for (int i = 0; i < ns; ++i) {
+                double a = P->cbar[i] - W->s[(k + 1) * ns + i];
+                for (int j = 0; j < ns; ++j) a += P->Abar[i][j] * W->s[k * ns + j];
+                for (int j = 0; j < nu; ++j) a += P->Bbar[i][j] * W->u[k * nu + j];
+                W->re[k * ns + i] = a;
+            }
+    }
+    /* polytope rows */
+    {
+        const int kp = P->kp;
+        double v[MAXNV];
+        for (int i = 0; i < ns; ++i) v[i] = W->s[kp * ns + i];
+        for (int i = 0; i < nu; ++i) v[ns + i] = (kp < N) ? W->u[kp * nu + i] : 0.0;
+        double gp[MAXNV];
+        memset(gp, 0, sizeof(gp));
+        for (int r = 0; r < P->mp; ++r) {
+            const double* F = P->Fp + (size_t)r * nv;
+            double a = W->tp[r] - W->hp[r];
+            for (int j = 0; j < nv; ++j) {
+                a += F[j] * v[j];
+                gp[j] += F[j] * W->lp[r];
+            }
+            W->rip[r] = a;
+            cs += W->tp[r] * W->lp[r]; ++mc;
+        }
+        for (int i = 0; i < ns; ++i) W->rs[kp * ns + i] += gp[i];
+        if (kp < N)
+            for (int i = 0; i < nu; ++i) W->ru[kp * nu + i] += gp[ns + i];
+    }
+    for (int i = 0; i < nx; ++i) W->rs[i] = 0.0; /* x_0 fixed */
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < ns; ++i) st = fmax(st, fabs(W->rs[k * ns + i]));
+    for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < nu; ++i) st = fmax(st, fabs(W->ru[k * nu + i]));
+        for (int i = 0; i < ns; ++i) fe = fmax(fe, fabs(W->re[k * ns + i]));
+    }
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < 2 * nx; ++i) fe = fmax(fe, fabs(W->rix[k * nx * 2 + i]));
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < 2 * nu; ++i) fe = fmax(fe, fabs(W->riu[k * nu * 2 + i]));
+    for (int r = 0; r < P->mp; ++r) fe = fmax(fe, fabs(W->rip[r]));
+    *stat = st; *feas = fe; *musum = cs; *mcount = mc;
+}
+
+/* ---------------- factorisation ---------------- */
+static int factor(const prob_t* P, work_t* W) {
+    const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv;
+    /* box diagonals */
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < nx; ++i) {
+            int o = (k * nx + i) * 2;
+            double d = 0;
+            if (k > 0 && isfinite(W->xub[k * nx + i])) d += W->lx[o] / W->tx[o];
+            if (k > 0 && isfinite(W->xlb[k * nx + i])) d += W->lx[o + 1] / W->tx[o + 1];
+            W->Dx[k * nx + i] = d;
+        }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int o = (k * nu + i) * 2;
+            double d = 0;
+            if (isfinite(W->uub[k * nu + i])) d += W->lu[o] / W->tu[o];
+            if (isfinite(W->ulb[k * nu + i])) d += W->lu[o + 1] / W->tu[o + 1];
+            W->Du[k * nu + i] = d;
+        }
+    memset(W->FD, 0, sizeof(double) * nv * nv);
+    for (int r = 0; r < P->mp; ++r) {
+        const double* F = P->Fp + (size_t)r * nv;
+        double d = W->lp[r] / W->tp[r];
+        for (int i = 0; i < nv; ++i) {
+            double di = d * F[i];
+            for (int j = i; j < nv; ++j) W->FD[i * nv + j] += di * F[j];
+        }
+    }
+    for (int i = 0; i < nv; ++i)
+        for (int j = 0; j < i; ++j) W->FD[i * nv + j] = W->FD[j * nv + i];
+    /* Htilde(k)[i][j] */
+#define HT(k, i, j)                                                                     \
+    (P->H[((size_t)(k) * nv + (i)) * nv + (j)] +                                          \
+     ((i) == (j) ? ((i) < nx ? W->Dx[(k) * nx + (i)] : ((i) >= ns ? W->Du[(k) * nu + (i) - ns] : 0.0)) : 0.0) + \
+     ((k) == P->kp ? W->FD[(i) * nv + (j)] : 0.0))
+    double* PN = W->Ptab + (size_t)N * ns * ns;
+    for (int i = 0; i < ns; ++i)
+        for (int j = 0; j < ns; ++j) PN[i * ns + j] = HT(N, i, j);
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
+        /* F = [Abar Bbar] (ns x nv); M = Ht + F' Pn F */
+        double F[MAXNS][MAXNV];
+        for (int a = 0; a < ns; ++a) {
+            for (int j = 0; j < ns; ++j) F[a][j] = P->Abar[a][j];
+            for (int j = 0; j < nu; ++j) F[a][ns + j] = P->Bbar[a][j];
+        }
+        double PF[MAXNS][MAXNV], M[MAXNV][MAXNV];
+        for (int a = 0; a < ns; ++a)
+            for (int j = 0; j < nv; ++j) {
+                double v = 0;
+                for (int b = 0; b < ns; ++b) v += Pn[a * ns + b] * F[b][j];
+                PF[a][j] = v;
+            }
+        for (int i = 0; i < nv; ++i)
+            for (int j = 0; j < nv; ++j) {
+                double v = HT(k, i, j);
+                for (int a = 0; a < ns; ++a) v += F[a][i] * PF[a][j];
+                M[i][j] = v;
+            }
+        double Ruu[MAXNU * MAXNU], Ri[MAXNU * MAXNU];
+        for (int a = 0; a < nu; ++a)
+            for (int b = 0; b < nu; ++b) Ruu[a * nu + b] = M[ns + a][ns + b];
+        if (chol_inv(nu, Ruu, Ri)) return -1;
+        double* Kk = W->Ktab + (size_t)k * nu * ns;
+        for (int a = 0; a < nu; ++a)
+            for (int j = 0; j < ns; ++j) {
+                double v = 0;
+                for (int b = 0; b < nu; ++b) v -= Ri[a * nu + b] * M[ns + b][j];
+                Kk[a * ns + j] = v;
+            }
+        for (int a = 0; a < nu * nu; ++a) W->Rinv[(size_t)k * nu * nu + a] = Ri[a];
+        double* Pk = W->Ptab + (size_t)k * ns * ns;
+        for (int i = 0; i < ns; ++i)
+            for (int j = i; j < ns; ++j) {
+                double v = M[i][j];
+                for (int a = 0; a < nu; ++a) v += M[i][ns + a] * Kk[a * ns + j];
+                Pk[i * ns + j] = v;
+                Pk[j * ns + i] = v;
+            }
+    }
+#undef HT
+    /* theta block of P_0 */
+    {
+        const int np = P->np;
+        double Pt[MAXNS * MAXNS];
+        const double* P0 = W->Ptab;
+        for (int a = 0; a < np; ++a)
+            for (int b = 0; b < np; ++b) Pt[a * np + b] = P0[(nx + a) * ns + nx + b];
+        if (chol_inv(np, Pt, W->P0inv)) return -1;
+    }
+    return 0;
+}
+
+/* ---------------- solve ---------------- */
+/* rcx/rcu/rcp: complementarity right-hand side per row */
+static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const double* rcu,
+                      const double* rcp) {
+    const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv, np = P->np;
+    /* q = r_v + C' e,  e = (lam o ri - rc)/t */
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < ns; ++i) W->qs[k * ns + i] = W->rs[k * ns + i];
+        for (int i = 0; i < nx; ++i) {
+            int o = (k * nx + i) * 2;
+            double e = 0;
+            if (k > 0 && isfinite(W->xub[k * nx + i])) e += (W->lx[o] * W->rix[o] - rcx[o]) / W->tx[o];
+            if (k > 0 && isfinite(W->xlb[k * nx + i])) e -= (W->lx[o + 1] * W->rix[o + 1] - rcx[o + 1]) / W->tx[o + 1];
+            W->qs[k * ns + i] += e;
+        }
+        if (k < N)
+            for (int i = 0; i < nu; ++i) {
+                int o = (k * nu + i) * 2;
+                double e = W->ru[k * nu + i];
+                if (isfinite(W->uub[k * nu + i])) e += (W->lu[o] * W->riu[o] - rcu[o]) / W->tu[o];
+                if (isfinite(W->ulb[k * nu + i])) e -= (W->lu[o + 1] * W->riu[o + 1] - rcu[o + 1]) / W->tu[o + 1];
+                W->qu[k * nu + i] = e;
+            }
+    }
+    {
+        double gp[MAXNV];
+        memset(gp, 0, sizeof(gp));
+        for (int r = 0; r < P->mp; ++r) {
+            double e = (W->lp[r] * W->rip[r] - rcp[r]) / W->tp[r];
+            const double* F = P->Fp + (size_t)r * nv;
+            for (int j = 0; j < nv; ++j) gp[j] += F[j] * e;
+        }
+        for (int i = 0; i < ns; ++i) W->qs[P->kp * ns + i] += gp[i];
+        if (P->kp < N)
+            for (int i = 0; i < nu; ++i) W->qu[P->kp * nu + i] += gp[ns + i];
+    }
+    /* pre-pass: wv_k = P_{k+1} re_k ; qt_k = qs_k + K_k' qu_k */
+    for (int k = 0; k < N; ++k) {
+        const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
+        const double* Kk = W->Ktab + (size_t)k * nu * ns;
+        for (int i = 0; i < ns; ++i) {
+            double v = 0;
+            for (int j = 0; j < ns; ++j) v += Pn[i * ns + j] * W->re[k * ns + j];
+            W->wv[k * ns + i] = v;
+            double q = W->qs[k * ns + i];
+            for (int a = 0; a < nu; ++a) q += Kk[a * ns + i] * W->qu[k * nu + a];
+            W->qt[k * ns + i] = q;
+        }
+    }
+    /* backward sweep: y = p_{k+1} + w_k;  p_k = Abar' y + K_k' (Bbar' y) + qt_k */
+    for (int i = 0; i < ns; ++i) W->p[N * ns + i] = W->qs[N * ns + i];
+    for (int k = N - 1; k >= 0; --k) {
+        double y[MAXNS], by[MAXNU];
+        const double* Kk = W->Ktab + (size_t)k * nu * ns;
+        for (int i = 0; i < ns; ++i) y[i] = W->p[(k + 1) * ns + i] + W->wv[k * ns + i];
+        for (int a = 0; a < nu; ++a) {
+            double v = 0;
+            for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * y[j];
+            by[a] = v;
+        }
+        for (int i = 0; i < ns; ++i) {
+            double v = W->qt[k * ns + i];
+            for (int j = 0; j < ns; ++j) v += P->Abar[j][i] * y[j];
+            for (int a = 0; a < nu; ++a) v += Kk[a * ns + i] * by[a];
+            W->p[k * ns + i] = v;
+        }
+    }
+    /* post-backward: kff_k = -Rinv_k (qu_k + Bbar'(p_{k+1} + w_k)); f_k = Bbar kff_k + re_k */
+    for (int k = 0; k < N; ++k) {
+        double y[MAXNS], r[MAXNU];
+        for (int i = 0; i < ns; ++i) y[i] = W->p[(k + 1) * ns + i] + W->wv[k * ns + i];
+        for (int a = 0; a < nu; ++a) {
+            double v = W->qu[k * nu + a];
+            for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * y[j];
+            r[a] = v;
+        }
+        const double* Ri = W->Rinv + (size_t)k * nu * nu;
+        for (int a = 0; a < nu; ++a) {
+            double v = 0;
+            for (int b = 0; b < nu; ++b) v -= Ri[a * nu + b] * r[b];
+            W->kff[k * nu + a] = v;
+        }
+        for (int i = 0; i < ns; ++i) {
+            double v = W->re[k * ns + i];
+            for (int a = 0; a < nu; ++a) v += P->Bbar[i][a] * W->kff[k * nu + a];
+            W->f[k * ns + i] = v;
+        }
+    }
+    /* theta_0 step and forward sweep: ds_{k+1} = Abar ds_k + Bbar (K_k ds_k) + f_k */
+    for (int i = 0; i < nx; ++i) W->ds[i] = 0.0;
+    for (int a = 0; a < np; ++a) {
+        double v = 0;
+        for (int b = 0; b < np; ++b) v -= W->P0inv[a * np + b] * W->p[nx + b];
+        W->ds[nx + a] = v;
+    }
+    for (int k = 0; k < N; ++k) {
+        const double* Kk = W->Ktab + (size_t)k * nu * ns;
+        const double* d = W->ds + k * ns;
+        double kd[MAXNU];
+        for (int a = 0; a < nu; ++a) {
+            double v = 0;
+            for (int j = 0; j < ns; ++j) v += Kk[a * ns + j] * d[j];
+            kd[a] = v;
+        }
+        for (int i = 0; i < ns; ++i) {
+            double v = W->f[k * ns + i];
+            for (int j = 0; j < ns; ++j) v += P->Abar[i][j] * d[j];
+            for (int a = 0; a < nu; ++a) v += P->Bbar[i][a] * kd[a];
+            W->ds[(k + 1) * ns + i] = v;
+        }
+    }
+    /* post-forward: du, dpi */
+    for (int k = 0; k < N; ++k) {
+        const double* Kk = W->Ktab + (size_t)k * nu * ns;
+        for (int a = 0; a < nu; ++a) {
+            double v = W->kff[k * nu + a];
+            for (int j = 0; j < ns; ++j) v += Kk[a * ns + j] * W->ds[k * ns + j];
+            W->du[k * nu + a] = v;
+        }
+    }
+    for (int k = 1; k <= N; ++k) {
+        const double* Pk = W->Ptab + (size_t)k * ns * ns;
+        for (int i = 0; i < ns; ++i) {
+            double v = W->p[k * ns + i];
+            for (int j = 0; j < ns; ++j) v += Pk[i * ns + j] * W->ds[k * ns + j];
+            W->dpi[k * ns + i] = v;
+        }
+    }
+    /* slack / multiplier steps */
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < nx; ++i) {
+            int o = (k * nx + i) * 2;
+            double dx = W->ds[k * ns + i];
+            W->dtx[o] = W->dtx[o + 1] = W->dlx[o] = W->dlx[o + 1] = 0;
+            if (k > 0 && isfinite(W->xub[k * nx + i])) {
+                W->dtx[o] = -W->rix[o] - dx;
+                W->dlx[o] = (-rcx[o] - W->lx[o] * W->dtx[o]) / W->tx[o];
+            }
+            if (k > 0 && isfinite(W->xlb[k * nx + i])) {
+                W->dtx[o + 1] = -W->rix[o + 1] + dx;
+                W->dlx[o + 1] = (-rcx[o + 1] - W->lx[o + 1] * W->dtx[o + 1]) / W->tx[o + 1];
+            }
+        }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int o = (k * nu + i) * 2;
+            double du = W->du[k * nu + i];
+            W->dtu[o] = W->dtu[o + 1] = W->dlu[o] = W->dlu[o + 1] = 0;
+            if (isfinite(W->uub[k * nu + i])) {
+                W->dtu[o] = -W->riu[o] - du;
+                W->dlu[o] = (-rcu[o] - W->lu[o] * W->dtu[o]) / W->tu[o];
+            }
+            if (isfinite(W->ulb[k * nu + i])) {
+                W->dtu[o + 1] = -W->riu[o + 1] + du;
+                W->dlu[o + 1] = (-rcu[o + 1] - W->lu[o + 1] * W->dtu[o + 1]) / W->tu[o + 1];
+            }
+        }
+    {
+        const int kp = P->kp;
+        double dv[MAXNV];
+        for (int i = 0; i < ns; ++i) dv[i] = W->ds[kp * ns + i];
+        for (int i = 0; i < nu; ++i) dv[ns + i] = (kp < N) ? W->du[kp * nu + i] : 0.0;
+        for (int r = 0; r < P->mp; ++r) {
+            const double* F = P->Fp + (size_t)r * nv;
+            double a = 0;
+            for (int j = 0; j < nv; ++j) a += F[j] * dv[j];
+            W->dtp[r] = -W->rip[r] - a;
+            W->dlp[r] = (-rcp[r] - W->lp[r] * W->dtp[r]) / W->tp[r];
+        }
+    }
+}
+
+static double max_step(const prob_t* P, work_t* W) {
+    const int N = P->N, nx = P->nx, nu = P->nu;
+    double a = 1.0;
+#define RATIO(v, dv) \
+    if ((dv) < 0) { double q = -(v) / (dv); if (q < a) a = q; }
+    for (int k = 1; k <= N; ++k)
+        for (int i = 0; i < nx; ++i) {
+            int o = (k * nx + i) * 2;
+            if (isfinite(W->xub[k * nx + i])) { RATIO(W->tx[o], W->dtx[o]); RATIO(W->lx[o], W->dlx[o]); }
+            if (isfinite(W->xlb[k * nx + i])) { RATIO(W->tx[o + 1], W->dtx[o + 1]); RATIO(W->lx[o + 1], W->dlx[o + 1]); }
+        }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int o = (k * nu + i) * 2;
+            if (isfinite(W->uub[k * nu + i])) { RATIO(W->tu[o], W->dtu[o]); RATIO(W->lu[o], W->dlu[o]); }
+            if (isfinite(W->ulb[k * nu + i])) { RATIO(W->tu[o + 1], W->dtu[o + 1]); RATIO(W->lu[o + 1], W->dlu[o + 1]); }
+        }
+    for (int r = 0; r < P->mp; ++r) { RATIO(W->tp[r], W->dtp[r]); RATIO(W->lp[r], W->dlp[r]); }
+#undef RATIO
+    return a;
+}
+
+static double comp_after(const prob_t* P, work_t* W, double a) {
+    const int N = P->N, nx = P->nx, nu = P->nu;
+    double s = 0;
+    for (int k = 1; k <= N; ++k)
+        for (int i = 0; i < nx; ++i) {
+            int o = (k * nx + i) * 2;
+            if (isfinite(W->xub[k * nx + i])) s += (W->tx[o] + a * W->dtx[o]) * (W->lx[o] + a * W->dlx[o]);
+            if (isfinite(W->xlb[k * nx + i])) s += (W->tx[o + 1] + a * W->dtx[o + 1]) * (W->lx[o + 1] + a * W->dlx[o + 1]);
+        }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i) {
+            int o = (k * nu + i) * 2;
+            if (isfinite(W->uub[k * nu + i])) s += (W->tu[o] + a * W->dtu[o]) * (W->lu[o] + a * W->dlu[o]);
+            if (isfinite(W->ulb[k * nu + i])) s += (W->tu[o + 1] + a * W->dtu[o + 1]) * (W->lu[o + 1] + a * W->dlu[o + 1]);
+        }
+    for (int r = 0; r < P->mp; ++r) s += (W->tp[r] + a * W->dtp[r]) * (W->lp[r] + a * W->dlp[r]);
+    return s;
+}
+
+/* ---------------- one instance ---------------- */
+typedef struct {
+    int max_iter;
+    double tol_stat, tol_feas, tol_comp, tau;
+} opts_t;
+
+static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, double* kkt) {
+    const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns;
+    const int nxr = (N + 1) * nx * 2, nur = N * nu * 2;
+    double stat, feas, cs;
+    int mc;
+    /* init: t = lam = 1 on every row, unit-scaled least-squares Newton solve (rc = t o lam) */
+    for (int i = 0; i < nxr; ++i) { W->tx[i] = 1.0; W->lx[i] = 1.0; }
+    for (int i = 0; i < nur; ++i) { W->tu[i] = 1.0; W->lu[i] = 1.0; }
+    for (int r = 0; r < P->mp; ++r) { W->tp[r] = 1.0; W->lp[r] = 1.0; }
+    double *rcx = (double*)malloc(sizeof(double) * (nxr + nur + P->mp + 1));
+    double *rcu = rcx + nxr, *rcp = rcu + nur;
+    for (int i = 0; i < nxr + nur + P->mp; ++i) rcx[i] = 1.0;
+    residuals(P, W, &stat, &feas, &cs, &mc);
+    if (factor(P, W)) { free(rcx); return -8; }
+    solve_kkt(P, W, rcx, rcu, rcp);
+    for (int i = 0; i < (N + 1) * ns; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
+    for (int i = 0; i < N * nu; ++i) W->u[i] += W->du[i];
+    /* tt = b - C v = t_old + dt = 1 + dt ; lam~ = -tt ; shift */
+    double tmin = INFINITY, tmax = -INFINITY;
+#define PRESENT_X(k, i, o) ((k) > 0 && isfinite(((o) & 1) ? W->xlb[(k) * nx + (i)] : W->xub[(k) * nx + (i)]))
+#define PRESENT_U(k, i, o) (isfinite(((o) & 1) ? W->ulb[(k) * nu + (i)] : W->uub[(k) * nu + (i)]))
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < nx; ++i)
+            for (int h = 0; h < 2; ++h)
+                if (PRESENT_X(k, i, h)) {
+                    double t = 1.0 + W->dtx[(k * nx + i) * 2 + h];
+                    tmin = fmin(tmin, t); tmax = fmax(tmax, t);
+                }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i)
+            for (int h = 0; h < 2; ++h)
+                if (PRESENT_U(k, i, h)) {
+                    double t = 1.0 + W->dtu[(k * nu + i) * 2 + h];
+                    tmin = fmin(tmin, t); tmax = fmax(tmax, t);
+                }
+    for (int r = 0; r < P->mp; ++r) {
+        double t = 1.0 + W->dtp[r];
+        tmin = fmin(tmin, t); tmax = fmax(tmax, t);
+    }
+    double shp = (tmin <= 0) ? 1.0 - tmin : 0.0;
+    double shd = (tmax >= 0) ? 1.0 + tmax : 0.0;
+    for (int k = 0; k <= N; ++k)
+        for (int i = 0; i < nx; ++i)
+            for (int h = 0; h < 2; ++h) {
+                int o = (k * nx + i) * 2 + h;
+                if (PRESENT_X(k, i, h)) {
+                    double t = 1.0 + W->dtx[o];
+                    W->tx[o] = t + shp; W->lx[o] = -t + shd;
+                } else { W->tx[o] = 1.0; W->lx[o] = 0.0; }
+            }
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < nu; ++i)
+            for (int h = 0; h < 2; ++h) {
+                int o = (k * nu + i) * 2 + h;
+                if (PRESENT_U(k, i, h)) {
+                    double t = 1.0 + W->dtu[o];
+                    W->tu[o] = t + shp; W->lu[o] = -t + shd;
+                } else { W->tu[o] = 1.0; W->lu[o] = 0.0; }
+            }
+    for (int r = 0; r < P->mp; ++r) {
+        double t = 1.0 + W->dtp[r];
+        W->tp[r] = t + shp; W->lp[r] = -t + shd;
+    }
+    /* main loop */
+    int flag = 0, it;
+    double mu = 0;
+    for (it = 0; it <= op->max_iter; ++it) {
+        residuals(P, W, &stat, &feas, &cs, &mc);
+        mu = cs / (mc > 0 ? mc : 1);
+        if (stat <= op->tol_stat && feas <= op->tol_feas && mu <= op->tol_comp) { flag = 1; break; }
+        if (it == op->max_iter) break;
+        if (factor(P, W)) { flag = -8; break; }
+        for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i];
+        for (int i = 0; i < nur; ++i) rcu[i] = W->tu[i] * W->lu[i];
+        for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r];
+        solve_kkt(P, W, rcx, rcu, rcp);
+        double a = max_step(P, W);
+        double mua = comp_after(P, W, a) / (mc > 0 ? mc : 1);
+        double sg = mua / mu;
+        sg = sg * sg * sg;
+        for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i] + W->dtx[i] * W->dlx[i] - sg * mu;
+        for (int i = 0; i < nur; ++i) rcu[i] = W->tu[i] * W->lu[i] + W->dtu[i] * W->dlu[i] - sg * mu;
+        for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r] + W->dtp[r] * W->dlp[r] - sg * mu;
+        solve_kkt(P, W, rcx, rcu, rcp);
+        a = max_step(P, W) * op->tau;
+        if (a > 1.0) a = 1.0;
+        for (int i = 0; i < (N + 1) * ns; ++i) { W->s[i] += a * W->ds[i]; W->pi[i] += a * W->dpi[i]; }
+        for (int i = 0; i < N * nu; ++i) W->u[i] += a * W->du[i];
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < nx; ++i)
+                for (int h = 0; h < 2; ++h)
+                    if (PRESENT_X(k, i, h)) {
+                        int o = (k * nx + i) * 2 + h;
+                        W->tx[o] += a * W->dtx[o]; W->lx[o] += a * W->dlx[o];
+                    }
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i)
+                for (int h = 0; h < 2; ++h)
+                    if (PRESENT_U(k, i, h)) {
+                        int o = (k * nu + i) * 2 + h;
+                        W->tu[o] += a * W->dtu[o]; W->lu[o] += a * W->dlu[o];
+                    }
+        for (int r = 0; r < P->mp; ++r) { W->tp[r] += a * W->dtp[r]; W->lp[r] += a * W->dlp[r]; }
+    }
+#undef PRESENT_X
+#undef PRESENT_U
+    free(rcx);
+    *iters = it;
+    kkt[0] = stat; kkt[1] = feas; kkt[2] = mu;
+    return flag;
+}
+
+/* ---------------- batched entry ---------------- */
+static double* alloc0(size_t n) { return (double*)calloc(n ? n : 1, sizeof(double)); }
+
+int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int max_iter,
+                  double tol_stat, double tol_feas, double tol_comp, double tau, int nthreads,
+                  double* x, double* u, double* theta, int* exitflag, int* iters, double* kkt3) {
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
+    const int ns = nx + np, nv = ns + nu, mp = d->n_poly;
+    if (ns > MAXNS || nu > MAXNU || nv > MAXNV || N < 1) return BQP_E_ARG;
+    opts_t op = {max_iter, tol_stat, tol_feas, tol_comp, tau};
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    int err = 0;
+#pragma omp parallel
+    {
+        /* per-thread workspace */
+        double* H = alloc0((size_t)(N + 1) * nv * nv);
+        double* Fp = alloc0((size_t)mp * nv);
+        work_t W;
+        memset(&W, 0, sizeof(W));
+        W.s = alloc0((N + 1) * ns); W.u = alloc0(N * nu); W.pi = alloc0((N + 1) * ns);
+        W.g = alloc0((N + 1) * nv);
+        W.xlb = alloc0((N + 1) * nx); W.xub = alloc0((N + 1) * nx);
+        W.ulb = alloc0(N * nu); W.uub = alloc0(N * nu); W.hp = alloc0(mp);
+        W.tx = alloc0((N + 1) * nx * 2); W.lx = alloc0((N + 1) * nx * 2);
+        W.tu = alloc0(N * nu * 2); W.lu = alloc0(N * nu * 2);
+        W.tp = alloc0(mp); W.lp = alloc0(mp);
+        W.rs = alloc0((N + 1) * ns); W.ru = alloc0(N * nu); W.re = alloc0(N * ns);
+        W.rix = alloc0((N + 1) * nx * 2); W.riu = alloc0(N * nu * 2); W.rip = alloc0(mp);
+        W.ds = alloc0((N + 1) * ns); W.du = alloc0(N * nu); W.dpi = alloc0((N + 1) * ns);
+        W.dtx = alloc0((N + 1) * nx * 2); W.dlx = alloc0((N + 1) * nx * 2);
+        W.dtu = alloc0(N * nu * 2); W.dlu = alloc0(N * nu * 2);
+        W.dtp = alloc0(mp); W.dlp = alloc0(mp);
+        W.Ptab = alloc0((size_t)(N + 1) * ns * ns); W.Ktab = alloc0((size_t)N * nu * ns);
+        W.Rinv = alloc0((size_t)N * nu * nu); W.p = alloc0((N + 1) * ns);
+        W.qs = alloc0((N + 1) * ns); W.qu = alloc0(N * nu); W.wv = alloc0(N * ns);
+        W.qt = alloc0(N * ns); W.kff = alloc0(N * nu); W.f = alloc0(N * ns);
+        W.Dx = alloc0((N + 1) * nx); W.Du = alloc0(N * nu); W.FD = alloc0(nv * nv);
+        prob_t P;
+        memset(&P, 0, sizeof(P));
+        P.nx = nx; P.nu = nu; P.np = np; P.ns = ns; P.nv = nv; P.N = N; P.mp = mp;
+        P.kp = d->poly_stage;
+        P.H = H; P.Fp = Fp;
+#pragma omp for schedule(dynamic, 4)
+        for (int b = 0; b < batch; ++b) {
+            const double* A = D->A + b * D->sA;
+            const double* B = D->B + b * D->sB;
+            for (int i = 0; i < ns; ++i)
+                for (int j = 0; j < ns; ++j)
+                    P.Abar[i][j] = (i < nx && j < nx) ? A[j * nx + i] : (i == j ? 1.0 : 0.0);
+            for (int i = 0; i < ns; ++i)
+                for (int j = 0; j < nu; ++j) P.Bbar[i][j] = (i < nx) ? B[j * nx + i] : 0.0;
+            for (int i = 0; i < ns; ++i) P.cbar[i] = (i < nx && D->c) ? D->c[b * D->sc + i] : 0.0;
+            /* permuted H (internal [x th u]) from W (external [x u th], column-major) */
+            const double* Wb = D->W + b * D->sW;
+            for (int k = 0; k <= N; ++k)
+                for (int i = 0; i < nv; ++i)
+                    for (int j = 0; j < nv; ++j) {
+                        int ei = perm_of(&P, i), ej = perm_of(&P, j);
+                        double v = Wb[(size_t)k * nv * nv + (size_t)ej * nv + ei];
+                        if (k == N && (i >= ns || j >= ns)) v = 0.0;
+                        H[((size_t)k * nv + i) * nv + j] = v;
+                    }
+            for (int k = 0; k <= N; ++k)
+                for (int i = 0; i < nv; ++i) {
+                    double v = D->w ? D->w[b * D->sw + (size_t)k * nv + perm_of(&P, i)] : 0.0;
+                    W.g[k * nv + i] = (k == N && i >= ns) ? 0.0 : v;
+                }
+            const double* Fb = D->Fp ? D->Fp + b * D->sFp : NULL;
+            for (int r = 0; r < mp; ++r)
+                for (int i = 0; i < nv; ++i) {
+                    double v = Fb[(size_t)perm_of(&P, i) * mp + r];
+                    Fp[(size_t)r * nv + i] = (P.kp == N && i >= ns) ? 0.0 : v;
+                }
+            for (int r = 0; r < mp; ++r) W.hp[r] = D->hp[b * D->shp + r];
+            for (int i = 0; i < (N + 1) * nx; ++i) {
+                W.xlb[i] = D->xlb ? D->xlb[b * D->sxb + i] : -INFINITY;
+                W.xub[i] = D->xub ? D->xub[b * D->sxb + i] : INFINITY;
+            }
+            for (int i = 0; i < N * nu; ++i) {
+                W.ulb[i] = D->ulb ? D->ulb[b * D->sub + i] : -INFINITY;
+                W.uub[i] = D->uub ? D->uub[b * D->sub + i] : INFINITY;
+            }
+            memset(W.s, 0, sizeof(double) * (N + 1) * ns);
+            memset(W.u, 0, sizeof(double) * N * nu);
+            memset(W.pi, 0, sizeof(double) * (N + 1) * ns);
+            for (int i = 0; i < nx; ++i) W.s[i] = D->x0[b * D->sx0 + i];
+            int it = 0;
+            double k3[3] = {0, 0, 0};
+            int fl = solve_one(&P, &W, &op, &it, k3);
+            if (fl == -8) { /* keep going; report */ }
+            for (int k = 0; k <= N; ++k)
+                for (int i = 0; i < nx; ++i) x[((size_t)b * (N + 1) + k) * nx + i] = W.s[k * ns + i];
+            for (int k = 0; k < N; ++k)
+                for (int i = 0; i < nu; ++i) u[((size_t)b * N + k) * nu + i] = W.u[k * nu + i];
+            for (int i = 0; i < np; ++i) theta[(size_t)b * np + i] = W.s[nx + i];
+            exitflag[b] = fl;
+            if (iters) iters[b] = it;
+            if (kkt3) for (int i = 0; i < 3; ++i) kkt3[(size_t)b * 3 + i] = k3[i];
+        }
+        free(H); free(Fp);
+        free(W.s); free(W.u); free(W.pi); free(W.g); free(W.xlb); free(W.xub); free(W.ulb);
+        free(W.uub); free(W.hp); free(W.tx); free(W.lx); free(W.tu); free(W.lu); free(W.tp);
+        free(W.lp); free(W.rs); free(W.ru); free(W.re); free(W.rix); free(W.riu); free(W.rip);
+        free(W.ds); free(W.du); free(W.dpi); free(W.dtx); free(W.dlx); free(W.dtu); free(W.dlu);
+        free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Ktab); free(W.Rinv); free(W.p);
+        free(W.qs); free(W.qu); free(W.wv); free(W.qt); free(W.kff); free(W.f); free(W.Dx);
+        free(W.Du); free(W.FD);
+    }
+    return err;
+}

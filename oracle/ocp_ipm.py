@@ -1,0 +1,308 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Algorithm specification (numpy, one instance) of the structured Mehrotra predictor-corrector
+IPM that ``learning-based-mpc_amd/csrc/bqp_ocp.hip`` runs on the GPU and ``oracle/cpu_ipm.c``
+runs on the host.  The three implementations follow the same steps in the same order so that
+iterates agree to round-off (the reference keeps no solver iterates, so
+iterate parity is pinned to this statement instead).
+
+Problem (the structured OCP of ``oracle/qp_forms.py``):
+
+    s_k = [x_k; theta_k],  s_{k+1} = Abar s_k + Bbar u_k + cbar   (theta_{k+1} = theta_k)
+    x_0 = x0 fixed,  theta_0 free
+    min  sum_{k<N} 0.5 [s;u]' H_k [s;u] + g_k'[s;u]  +  0.5 s_N' H_N s_N + g_N' s_N
+    box rows on x_k (k = 1..N), u_k (k = 0..N-1); polytope rows Fp [x; u; theta] <= hp at kp.
+
+Residuals (Lagrangian L = f + sum pi_{k+1}'(Abar s_k + Bbar u_k + cbar - s_{k+1}) + lam'(C v - b)):
+
+    rv  = dL/dv   (x_0 entries are dropped: x_0 is fixed)
+    re_k = Abar s_k + Bbar u_k + cbar - s_{k+1}
+    ri  = C v + t - b
+    rc  = t o lam  (predictor)  |  t o lam + dt_a o dlam_a - sigma mu  (corrector)
+
+Newton step (D = lam / t):  (H + C'DC) dv + E'dpi = -(rv + C'((lam o ri - rc)/t)) with the
+linearised dynamics ds_{k+1} = Abar ds_k + Bbar du_k + re_k and dx_0 = 0, solved by the
+backward Riccati recursion and a forward rollout; dt = -ri - C dv, dlam = (-rc - lam o dt)/t.
+"""
+import numpy as np
+
+INF = np.inf
+
+
+class OCP:
+    """Flattened structured OCP (internal ordering s = [x; theta], u separately)."""
+
+    def __init__(self, d, x0, w=None):
+        self.nx, self.nu, self.np_, self.N = d['nx'], d['nu'], d['np'], d['N']
+        nx, nu, p, N = self.nx, self.nu, self.np_, self.N
+        ns = nx + p
+        self.ns = ns
+        self.x0 = np.asarray(x0, float).reshape(nx)
+        W = d['W']; w = d['w'] if w is None else w
+        # permutation [x; u; th] -> [s; u] = [x; th; u]
+        perm = np.concatenate([np.arange(nx), np.arange(nx + nu, nx + nu + p), np.arange(nx, nx + nu)])
+        self.H = np.zeros((N + 1, ns + nu, ns + nu))
+        self.g = np.zeros((N + 1, ns + nu))
+        for k in range(N + 1):
+            self.H[k] = W[k][np.ix_(perm, perm)]
+            self.g[k] = w[k][perm]
+        self.Abar = np.zeros((ns, ns)); self.Abar[:nx, :nx] = d['A']; self.Abar[nx:, nx:] = np.eye(p)
+        self.Bbar = np.zeros((ns, nu)); self.Bbar[:nx] = d['B']
+        self.cbar = np.zeros(ns); self.cbar[:nx] = d['c']
+        self.xlb, self.xub = d['xlb'].copy(), d['xub'].copy()
+        self.ulb, self.uub = d['ulb'].copy(), d['uub'].copy()
+        self.xlb[0] = -INF; self.xub[0] = INF                      # x_0 fixed: no rows
+        self.kp = d['kp']
+        Fp = d['Fp']
+        self.Fp = Fp[:, perm] if self.kp < N else np.hstack([Fp[:, :nx], Fp[:, nx + nu:], Fp[:, nx:nx + nu]])
+        self.hp = np.asarray(d['hp'], float).copy()
+        self.mp = self.Fp.shape[0]
+        # finite-bound masks
+        self.mxu = np.isfinite(self.xub); self.mxl = np.isfinite(self.xlb)
+        self.muu = np.isfinite(self.uub); self.mul = np.isfinite(self.ulb)
+        self.m = int(self.mxu.sum() + self.mxl.sum() + self.muu.sum() + self.mul.sum() + self.mp)
+
+
+class State:
+    def __init__(self, o):
+        N, ns, nu, nx = o.N, o.ns, o.nu, o.nx
+        self.s = np.zeros((N + 1, ns)); self.s[0, :nx] = o.x0
+        self.u = np.zeros((N, nu))
+        self.pi = np.zeros((N + 1, ns))          # pi[k] multiplies the constraint into s_k (k>=1)
+        # slacks / multipliers: x upper/lower, u upper/lower, polytope
+        self.txu = np.ones((N + 1, nx)); self.lxu = np.ones((N + 1, nx))
+        self.txl = np.ones((N + 1, nx)); self.lxl = np.ones((N + 1, nx))
+        self.tuu = np.ones((N, nu)); self.luu = np.ones((N, nu))
+        self.tul = np.ones((N, nu)); self.lul = np.ones((N, nu))
+        self.tp = np.ones(o.mp); self.lp = np.ones(o.mp)
+
+
+def _pvec(o, s, u):
+    """[x; u; th] stage vector of stage kp in the internal [s; u] ordering."""
+    k = o.kp
+    return np.concatenate([s[k], u[k]]) if k < o.N else s[k]
+
+
+def residuals(o, st):
+    N, nx, ns, nu = o.N, o.nx, o.ns, o.nu
+    s, u, pi = st.s, st.u, st.pi
+    rs = np.zeros((N + 1, ns)); ru = np.zeros((N, nu)); re = np.zeros((N, ns))
+    for k in range(N + 1):
+        H, g = o.H[k], o.g[k]
+        if k < N:
+            v = np.concatenate([s[k], u[k]])
+            gv = H @ v + g
+            rs[k] = gv[:ns] + o.Abar.T @ pi[k + 1]
+            ru[k] = gv[ns:] + o.Bbar.T @ pi[k + 1]
+            re[k] = o.Abar @ s[k] + o.Bbar @ u[k] + o.cbar - s[k + 1]
+        else:
+            rs[k] = H[:ns, :ns] @ s[k] + g[:ns]
+        if k > 0:
+            rs[k] -= pi[k]
+    # box rows
+    rs[:, :nx] += np.where(o.mxu, st.lxu, 0) - np.where(o.mxl, st.lxl, 0)
+    ru += np.where(o.muu, st.luu, 0) - np.where(o.mul, st.lul, 0)
+    # polytope rows
+    gp = o.Fp.T @ st.lp
+    rs[o.kp] += gp[:ns]
+    if o.kp < N:
+        ru[o.kp] += gp[ns:]
+    rs[0, :nx] = 0.0                                           # x_0 fixed
+    # inequality residuals ri = a'v + t - b
+    X = s[:, :nx]
+    rixu = np.where(o.mxu, X + st.txu - np.where(o.mxu, o.xub, 0), 0)
+    rixl = np.where(o.mxl, -X + st.txl + np.where(o.mxl, o.xlb, 0), 0)
+    riuu = np.where(o.muu, u + st.tuu - np.where(o.muu, o.uub, 0), 0)
+    riul = np.where(o.mul, -u + st.tul + np.where(o.mul, o.ulb, 0), 0)
+    rip = o.Fp @ _pvec(o, s, u) + st.tp - o.hp
+    return rs, ru, re, (rixu, rixl, riuu, riul, rip)
+
+
+def _comp_sum(o, st, dt=None, dl=None, a=0.0):
+    """sum over active rows of (t + a dt)(lam + a dl)."""
+    tot = 0.0
+    pairs = [(st.txu, st.lxu, o.mxu), (st.txl, st.lxl, o.mxl), (st.tuu, st.luu, o.muu),
+             (st.tul, st.lul, o.mul), (st.tp, st.lp, np.ones(o.mp, bool))]
+    for i, (t, l, msk) in enumerate(pairs):
+        if dt is None:
+            tot += (t * l)[msk].sum()
+        else:
+            tot += ((t + a * dt[i]) * (l + a * dl[i]))[msk].sum()
+    return tot
+
+
+def riccati_factor(o, st):
+    """Backward factorisation of the reduced KKT; returns per-stage (Rhat chol, K, Hs, P)."""
+    N, nx, ns, nu = o.N, o.nx, o.ns, o.nu
+    Dxu = np.where(o.mxu, st.lxu / st.txu, 0); Dxl = np.where(o.mxl, st.lxl / st.txl, 0)
+    Duu = np.where(o.muu, st.luu / st.tuu, 0); Dul = np.where(o.mul, st.lul / st.tul, 0)
+    Dp = st.lp / st.tp
+    Ht = o.H.copy()
+    for k in range(N + 1):
+        Ht[k][np.arange(nx), np.arange(nx)] += Dxu[k] + Dxl[k]
+        if k < N:
+            Ht[k][ns + np.arange(nu), ns + np.arange(nu)] += Duu[k] + Dul[k]
+    FD = o.Fp.T @ (Dp[:, None] * o.Fp)
+    if o.kp < N:
+        Ht[o.kp] += FD
+    else:
+        Ht[N][:ns, :ns] += FD
+    P = np.zeros((N + 1, ns, ns))
+    Kg = np.zeros((N, nu, ns))
+    L = np.zeros((N, nu, nu))
+    Sh = np.zeros((N, nu, ns))
+    P[N] = Ht[N][:ns, :ns]
+    A, B = o.Abar, o.Bbar
+    for k in range(N - 1, -1, -1):
+        Q = Ht[k][:ns, :ns]; S = Ht[k][ns:, :ns]; R = Ht[k][ns:, ns:]
+        PA = P[k + 1] @ A
+        PB = P[k + 1] @ B
+        Rh = R + B.T @ PB
+        Shat = S + B.T @ PA
+        Lk = np.linalg.cholesky(Rh)
+        Kk = -np.linalg.solve(Rh, Shat)
+        P[k] = Q + A.T @ PA + Shat.T @ Kk
+        P[k] = 0.5 * (P[k] + P[k].T)
+        L[k] = Lk; Kg[k] = Kk; Sh[k] = Shat
+    return dict(P=P, K=Kg, L=L, Sh=Sh, D=(Dxu, Dxl, Duu, Dul, Dp))
+
+
+def riccati_solve(o, st, fac, rs, ru, re, ri, rc):
+    """Solve the reduced Newton system for rhs (rv, re, ri, rc); returns the full step."""
+    N, nx, ns, nu = o.N, o.nx, o.ns, o.nu
+    Dxu, Dxl, Duu, Dul, Dp = fac['D']
+    rixu, rixl, riuu, riul, rip = ri
+    rcxu, rcxl, rcuu, rcul, rcp = rc
+    # q = rv + C'((lam o ri - rc)/t)
+    qs = rs.copy(); qu = ru.copy()
+    exu = np.where(o.mxu, (st.lxu * rixu - rcxu) / st.txu, 0)
+    exl = np.where(o.mxl, (st.lxl * rixl - rcxl) / st.txl, 0)
+    euu = np.where(o.muu, (st.luu * riuu - rcuu) / st.tuu, 0)
+    eul = np.where(o.mul, (st.lul * riul - rcul) / st.tul, 0)
+    ep = (st.lp * rip - rcp) / st.tp
+    qs[:, :nx] += exu - exl
+    qu += euu - eul
+    gp = o.Fp.T @ ep
+    qs[o.kp] += gp[:ns]
+    if o.kp < N:
+        qu[o.kp] += gp[ns:]
+    A, B = o.Abar, o.Bbar
+    P = fac['P']
+    p = np.zeros((N + 1, ns))
+    kff = np.zeros((N, nu))
+    p[N] = qs[N]
+    for k in range(N - 1, -1, -1):
+        Pe = P[k + 1] @ re[k] + p[k + 1]
+        rh = qu[k] + B.T @ Pe
+        kk = -np.linalg.solve(fac['L'][k] @ fac['L'][k].T, rh)
+        p[k] = qs[k] + A.T @ Pe + fac['Sh'][k].T @ kk
+        kff[k] = kk
+    ds = np.zeros((N + 1, ns)); du = np.zeros((N, nu)); dpi = np.zeros((N + 1, ns))
+    th = slice(nx, ns)
+    ds[0, th] = -np.linalg.solve(P[0][th, th], p[0][th])
+    for k in range(N):
+        du[k] = fac['K'][k] @ ds[k] + kff[k]
+        ds[k + 1] = A @ ds[k] + B @ du[k] + re[k]
+        dpi[k + 1] = P[k + 1] @ ds[k + 1] + p[k + 1]
+    # slack / multiplier steps
+    dX = ds[:, :nx]
+    dpv = np.concatenate([ds[o.kp], du[o.kp]]) if o.kp < N else ds[N]
+    dt = [np.where(o.mxu, -rixu - dX, 0), np.where(o.mxl, -rixl + dX, 0),
+          np.where(o.muu, -riuu - du, 0), np.where(o.mul, -riul + du, 0),
+          -rip - o.Fp @ dpv]
+    ts = [st.txu, st.txl, st.tuu, st.tul, st.tp]
+    ls = [st.lxu, st.lxl, st.luu, st.lul, st.lp]
+    rcs = [rcxu, rcxl, rcuu, rcul, rcp]
+    msk = [o.mxu, o.mxl, o.muu, o.mul, np.ones(o.mp, bool)]
+    dl = [np.where(mk, (-rcq - l * d) / t, 0) for t, l, d, rcq, mk in zip(ts, ls, dt, rcs, msk)]
+    return ds, du, dpi, dt, dl
+
+
+def _max_step(st, o, dt, dl):
+    a = 1.0
+    ts = [st.txu, st.txl, st.tuu, st.tul, st.tp]
+    ls = [st.lxu, st.lxl, st.luu, st.lul, st.lp]
+    msk = [o.mxu, o.mxl, o.muu, o.mul, np.ones(o.mp, bool)]
+    for v, dv, mk in list(zip(ts, dt, msk)) + list(zip(ls, dl, msk)):
+        neg = mk & (dv < 0)
+        if neg.any():
+            a = min(a, (-v[neg] / dv[neg]).min())
+    return a
+
+
+def _apply(st, o, a, ds, du, dpi, dt, dl):
+    st.s += a * ds; st.u += a * du; st.pi += a * dpi
+    for name, d in zip(('txu', 'txl', 'tuu', 'tul', 'tp'), dt):
+        setattr(st, name, getattr(st, name) + a * d)
+    for name, d in zip(('lxu', 'lxl', 'luu', 'lul', 'lp'), dl):
+        setattr(st, name, getattr(st, name) + a * d)
+
+
+def initialize(o, st):
+    """Unit-scaled least-squares start (CVXOPT coneqp style) + positivity shift."""
+    rs, ru, re, ri = residuals(o, st)
+    fac = riccati_factor(o, st)                       # t = lam = 1 -> D = 1
+    rc = [st.txu * st.lxu, st.txl * st.lxl, st.tuu * st.luu, st.tul * st.lul, st.tp * st.lp]
+    ds, du, dpi, dt, dl = riccati_solve(o, st, fac, rs, ru, re, ri, rc)
+    st.s += ds; st.u += du; st.pi += dpi
+    # tt = b - C v  (primal slack of the LS point), lam~ = -tt
+    X = st.s[:, :nx_(o)]
+    tt = [np.where(o.mxu, o.xub - X, 1.0), np.where(o.mxl, X - o.xlb, 1.0),
+          np.where(o.muu, o.uub - st.u, 1.0), np.where(o.mul, st.u - o.ulb, 1.0),
+          o.hp - o.Fp @ _pvec(o, st.s, st.u)]
+    msk = [o.mxu, o.mxl, o.muu, o.mul, np.ones(o.mp, bool)]
+    tmin = min(t[m_].min(initial=INF) for t, m_ in zip(tt, msk))
+    tmax = max(t[m_].max(initial=-INF) for t, m_ in zip(tt, msk))
+    shp = (1.0 - tmin) if tmin <= 0 else 0.0          # make min t >= 1 if infeasible
+    shd = 1.0 + tmax if tmax >= 0 else 0.0            # lam~ = -tt; shift so min lam >= 1
+    names_t = ('txu', 'txl', 'tuu', 'tul', 'tp'); names_l = ('lxu', 'lxl', 'luu', 'lul', 'lp')
+    for nt, nl, t, mk in zip(names_t, names_l, tt, msk):
+        setattr(st, nt, np.where(mk, t + shp, 1.0))
+        setattr(st, nl, np.where(mk, -t + shd, 0.0))
+
+
+def nx_(o):
+    return o.nx
+
+
+DEFAULTS = dict(max_iter=50, tol_stat=1e-10, tol_feas=1e-10, tol_comp=1e-10, tau=0.995)
+
+
+def solve(d, x0, w=None, opts=None, trace=None):
+    """Returns dict(x, u, theta, iterations, exitflag, ...)."""
+    op = dict(DEFAULTS, **(opts or {}))
+    o = OCP(d, x0, w)
+    st = State(o)
+    initialize(o, st)
+    m = max(o.m, 1)
+    exitflag = 0
+    it = 0
+    for it in range(op['max_iter'] + 1):
+        rs, ru, re, ri = residuals(o, st)
+        mu = _comp_sum(o, st) / m
+        r_stat = max(np.abs(rs).max(initial=0), np.abs(ru).max(initial=0))
+        r_feas = max(np.abs(re).max(initial=0), max(np.abs(r).max(initial=0) for r in ri))
+        if trace is not None:
+            trace.append(dict(it=it, mu=mu, r_stat=r_stat, r_feas=r_feas,
+                              s=st.s.copy(), u=st.u.copy()))
+        if r_stat <= op['tol_stat'] and r_feas <= op['tol_feas'] and mu <= op['tol_comp']:
+            exitflag = 1
+            break
+        if it == op['max_iter']:
+            break
+        fac = riccati_factor(o, st)
+        rc = [st.txu * st.lxu, st.txl * st.lxl, st.tuu * st.luu, st.tul * st.lul, st.tp * st.lp]
+        ds, du, dpi, dt, dl = riccati_solve(o, st, fac, rs, ru, re, ri, rc)
+        a = _max_step(st, o, dt, dl)
+        mua = _comp_sum(o, st, dt, dl, a) / m
+        sig = (mua / mu) ** 3
+        rc = [t * l + dta * dla - sig * mu
+              for t, l, dta, dla in zip([st.txu, st.txl, st.tuu, st.tul, st.tp],
+                                         [st.lxu, st.lxl, st.luu, st.lul, st.lp], dt, dl)]
+        ds, du, dpi, dt, dl = riccati_solve(o, st, fac, rs, ru, re, ri, rc)
+        a = min(1.0, op['tau'] * _max_step(st, o, dt, dl))
+        _apply(st, o, a, ds, du, dpi, dt, dl)
+    nx = o.nx
+    return dict(x=st.s[:, :nx].copy(), u=st.u.copy(), theta=st.s[0, nx:].copy(),
+                iterations=it, exitflag=exitflag, pi=st.pi.copy(),
+                lam=dict(xu=st.lxu, xl=st.lxl, uu=st.luu, ul=st.lul, p=st.lp), mu=mu)

@@ -47,9 +47,9 @@ typedef struct bqp_handle_s* bqp_handle;
 
 typedef struct {
     int max_iter;      /* default 50 */
-    double tol_stat;   /* stationarity inf-norm (absolute), default 1e-10 */
-    double tol_feas;   /* primal residual inf-norm (absolute), default 1e-10 */
-    double tol_comp;   /* average complementarity mu, default 1e-12 */
+    double tol_stat;   /* stationarity inf-norm / (1 + |cost gradient|_inf), default 1e-8 */
+    double tol_feas;   /* primal residual inf-norm / (1 + |bounds, rhs|_inf), default 1e-10 */
+    double tol_comp;   /* average complementarity mu (absolute), default 1e-14 */
     double tau;        /* fraction-to-boundary, default 0.995 */
     int precision;     /* 0 = fp64 (default) */
     int want_duals;    /* 1: fill the multiplier outputs (structured API) */

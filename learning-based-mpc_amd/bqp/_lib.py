@@ -1,0 +1,157 @@
+"""ctypes binding of libbqp.so (include/bqp.h).  The HIP library is mandatory: importing the
+solver on a machine without the built library raises, there is no CPU fallback."""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libbqp.so')
+
+BQP_OK = 0
+BQP_E_ARG = -1
+BQP_E_HIP = -2
+BQP_E_NODEV = -3
+BQP_E_UNSUPPORTED = -4
+_ERR = {BQP_E_ARG: 'invalid argument', BQP_E_HIP: 'HIP runtime error',
+        BQP_E_NODEV: 'no usable gfx950 device', BQP_E_UNSUPPORTED: 'unsupported dimensions'}
+
+_PD = C.POINTER(C.c_double)
+_PI = C.POINTER(C.c_int)
+
+
+class Options(C.Structure):
+    _fields_ = [('max_iter', C.c_int), ('tol_stat', C.c_double), ('tol_feas', C.c_double),
+                ('tol_comp', C.c_double), ('tau', C.c_double), ('precision', C.c_int),
+                ('want_duals', C.c_int)]
+
+
+class Output(C.Structure):
+    _fields_ = [('iterations', C.c_int), ('constrviolation', C.c_double),
+                ('firstorderopt', C.c_double), ('mu', C.c_double), ('kkt', C.c_double * 4)]
+
+
+class OcpDims(C.Structure):
+    _fields_ = [('nx', C.c_int), ('nu', C.c_int), ('np', C.c_int), ('N', C.c_int),
+                ('n_poly', C.c_int), ('poly_stage', C.c_int)]
+
+
+class OcpData(C.Structure):
+    _fields_ = [(n, _PD) for n in ('A', 'B', 'c', 'W', 'w', 'xlb', 'xub', 'ulb', 'uub', 'Fp', 'hp', 'x0')] + \
+               [(n, C.c_int64) for n in ('sA', 'sB', 'sc', 'sW', 'sw', 'sxb', 'sub', 'sFp', 'shp', 'sx0')]
+
+
+class OcpDuals(C.Structure):
+    _fields_ = [('pi', _PD), ('lam_x', _PD), ('lam_u', _PD), ('lam_p', _PD)]
+
+
+class Dims(C.Structure):
+    _fields_ = [('n', C.c_int), ('m', C.c_int), ('me', C.c_int)]
+
+
+class Strides(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ('sH', 'sf', 'sA', 'sb', 'sAeq', 'sbeq', 'slb', 'sub')]
+
+
+EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version',
+           'bqp_solve_ocp_batched', 'bqp_solve_ocp_batched_device', 'bqp_quadprog_batched',
+           'bqp_quadprog_batched_device', 'bqp_last_kernel_ms']
+
+_lib = None
+
+
+class BqpError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libbqp.so; raises BqpError (loudly) if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BqpError('libbqp.so not built (%s); run `make -C learning-based-mpc_amd` or '
+                       '__graft_entry__.build()' % LIB_PATH)
+    lib = C.CDLL(LIB_PATH)
+    lib.bqp_version.restype = C.c_char_p
+    lib.bqp_create.argtypes = [C.POINTER(C.c_void_p), C.c_int]
+    lib.bqp_destroy.argtypes = [C.c_void_p]
+    lib.bqp_default_options.argtypes = [C.POINTER(Options)]
+    lib.bqp_default_options.restype = None
+    lib.bqp_solve_ocp_batched.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int,
+                                          C.POINTER(OcpData), C.POINTER(Options), _PD, _PD,
+                                          _PD, _PD, _PI, C.POINTER(Output), C.POINTER(OcpDuals)]
+    lib.bqp_solve_ocp_batched_device.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int,
+                                                 C.POINTER(OcpData), C.POINTER(Options), _PD,
+                                                 _PD, _PD, _PD, _PI, C.c_void_p,
+                                                 C.POINTER(OcpDuals), C.c_void_p]
+    lib.bqp_quadprog_batched.argtypes = [C.c_void_p, C.POINTER(Dims), C.c_int, C.POINTER(Strides)] + \
+        [_PD] * 9 + [C.POINTER(Options), _PD, _PD, _PI, _PD, _PD, _PD, _PD, C.POINTER(Output)]
+    lib.bqp_quadprog_batched_device.argtypes = [C.c_void_p, C.POINTER(Dims), C.c_int, C.POINTER(Strides)] + \
+        [_PD] * 8 + [C.POINTER(Options), _PD, _PD, _PI, _PD, _PD, _PD, _PD, C.c_void_p, C.c_void_p]
+    lib.bqp_last_kernel_ms.argtypes = [C.c_void_p, _PD, _PI]
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != BQP_OK:
+        raise BqpError('%s failed: %s (%d)' % (what, _ERR.get(rc, 'error'), rc))
+
+
+def ptr(a):
+    import numpy as np
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags['C_CONTIGUOUS']
+    return a.ctypes.data_as(_PD)
+
+
+def iptr(a):
+    return None if a is None else a.ctypes.data_as(_PI)
+
+
+def dptr(t):
+    """Device pointer of a torch tensor (float64)."""
+    if t is None:
+        return None
+    return C.cast(C.c_void_p(t.data_ptr()), _PD)
+
+
+class Handle:
+    """Owns a bqp_handle (one per host thread / stream)."""
+
+    def __init__(self, device=-1):
+        lib = load()
+        h = C.c_void_p()
+        check(lib.bqp_create(C.byref(h), C.c_int(device)), 'bqp_create')
+        self._h = h
+        self._lib = lib
+
+    @property
+    def value(self):
+        return self._h
+
+    def kernel_ms(self):
+        ms = C.c_double(0.0)
+        n = C.c_int(0)
+        check(self._lib.bqp_last_kernel_ms(self._h, C.byref(ms), C.byref(n)), 'bqp_last_kernel_ms')
+        return ms.value, n.value
+
+    def close(self):
+        if self._h:
+            self._lib.bqp_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def options(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995,
+            want_duals=0):
+    o = Options()
+    load().bqp_default_options(C.byref(o))
+    o.max_iter, o.tol_stat, o.tol_feas, o.tol_comp, o.tau = max_iter, tol_stat, tol_feas, tol_comp, tau
+    o.want_duals = want_duals
+    return o

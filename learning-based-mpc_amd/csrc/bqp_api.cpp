@@ -1,0 +1,429 @@
+// bqp_api.cpp — implementation of the C ABI declared in include/bqp.h.
+//
+// Host-side responsibilities only: argument validation, workspace management (grow-only device
+// buffers owned by the handle), host<->device staging for the host-pointer entry points, and
+// dispatch of the HIP kernels (bqp_ocp.hip, bqp_dense.hip, bqp_prep.hip).  No arithmetic of
+// the solve happens on the host: there is no CPU fallback path.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/bqp.h"
+#include "bqp_internal.h"
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct bqp_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    int launches = 0;
+    DevBuf work;   // tables + stats (device entry points)
+    DevBuf stage;  // staging of host-pointer calls
+    DevBuf dwork;  // dense per-instance scratch
+};
+
+namespace {
+
+struct DevScope {
+    int prev = -1;
+    explicit DevScope(int d) {
+        hipGetDevice(&prev);
+        if (prev != d) hipSetDevice(d);
+    }
+    ~DevScope() {
+        int cur = -1;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+inline size_t span(int batch, int64_t stride, size_t n) {
+    return n == 0 ? 0 : (size_t)(batch - 1) * (size_t)stride + n;
+}
+
+void resolve(const bqp_options* in, bqp_options* o) {
+    bqp_default_options(o);
+    if (!in) return;
+    if (in->max_iter > 0) o->max_iter = in->max_iter;
+    if (in->tol_stat > 0) o->tol_stat = in->tol_stat;
+    if (in->tol_feas > 0) o->tol_feas = in->tol_feas;
+    if (in->tol_comp > 0) o->tol_comp = in->tol_comp;
+    if (in->tau > 0 && in->tau < 1) o->tau = in->tau;
+    o->precision = in->precision;
+    o->want_duals = in->want_duals;
+}
+
+#define HIP_TRY(x)                                                        \
+    do {                                                                  \
+        hipError_t _e = (x);                                              \
+        if (_e != hipSuccess) {                                           \
+            fprintf(stderr, "bqp: %s failed: %s\n", #x, hipGetErrorString(_e)); \
+            return BQP_E_HIP;                                             \
+        }                                                                 \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+const char* bqp_version(void) { return "bqp 0.1.0 (gfx950, structured Riccati Mehrotra IPM)"; }
+
+void bqp_default_options(bqp_options* o) {
+    if (!o) return;
+    o->max_iter = 50;
+    o->tol_stat = 1e-8;
+    o->tol_feas = 1e-10;
+    o->tol_comp = 1e-14;
+    o->tau = 0.995;
+    o->precision = 0;
+    o->want_duals = 0;
+}
+
+int bqp_create(bqp_handle* h, int device) {
+    if (!h) return BQP_E_ARG;
+    *h = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return BQP_E_NODEV;
+    int dev = device;
+    if (dev < 0) hipGetDevice(&dev);
+    if (dev >= n) return BQP_E_ARG;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return BQP_E_NODEV;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fprintf(stderr, "bqp: device %d is %s; this build targets gfx950 only\n", dev, prop.gcnArchName);
+        return BQP_E_NODEV;
+    }
+    bqp_handle_s* s = new bqp_handle_s();
+    s->device = dev;
+    DevScope ds(dev);
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
+        delete s;
+        return BQP_E_HIP;
+    }
+    *h = s;
+    return BQP_OK;
+}
+
+int bqp_destroy(bqp_handle h) {
+    if (!h) return BQP_OK;
+    {
+        DevScope ds(h->device);
+        if (h->stream) hipStreamSynchronize(h->stream);
+        h->work.release();
+        h->stage.release();
+        h->dwork.release();
+        if (h->ev0) hipEventDestroy(h->ev0);
+        if (h->ev1) hipEventDestroy(h->ev1);
+        if (h->stream) hipStreamDestroy(h->stream);
+    }
+    delete h;
+    return BQP_OK;
+}
+
+int bqp_last_kernel_ms(bqp_handle h, double* ms, int* launches) {
+    if (!h || !ms) return BQP_E_ARG;
+    *ms = 0.0;
+    if (launches) *launches = h->launches;
+    if (!h->timed) return BQP_OK;
+    DevScope ds(h->device);
+    HIP_TRY(hipEventSynchronize(h->ev1));
+    float f = 0.f;
+    HIP_TRY(hipEventElapsedTime(&f, h->ev0, h->ev1));
+    *ms = (double)f;
+    return BQP_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// structured OCP
+// ------------------------------------------------------------------------------------------
+static int ocp_check(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D) {
+    if (!d || !D || batch <= 0) return BQP_E_ARG;
+    if (d->nx <= 0 || d->nu <= 0 || d->np <= 0 || d->N < 1 || d->n_poly < 0) return BQP_E_ARG;
+    if (d->poly_stage < 0 || d->poly_stage > d->N) return BQP_E_ARG;
+    if (!D->A || !D->B || !D->W || !D->x0) return BQP_E_ARG;
+    if (d->n_poly > 0 && (!D->Fp || !D->hp)) return BQP_E_ARG;
+    if (!bqp::ocp_supported(d->nx, d->nu, d->np)) return BQP_E_UNSUPPORTED;
+    if (d->N > 127 || bqp::ocp_rpl_for(std::max(d->n_poly, 1)) < 0) return BQP_E_UNSUPPORTED;
+    if (D->sW != 0 || D->sFp != 0) return BQP_E_UNSUPPORTED;  // shared stage costs / polytope
+    return BQP_OK;
+}
+
+int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
+                                 const bqp_ocp_data* D, const bqp_options* opt, double* x,
+                                 double* u, double* theta, double* fval, int* exitflag,
+                                 bqp_output* out, const bqp_ocp_duals* duals, void* stream) {
+    if (!h) return BQP_E_ARG;
+    int rc = ocp_check(d, batch, D);
+    if (rc) return rc;
+    if (!x || !u || !theta || !exitflag) return BQP_E_ARG;
+    DevScope ds(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    bqp_options o;
+    resolve(opt, &o);
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
+    const int nv = nx + nu + np;
+    const int mp = d->n_poly;
+    const int hstride = nv * nv + 1;
+    const int mpad = std::max(64, ((mp + 63) / 64) * 64);
+    const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;
+    const int per_wave = bqp::ocp_wave_lds_doubles(N, nx, nu, np);
+    const size_t lds_budget = 160 * 1024 / sizeof(double);
+    int wpb = 4;
+    while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
+    if ((size_t)shared_doubles + (size_t)per_wave > lds_budget) return BQP_E_UNSUPPORTED;
+    // workspace: H, Fp, stats
+    const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * 4;
+    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8)));
+    double* Hd = (double*)h->work.p;
+    double* Fd = Hd + nH;
+    double* Sd = Fd + nF;
+    static const double zero = 0.0;
+    (void)zero;
+    HIP_TRY(bqp::launch_ocp_prep(D->W, mp > 0 ? D->Fp : D->W, nx, nu, np, N, mp, d->poly_stage,
+                                 hstride, mpad, Hd, Fd, st));
+    bqp::OcpKernelArgs a;
+    memset(&a, 0, sizeof(a));
+    a.N = N; a.mp = mp; a.kp = d->poly_stage; a.batch = batch; a.wpb = wpb;
+    a.hstride = hstride; a.mpad = mpad; a.shared_doubles = shared_doubles;
+    a.max_iter = o.max_iter; a.tol_stat = o.tol_stat; a.tol_feas = o.tol_feas;
+    a.tol_comp = o.tol_comp; a.tau = o.tau;
+    a.H = Hd; a.Fp = Fd;
+    a.A = D->A; a.B = D->B; a.c = D->c; a.w = D->w; a.xlb = D->xlb; a.xub = D->xub;
+    a.ulb = D->ulb; a.uub = D->uub; a.hp = mp > 0 ? D->hp : Hd; a.x0 = D->x0;
+    a.sA = D->sA; a.sB = D->sB; a.sc = D->sc; a.sw = D->sw; a.sxb = D->sxb; a.sub = D->sub;
+    a.shp = D->shp; a.sx0 = D->sx0;
+    a.x = x; a.u = u; a.theta = theta; a.fval = fval; a.exitflag = exitflag; a.stats = Sd;
+    if (duals) {
+        a.pi_out = duals->pi; a.lamx_out = duals->lam_x; a.lamu_out = duals->lam_u;
+        a.lamp_out = duals->lam_p;
+    }
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->timed = true;
+    h->launches = 1;
+    if (out) HIP_TRY(bqp::launch_ocp_finalize(Sd, batch, out, st));
+    return BQP_OK;
+}
+
+int bqp_solve_ocp_batched(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
+                          const bqp_options* opt, double* x, double* u, double* theta,
+                          double* fval, int* exitflag, bqp_output* out,
+                          const bqp_ocp_duals* duals) {
+    if (!h) return BQP_E_ARG;
+    int rc = ocp_check(d, batch, D);
+    if (rc) return rc;
+    if (!x || !u || !theta || !exitflag) return BQP_E_ARG;
+    DevScope ds(h->device);
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N, mp = d->n_poly;
+    const size_t nv = nx + nu + np;
+    // input spans (elements)
+    struct In { const double* src; size_t n; double* dst; };
+    In in[12] = {
+        {D->A, span(batch, D->sA, nx * nx), nullptr},
+        {D->B, span(batch, D->sB, nx * nu), nullptr},
+        {D->c, D->c ? span(batch, D->sc, nx) : 0, nullptr},
+        {D->W, span(batch, D->sW, (N + 1) * nv * nv), nullptr},
+        {D->w, D->w ? span(batch, D->sw, (N + 1) * nv) : 0, nullptr},
+        {D->xlb, D->xlb ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},
+        {D->xub, D->xub ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},
+        {D->ulb, D->ulb ? span(batch, D->sub, (size_t)N * nu) : 0, nullptr},
+        {D->uub, D->uub ? span(batch, D->sub, (size_t)N * nu) : 0, nullptr},
+        {D->Fp, mp > 0 ? span(batch, D->sFp, (size_t)mp * nv) : 0, nullptr},
+        {D->hp, mp > 0 ? span(batch, D->shp, (size_t)mp) : 0, nullptr},
+        {D->x0, span(batch, D->sx0, nx), nullptr},
+    };
+    const size_t nxo = (size_t)batch * (N + 1) * nx, nuo = (size_t)batch * N * nu,
+                 nto = (size_t)batch * np, nfo = (size_t)batch;
+    size_t ndual = 0;
+    if (duals) ndual = (size_t)batch * ((size_t)N * nx + (size_t)(N + 1) * nx * 2 + (size_t)N * nu * 2 + mp);
+    size_t total = 0;
+    for (auto& e : in) total += e.n;
+    total += nxo + nuo + nto + nfo + ndual;
+    const size_t outbytes = sizeof(bqp_output) * (size_t)batch;
+    const size_t bytes = sizeof(double) * (total + 16) + sizeof(int) * (size_t)batch + outbytes + 64;
+    HIP_TRY(h->stage.reserve(bytes));
+    double* cur = (double*)h->stage.p;
+    for (auto& e : in) {
+        if (e.n) {
+            e.dst = cur;
+            HIP_TRY(hipMemcpyAsync(cur, e.src, sizeof(double) * e.n, hipMemcpyHostToDevice, h->stream));
+            cur += e.n;
+        }
+    }
+    double* xd = cur; cur += nxo;
+    double* ud = cur; cur += nuo;
+    double* td = cur; cur += nto;
+    double* fd = cur; cur += nfo;
+    double* dual_base = cur; cur += ndual;
+    int* ed = (int*)cur;
+    bqp_output* od = (bqp_output*)(((uintptr_t)(ed + batch) + 63) & ~(uintptr_t)63);
+    bqp_ocp_data Dd = *D;
+    Dd.A = in[0].dst; Dd.B = in[1].dst; Dd.c = in[2].dst; Dd.W = in[3].dst; Dd.w = in[4].dst;
+    Dd.xlb = in[5].dst; Dd.xub = in[6].dst; Dd.ulb = in[7].dst; Dd.uub = in[8].dst;
+    Dd.Fp = in[9].dst; Dd.hp = in[10].dst; Dd.x0 = in[11].dst;
+    bqp_ocp_duals dd;
+    memset(&dd, 0, sizeof(dd));
+    if (duals) {
+        double* q = dual_base;
+        dd.pi = q; q += (size_t)batch * N * nx;
+        dd.lam_x = q; q += (size_t)batch * (N + 1) * nx * 2;
+        dd.lam_u = q; q += (size_t)batch * N * nu * 2;
+        dd.lam_p = q;
+    }
+    rc = bqp_solve_ocp_batched_device(h, d, batch, &Dd, opt, xd, ud, td, fd, ed,
+                                      out ? od : nullptr, duals ? &dd : nullptr, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(x, xd, sizeof(double) * nxo, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(u, ud, sizeof(double) * nuo, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(theta, td, sizeof(double) * nto, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(exitflag, ed, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    if (fval) HIP_TRY(hipMemcpyAsync(fval, fd, sizeof(double) * nfo, hipMemcpyDeviceToHost, h->stream));
+    if (out) HIP_TRY(hipMemcpyAsync(out, od, outbytes, hipMemcpyDeviceToHost, h->stream));
+    if (duals) {
+        if (duals->pi) HIP_TRY(hipMemcpyAsync(duals->pi, dd.pi, sizeof(double) * batch * N * nx, hipMemcpyDeviceToHost, h->stream));
+        if (duals->lam_x) HIP_TRY(hipMemcpyAsync(duals->lam_x, dd.lam_x, sizeof(double) * batch * (N + 1) * nx * 2, hipMemcpyDeviceToHost, h->stream));
+        if (duals->lam_u) HIP_TRY(hipMemcpyAsync(duals->lam_u, dd.lam_u, sizeof(double) * batch * N * nu * 2, hipMemcpyDeviceToHost, h->stream));
+        if (duals->lam_p && mp > 0) HIP_TRY(hipMemcpyAsync(duals->lam_p, dd.lam_p, sizeof(double) * batch * mp, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return BQP_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// dense quadprog
+// ------------------------------------------------------------------------------------------
+static int dense_check(const bqp_dims* d, int batch, const double* H, const double* f) {
+    if (!d || batch <= 0 || !H || !f) return BQP_E_ARG;
+    if (d->n <= 0 || d->m < 0 || d->me < 0) return BQP_E_ARG;
+    if (d->n > 256 || d->me > 256 || d->m > 8192) return BQP_E_UNSUPPORTED;
+    return BQP_OK;
+}
+
+int bqp_quadprog_batched_device(bqp_handle h, const bqp_dims* d, int batch, const bqp_strides* s,
+                                const double* H, const double* f, const double* A,
+                                const double* b, const double* Aeq, const double* beq,
+                                const double* lb, const double* ub, const bqp_options* opt,
+                                double* x, double* fval, int* exitflag, double* lam_ineqlin,
+                                double* lam_eqlin, double* lam_lower, double* lam_upper,
+                                bqp_output* out, void* stream) {
+    if (!h) return BQP_E_ARG;
+    int rc = dense_check(d, batch, H, f);
+    if (rc) return rc;
+    if (!x || !exitflag || !s) return BQP_E_ARG;
+    if ((d->m > 0 && (!A || !b)) || (d->me > 0 && (!Aeq || !beq))) return BQP_E_ARG;
+    DevScope ds(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    bqp_options o;
+    resolve(opt, &o);
+    const int64_t wst = bqp::dense_work_doubles(d->n, d->m, d->me);
+    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * batch + (size_t)batch * 4 + 8)));
+    double* wk = (double*)h->dwork.p;
+    double* Sd = wk + (size_t)wst * batch;
+    bqp::DenseKernelArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = d->n; a.m = d->m; a.me = d->me; a.batch = batch; a.max_iter = o.max_iter;
+    a.tol_stat = o.tol_stat; a.tol_feas = o.tol_feas; a.tol_comp = o.tol_comp; a.tau = o.tau;
+    a.H = H; a.f = f; a.A = A; a.b = b; a.Aeq = Aeq; a.beq = beq; a.lb = lb; a.ub = ub;
+    a.sH = s->sH; a.sf = s->sf; a.sA = s->sA; a.sb = s->sb; a.sAeq = s->sAeq; a.sbeq = s->sbeq;
+    a.slb = s->slb; a.sub = s->sub;
+    a.x = x; a.fval = fval; a.lam_ineqlin = lam_ineqlin; a.lam_eqlin = lam_eqlin;
+    a.lam_lower = lam_lower; a.lam_upper = lam_upper; a.exitflag = exitflag; a.stats = Sd;
+    a.work = wk; a.work_stride = wst;
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    HIP_TRY(bqp::launch_dense(a, st));
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->timed = true;
+    h->launches = 1;
+    if (out) HIP_TRY(bqp::launch_ocp_finalize(Sd, batch, out, st));
+    return BQP_OK;
+}
+
+int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_strides* s,
+                         const double* H, const double* f, const double* A, const double* b,
+                         const double* Aeq, const double* beq, const double* lb, const double* ub,
+                         const double* x0, const bqp_options* opt, double* x, double* fval,
+                         int* exitflag, double* lam_ineqlin, double* lam_eqlin,
+                         double* lam_lower, double* lam_upper, bqp_output* out) {
+    (void)x0;
+    if (!h) return BQP_E_ARG;
+    int rc = dense_check(d, batch, H, f);
+    if (rc) return rc;
+    if (!x || !exitflag) return BQP_E_ARG;
+    bqp_strides zs;
+    memset(&zs, 0, sizeof(zs));
+    if (!s) s = &zs;
+    DevScope ds(h->device);
+    const size_t n = d->n, m = d->m, me = d->me;
+    struct In { const double* src; size_t n; double* dst; };
+    In in[8] = {
+        {H, span(batch, s->sH, n * n), nullptr},
+        {f, span(batch, s->sf, n), nullptr},
+        {A, (A && m) ? span(batch, s->sA, m * n) : 0, nullptr},
+        {b, (b && m) ? span(batch, s->sb, m) : 0, nullptr},
+        {Aeq, (Aeq && me) ? span(batch, s->sAeq, me * n) : 0, nullptr},
+        {beq, (beq && me) ? span(batch, s->sbeq, me) : 0, nullptr},
+        {lb, lb ? span(batch, s->slb, n) : 0, nullptr},
+        {ub, ub ? span(batch, s->sub, n) : 0, nullptr},
+    };
+    size_t total = 0;
+    for (auto& e : in) total += e.n;
+    const size_t nxo = (size_t)batch * n, nli = (size_t)batch * m, nle = (size_t)batch * me;
+    total += nxo + batch + nli + nle + 2 * nxo;
+    const size_t outbytes = sizeof(bqp_output) * (size_t)batch;
+    HIP_TRY(h->stage.reserve(sizeof(double) * (total + 16) + sizeof(int) * batch + outbytes + 64));
+    double* cur = (double*)h->stage.p;
+    for (auto& e : in)
+        if (e.n) {
+            e.dst = cur;
+            HIP_TRY(hipMemcpyAsync(cur, e.src, sizeof(double) * e.n, hipMemcpyHostToDevice, h->stream));
+            cur += e.n;
+        }
+    double* xd = cur; cur += nxo;
+    double* fd = cur; cur += batch;
+    double* lid = cur; cur += nli;
+    double* led = cur; cur += nle;
+    double* lld = cur; cur += nxo;
+    double* lud = cur; cur += nxo;
+    int* ed = (int*)cur;
+    bqp_output* od = (bqp_output*)(((uintptr_t)(ed + batch) + 63) & ~(uintptr_t)63);
+    rc = bqp_quadprog_batched_device(h, d, batch, s, in[0].dst, in[1].dst, in[2].dst, in[3].dst,
+                                     in[4].dst, in[5].dst, in[6].dst, in[7].dst, opt, xd, fd, ed,
+                                     lid, led, lld, lud, out ? od : nullptr, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(x, xd, sizeof(double) * nxo, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(exitflag, ed, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    if (fval) HIP_TRY(hipMemcpyAsync(fval, fd, sizeof(double) * batch, hipMemcpyDeviceToHost, h->stream));
+    if (lam_ineqlin && m) HIP_TRY(hipMemcpyAsync(lam_ineqlin, lid, sizeof(double) * nli, hipMemcpyDeviceToHost, h->stream));
+    if (lam_eqlin && me) HIP_TRY(hipMemcpyAsync(lam_eqlin, led, sizeof(double) * nle, hipMemcpyDeviceToHost, h->stream));
+    if (lam_lower) HIP_TRY(hipMemcpyAsync(lam_lower, lld, sizeof(double) * nxo, hipMemcpyDeviceToHost, h->stream));
+    if (lam_upper) HIP_TRY(hipMemcpyAsync(lam_upper, lud, sizeof(double) * nxo, hipMemcpyDeviceToHost, h->stream));
+    if (out) HIP_TRY(hipMemcpyAsync(out, od, outbytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return BQP_OK;
+}
+
+}  // extern "C"

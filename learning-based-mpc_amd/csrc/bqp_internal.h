@@ -1,0 +1,51 @@
+// bqp_internal.h — kernel argument blocks and launch helpers shared by the HIP kernels and the
+// C-ABI implementation (bqp_api.cpp).  Not part of the public ABI (include/bqp.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bqp {
+
+// Structured OCP kernel arguments (device pointers).  H and Fp are the prepared shared tables:
+//   H  : (N+1) stages x hstride doubles, stage cost in internal order [x; theta; u], row-major
+//   Fp : column-major [NV][mpad] polytope matrix in internal order
+// All other arrays are in the public (external) layout with per-instance element strides.
+struct OcpKernelArgs {
+    int N, mp, kp, batch, wpb, hstride, mpad, shared_doubles, max_iter;
+    double tol_stat, tol_feas, tol_comp, tau;
+    const double* H;
+    const double* Fp;
+    const double *A, *B, *c, *w, *xlb, *xub, *ulb, *uub, *hp, *x0;
+    int64_t sA, sB, sc, sw, sxb, sub, shp, sx0;
+    double *x, *u, *theta, *fval;
+    int* exitflag;
+    double* stats;  // batch x 4: iterations, stationarity, feasibility, mu
+    double *pi_out, *lamx_out, *lamu_out, *lamp_out;
+};
+
+bool ocp_supported(int nx, int nu, int np);
+int ocp_rpl_for(int mp);
+int ocp_wave_lds_doubles(int N, int nx, int nu, int np);
+hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
+hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
+                           int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,
+                           hipStream_t st);
+hipError_t launch_ocp_finalize(const double* stats, int batch, void* out, hipStream_t st);
+
+// Dense quadprog kernel arguments.
+struct DenseKernelArgs {
+    int n, m, me, batch, max_iter, mrows;  // mrows = m + finite bound rows (set per instance)
+    double tol_stat, tol_feas, tol_comp, tau;
+    const double *H, *f, *A, *b, *Aeq, *beq, *lb, *ub;
+    int64_t sH, sf, sA, sb, sAeq, sbeq, slb, sub;
+    double *x, *fval, *lam_ineqlin, *lam_eqlin, *lam_lower, *lam_upper;
+    int* exitflag;
+    double* stats;
+    double* work;      // per-instance scratch (global), work_stride doubles each
+    int64_t work_stride;
+};
+
+int dense_work_doubles(int n, int m, int me);
+hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st);
+
+}  // namespace bqp

@@ -88,9 +88,9 @@ static int chol_inv(int n, const double* M, double* Minv) {
 
 /* ---------------- residuals ---------------- */
 static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, double* musum,
-                      int* mcount) {
+                      int* mcount, double* gscale) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv;
-    double st = 0, fe = 0, cs = 0;
+    double st = 0, fe = 0, cs = 0, gs = 0;
     int mc = 0;
     for (int k = 0; k <= N; ++k) {
         const double* H = P->H + (size_t)k * nv * nv;
@@ -103,6 +103,7 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
             double a = W->g[k * nv + i];
             for (int j = 0; j < nvk; ++j) a += H[i * nv + j] * v[j];
             gv[i] = a;
+            gs = fmax(gs, fabs(a));
         }
         for (int i = 0; i < ns; ++i) {
             double a = gv[i];
@@ -193,7 +194,7 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < 2 * nu; ++i) fe = fmax(fe, fabs(W->riu[k * nu * 2 + i]));
     for (int r = 0; r < P->mp; ++r) fe = fmax(fe, fabs(W->rip[r]));
-    *stat = st; *feas = fe; *musum = cs; *mcount = mc;
+    *stat = st; *feas = fe; *musum = cs; *mcount = mc; *gscale = gs;
 }
 
 /* ---------------- factorisation ---------------- */
@@ -237,42 +238,58 @@ static int factor(const prob_t* P, work_t* W) {
         for (int j = 0; j < ns; ++j) PN[i * ns + j] = HT(N, i, j);
     for (int k = N - 1; k >= 0; --k) {
         const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
-        /* F = [Abar Bbar] (ns x nv); M = Ht + F' Pn F */
+        /* input rows of M = Ht + F' Pn F, F = [Abar Bbar]:  Rhat = M_uu, Shat = M_us */
         double F[MAXNS][MAXNV];
         for (int a = 0; a < ns; ++a) {
             for (int j = 0; j < ns; ++j) F[a][j] = P->Abar[a][j];
             for (int j = 0; j < nu; ++j) F[a][ns + j] = P->Bbar[a][j];
         }
-        double PF[MAXNS][MAXNV], M[MAXNV][MAXNV];
-        for (int a = 0; a < ns; ++a)
+        double Mu[MAXNU][MAXNV];
+        for (int x = 0; x < nu; ++x)
             for (int j = 0; j < nv; ++j) {
-                double v = 0;
-                for (int b = 0; b < ns; ++b) v += Pn[a * ns + b] * F[b][j];
-                PF[a][j] = v;
-            }
-        for (int i = 0; i < nv; ++i)
-            for (int j = 0; j < nv; ++j) {
-                double v = HT(k, i, j);
-                for (int a = 0; a < ns; ++a) v += F[a][i] * PF[a][j];
-                M[i][j] = v;
+                double acc = 0;
+                for (int a = 0; a < ns; ++a) {
+                    double pf = 0;
+                    for (int b = 0; b < ns; ++b) pf += Pn[a * ns + b] * F[b][j];
+                    acc += P->Bbar[a][x] * pf;
+                }
+                Mu[x][j] = HT(k, ns + x, j) + acc;
             }
         double Ruu[MAXNU * MAXNU], Ri[MAXNU * MAXNU];
         for (int a = 0; a < nu; ++a)
-            for (int b = 0; b < nu; ++b) Ruu[a * nu + b] = M[ns + a][ns + b];
+            for (int b = 0; b < nu; ++b) Ruu[a * nu + b] = Mu[a][ns + b];
         if (chol_inv(nu, Ruu, Ri)) return -1;
         double* Kk = W->Ktab + (size_t)k * nu * ns;
         for (int a = 0; a < nu; ++a)
             for (int j = 0; j < ns; ++j) {
                 double v = 0;
-                for (int b = 0; b < nu; ++b) v -= Ri[a * nu + b] * M[ns + b][j];
+                for (int b = 0; b < nu; ++b) v -= Ri[a * nu + b] * Mu[b][j];
                 Kk[a * ns + j] = v;
             }
         for (int a = 0; a < nu * nu; ++a) W->Rinv[(size_t)k * nu * nu + a] = Ri[a];
+        /* Joseph form: P_k = [I;K]' Ht [I;K] + Phi' Pn Phi,  Phi = Abar + Bbar K */
+        double Phi[MAXNS][MAXNS];
+        for (int a = 0; a < ns; ++a)
+            for (int j = 0; j < ns; ++j) {
+                double v = P->Abar[a][j];
+                for (int x = 0; x < nu; ++x) v += P->Bbar[a][x] * Kk[x * ns + j];
+                Phi[a][j] = v;
+            }
         double* Pk = W->Ptab + (size_t)k * ns * ns;
         for (int i = 0; i < ns; ++i)
             for (int j = i; j < ns; ++j) {
-                double v = M[i][j];
-                for (int a = 0; a < nu; ++a) v += M[i][ns + a] * Kk[a * ns + j];
+                double v = HT(k, i, j);
+                for (int x = 0; x < nu; ++x) {
+                    v += Kk[x * ns + i] * HT(k, ns + x, j) + HT(k, i, ns + x) * Kk[x * ns + j];
+                    for (int y = 0; y < nu; ++y) v += Kk[x * ns + i] * HT(k, ns + x, ns + y) * Kk[y * ns + j];
+                }
+                double acc = 0;
+                for (int a = 0; a < ns; ++a) {
+                    double pf = 0;
+                    for (int b = 0; b < ns; ++b) pf += Pn[a * ns + b] * Phi[b][j];
+                    acc += Phi[a][i] * pf;
+                }
+                v += acc;
                 Pk[i * ns + j] = v;
                 Pk[j * ns + i] = v;
             }
@@ -512,8 +529,20 @@ typedef struct {
 static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, double* kkt) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns;
     const int nxr = (N + 1) * nx * 2, nur = N * nu * 2;
-    double stat, feas, cs;
+    double stat, feas, cs, gs;
     int mc;
+    double bs = 0;
+    for (int i = 0; i < nx; ++i) bs = fmax(bs, fabs(W->s[i]));
+    for (int k = 1; k <= N; ++k)
+        for (int i = 0; i < nx; ++i) {
+            if (isfinite(W->xub[k * nx + i])) bs = fmax(bs, fabs(W->xub[k * nx + i]));
+            if (isfinite(W->xlb[k * nx + i])) bs = fmax(bs, fabs(W->xlb[k * nx + i]));
+        }
+    for (int k = 0; k < N * nu; ++k) {
+        if (isfinite(W->uub[k])) bs = fmax(bs, fabs(W->uub[k]));
+        if (isfinite(W->ulb[k])) bs = fmax(bs, fabs(W->ulb[k]));
+    }
+    for (int r = 0; r < P->mp; ++r) bs = fmax(bs, fabs(W->hp[r]));
     /* init: t = lam = 1 on every row, unit-scaled least-squares Newton solve (rc = t o lam) */
     for (int i = 0; i < nxr; ++i) { W->tx[i] = 1.0; W->lx[i] = 1.0; }
     for (int i = 0; i < nur; ++i) { W->tu[i] = 1.0; W->lu[i] = 1.0; }
@@ -521,7 +550,7 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     double *rcx = (double*)malloc(sizeof(double) * (nxr + nur + P->mp + 1));
     double *rcu = rcx + nxr, *rcp = rcu + nur;
     for (int i = 0; i < nxr + nur + P->mp; ++i) rcx[i] = 1.0;
-    residuals(P, W, &stat, &feas, &cs, &mc);
+    residuals(P, W, &stat, &feas, &cs, &mc, &gs);
     if (factor(P, W)) { free(rcx); return -8; }
     solve_kkt(P, W, rcx, rcu, rcp);
     for (int i = 0; i < (N + 1) * ns; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
@@ -576,9 +605,9 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     int flag = 0, it;
     double mu = 0;
     for (it = 0; it <= op->max_iter; ++it) {
-        residuals(P, W, &stat, &feas, &cs, &mc);
+        residuals(P, W, &stat, &feas, &cs, &mc, &gs);
         mu = cs / (mc > 0 ? mc : 1);
-        if (stat <= op->tol_stat && feas <= op->tol_feas && mu <= op->tol_comp) { flag = 1; break; }
+        if (stat <= op->tol_stat * (1.0 + gs) && feas <= op->tol_feas * (1.0 + bs) && mu <= op->tol_comp) { flag = 1; break; }
         if (it == op->max_iter) break;
         if (factor(P, W)) { flag = -8; break; }
         for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i];

@@ -83,8 +83,8 @@ def pack_ocp(ocp, x0, w=None, hp=None, A=None, B=None):
     return dims, d, batch, keep
 
 
-def solve(ocp, x0, w=None, hp=None, A=None, B=None, max_iter=50, tol_stat=1e-10,
-          tol_feas=1e-10, tol_comp=1e-12, tau=0.995, threads=0):
+def solve(ocp, x0, w=None, hp=None, A=None, B=None, max_iter=50, tol_stat=1e-8,
+          tol_feas=1e-10, tol_comp=1e-14, tau=0.995, threads=0):
     dims, d, batch, keep = pack_ocp(ocp, x0, w, hp, A, B)
     nx, nu, p, N = ocp['nx'], ocp['nu'], ocp['np'], ocp['N']
     x = np.zeros((batch, N + 1, nx)); u = np.zeros((batch, N, nu)); th = np.zeros((batch, p))

@@ -80,6 +80,20 @@ def dump_constants():
     return consts, inst
 
 
+def write_design(consts, inst):
+    """mg_design.npz: the MG LMPC design data exactly as MATLAB held it (DSS_NMPC.m dump:
+    A, B, Kstabil, P, LAMBDA, PSI, F_x, h_x, F_u, h_u; Q = I, R = 1, T = 1000 from matOCP.m:27-31;
+    working point from LMPC_RunExample.m:48-52).  Used by bench.py / smoke() as problem data."""
+    text = open(REF + '/examples/DSS_NMPC.m').read()
+    d = dict(A=consts['A'], B=consts['B'].reshape(4, 1), K=consts['K'].reshape(1, 4),
+             P=consts['P'], LAMBDA=consts['LAMBDA'].reshape(4, 1), PSI=consts['PSI'].reshape(1, 1),
+             Q=np.eye(4), R=np.eye(1), T=np.array(1000.0), F_x=inst['F_x'], h_x=inst['h_x'],
+             F_u=parse_matlab_literal(text, 'F_u').reshape(2, 1),
+             h_u=parse_matlab_literal(text, 'h_u'),
+             x_wp=parse_matlab_literal(text, 'x_wp'), u_wp=np.array(1.1547))
+    np.savez(os.path.join(OUT, 'mg_design.npz'), **d)
+
+
 def invert_rk4(x, xn, delta=0.01):
     """Applied input u with RK4(x,u) = xn (1-D root find on the x4 component)."""
     f = lambda u: mg_rk4(delta, x, u)[3] - xn[3]
@@ -104,6 +118,7 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     consts, inst = dump_constants()
     np.savez(os.path.join(OUT, 'mg_constants.npz'), **consts)
+    write_design(consts, inst)
     np.savez(os.path.join(OUT, 'lbmpc_instance.npz'), **inst)
     ts = sio.loadmat(DATA + '/term_set.mat')
     F_T = ts['F_w_N'].astype(float)

@@ -54,13 +54,16 @@ class OCP:
         self.xlb[0] = -INF; self.xub[0] = INF                      # x_0 fixed: no rows
         self.kp = d['kp']
         Fp = d['Fp']
-        self.Fp = Fp[:, perm] if self.kp < N else np.hstack([Fp[:, :nx], Fp[:, nx + nu:], Fp[:, nx:nx + nu]])
+        self.Fp = Fp[:, perm] if self.kp < N else np.hstack([Fp[:, :nx], Fp[:, nx + nu:]])
         self.hp = np.asarray(d['hp'], float).copy()
         self.mp = self.Fp.shape[0]
         # finite-bound masks
         self.mxu = np.isfinite(self.xub); self.mxl = np.isfinite(self.xlb)
         self.muu = np.isfinite(self.uub); self.mul = np.isfinite(self.ulb)
         self.m = int(self.mxu.sum() + self.mxl.sum() + self.muu.sum() + self.mul.sum() + self.mp)
+        fin = lambda a: np.abs(a[np.isfinite(a)]).max(initial=0.0)
+        self.bscale = max(fin(self.xub), fin(self.xlb), fin(self.uub), fin(self.ulb), fin(self.hp),
+                          np.abs(self.x0).max(initial=0.0))
 
 
 class State:
@@ -87,16 +90,19 @@ def residuals(o, st):
     N, nx, ns, nu = o.N, o.nx, o.ns, o.nu
     s, u, pi = st.s, st.u, st.pi
     rs = np.zeros((N + 1, ns)); ru = np.zeros((N, nu)); re = np.zeros((N, ns))
+    gscale = 0.0
     for k in range(N + 1):
         H, g = o.H[k], o.g[k]
         if k < N:
             v = np.concatenate([s[k], u[k]])
             gv = H @ v + g
+            gscale = max(gscale, np.abs(gv).max())
             rs[k] = gv[:ns] + o.Abar.T @ pi[k + 1]
             ru[k] = gv[ns:] + o.Bbar.T @ pi[k + 1]
             re[k] = o.Abar @ s[k] + o.Bbar @ u[k] + o.cbar - s[k + 1]
         else:
             rs[k] = H[:ns, :ns] @ s[k] + g[:ns]
+            gscale = max(gscale, np.abs(rs[k]).max())
         if k > 0:
             rs[k] -= pi[k]
     # box rows
@@ -115,6 +121,7 @@ def residuals(o, st):
     riuu = np.where(o.muu, u + st.tuu - np.where(o.muu, o.uub, 0), 0)
     riul = np.where(o.mul, -u + st.tul + np.where(o.mul, o.ulb, 0), 0)
     rip = o.Fp @ _pvec(o, s, u) + st.tp - o.hp
+    o.gscale = gscale
     return rs, ru, re, (rixu, rixl, riuu, riul, rip)
 
 
@@ -161,7 +168,9 @@ def riccati_factor(o, st):
         Shat = S + B.T @ PA
         Lk = np.linalg.cholesky(Rh)
         Kk = -np.linalg.solve(Rh, Shat)
-        P[k] = Q + A.T @ PA + Shat.T @ Kk
+        # stabilised (Joseph) form: sum of PSD terms, no cancellation near convergence
+        Phi = A + B @ Kk
+        P[k] = Q + S.T @ Kk + Kk.T @ S + Kk.T @ R @ Kk + Phi.T @ P[k + 1] @ Phi
         P[k] = 0.5 * (P[k] + P[k].T)
         L[k] = Lk; Kg[k] = Kk; Sh[k] = Shat
     return dict(P=P, K=Kg, L=L, Sh=Sh, D=(Dxu, Dxl, Duu, Dul, Dp))
@@ -265,7 +274,8 @@ def nx_(o):
     return o.nx
 
 
-DEFAULTS = dict(max_iter=50, tol_stat=1e-10, tol_feas=1e-10, tol_comp=1e-10, tau=0.995)
+# stationarity is relative to 1 + |H v + g|_inf, feasibility to 1 + |bounds|_inf, mu absolute
+DEFAULTS = dict(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995)
 
 
 def solve(d, x0, w=None, opts=None, trace=None):
@@ -285,7 +295,8 @@ def solve(d, x0, w=None, opts=None, trace=None):
         if trace is not None:
             trace.append(dict(it=it, mu=mu, r_stat=r_stat, r_feas=r_feas,
                               s=st.s.copy(), u=st.u.copy()))
-        if r_stat <= op['tol_stat'] and r_feas <= op['tol_feas'] and mu <= op['tol_comp']:
+        if (r_stat <= op['tol_stat'] * (1.0 + o.gscale) and r_feas <= op['tol_feas'] * (1.0 + o.bscale)
+                and mu <= op['tol_comp']):
             exitflag = 1
             break
         if it == op['max_iter']:

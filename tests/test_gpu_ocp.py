@@ -1,0 +1,164 @@
+"""GPU parity tests of the structured solver (bqp_solve_ocp_batched through the C ABI) against
+the oracle: exact QP optima z* of the restated reference problems (tests/golden), MATLAB's
+stored moves, and the C restatement of the same algorithm (iterate-level agreement)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+TOL_Z = 1e-8          # |z - z*|_inf / max(1, |z*|_inf)  (north-star tolerance, fp64)
+TOL_ITER = 1e-9       # GPU vs C restatement of the same iteration
+
+
+@pytest.fixture(scope='module')
+def handle():
+    import bqp
+    return bqp.Handle(0)
+
+
+def _lmpc(mg, ts, N):
+    import bqp
+    return bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                    mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                    ts[0], ts[1], N=N)
+
+
+@pytest.mark.parametrize('N', [20, 40, 50])
+def test_f1_lmpc_vs_exact(mg, term_set, handle, N):
+    """config C2 problem (F1, MG, 616-row terminal set) vs exact optimum + fmincon."""
+    g = golden('lmpc_N%d.npz' % N)
+    lm = _lmpc(mg, term_set, N)
+    r = lm.solve(g['dx'][g['idx']], handle=handle)
+    assert (r.exitflag == 1).all()
+    zs = g['z_star']
+    err = np.abs(r.opt_var - zs).max() / max(1.0, np.abs(zs).max())
+    assert err < TOL_Z, err
+    # MATLAB fmincon's stored applied moves (tolerance set by fmincon, see test_oracle)
+    du_m = g['du_matlab'][g['idx']]
+    assert np.median(np.abs(r.du0[:, 0] - du_m)) < 1e-7
+
+
+def test_f1_matches_cpu_restatement(mg, term_set, handle):
+    from oracle import cpu_ref, qp_forms
+    g = golden('lmpc_N20.npz')
+    lm = _lmpc(mg, term_set, 20)
+    X0 = g['dx'][:256]
+    r = lm.solve(X0, handle=handle)
+    c = cpu_ref.solve(qp_forms.lmpc_ocp(mg, 20, *term_set), X0)
+    assert np.abs(r.x - c['x']).max() < TOL_ITER
+    assert np.abs(r.u - c['u']).max() < TOL_ITER
+    assert np.mean(r.iterations == c['iterations']) > 0.95
+
+
+@pytest.mark.parametrize('fname', ['dms_DSS_tLMPC.npz', 'dms_DMS_N50_tLMPC.npz'])
+def test_f2_tracking_lmpc_vs_exact(mg, term_set, handle, fname):
+    import bqp
+    g = golden(fname)
+    N = int(g['N'])
+    tl = bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                          mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                          term_set[0], term_set[1], mg['x_wp'], mg['u_wp'], N=N)
+    r = tl.solve(g['x'][g['idx']], handle=handle)
+    assert (r.exitflag == 1).all()
+    zs = g['z_star']
+    err = np.abs(r.y_OL - zs).max() / max(1.0, np.abs(zs).max())
+    assert err < TOL_Z, err
+
+
+def test_f5_tracking_mpc_di(di, handle):
+    """trackingMPC double integrator (F5) vs the oracle's dense restatement of costFunction.m /
+    constraintsFunction.m (parity pinned to the restatement only: the reference stores no DI
+    results)."""
+    import bqp
+    from oracle import dense_qp, mpis, qp_forms
+    F_T, h_T = mpis.di_terminal_set(di)
+    N = 30
+    tm = bqp.TrackingMPC(di['A'], di['B'], di['Q'], di['R'], di['P'], di['T'], di['LAMBDA'],
+                         di['PSI'], di['F_x'], di['h_x'], di['F_u'], di['h_u'], F_T, h_T, N=N)
+    rng = np.random.default_rng(30)
+    X = rng.uniform(-3, 3, size=(6, 2))
+    XS = np.array([[4.95, 0], [-5.5, 0], [2, 0], [0, 0], [4.95, 0], [2, 0]])
+    r = tm.solve(X, XS, handle=handle)
+    assert (r.exitflag == 1).all()
+    for i in range(len(X)):
+        qp = qp_forms.track_dense(di, N, X[i], XS[i], F_T, h_T)
+        z, fval, _, _ = dense_qp.solve(qp)
+        # F5 is not strictly convex in the last input (no cost on u_{N-1}); compare the
+        # objective, the first move and the artificial steady state LAMBDA*theta.
+        assert abs(r.fval[i] - (fval + qp['const'])) < 1e-7 * max(1, abs(fval))
+        assert np.abs(r.u0[i] - z[:2]).max() < 1e-6
+        assert np.abs(di['LAMBDA'] @ (r.theta[i] - z[-2:])).max() < 1e-6
+
+
+def test_duals_kkt(mg, term_set, handle):
+    """Multiplier outputs satisfy the KKT conditions of the dense F2 problem."""
+    import bqp
+    from oracle import qp_forms
+    g = golden('dms_DMS_N50_tLMPC.npz')
+    N = 50
+    tl = bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                          mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                          term_set[0], term_set[1], mg['x_wp'], mg['u_wp'], N=N)
+    i = g['idx'][0]
+    r = tl.solve(g['x'][i:i + 1], handle=handle, want_duals=True)
+    assert r.exitflag[0] == 1
+    lam_p = r.lam_p[0]
+    assert (lam_p >= -1e-12).all() and (r.lam_x >= -1e-12).all() and (r.lam_u >= -1e-12).all()
+    # complementarity on the terminal rows
+    ocp = qp_forms.dms_ocp(mg, N, *term_set)
+    xN = r.x[0, N] - mg['x_wp']
+    slack = term_set[1] - term_set[0] @ np.concatenate([xN, r.theta[0]])
+    assert np.abs(lam_p * slack).max() < 1e-8
+    assert slack.min() > -1e-9
+    assert ocp['Fp'].shape[0] == lam_p.size
+
+
+def test_per_instance_models(mg, term_set, handle):
+    """C4-style Monte-Carlo batch: per-instance (A, B) through the strided ABI == C port."""
+    import bqp
+    from oracle import cpu_ref, qp_forms
+    rng = np.random.default_rng(4)
+    b = 32
+    A = mg['A'] + 0.01 * rng.standard_normal((b, 4, 4)) * np.abs(mg['A'])
+    B = mg['B'] + 0.01 * rng.standard_normal((b, 4, 1)) * np.abs(mg['B'])
+    g = golden('lmpc_N20.npz')
+    X0 = g['dx'][:b]
+    lm = _lmpc(mg, term_set, 20)
+    r = bqp.solve_ocp(lm.prob, X0, A=A, B=B, handle=handle)
+    c = cpu_ref.solve(qp_forms.lmpc_ocp(mg, 20, *term_set), X0, A=A, B=B)
+    ok = c['exitflag'] == 1
+    assert ok.mean() > 0.5
+    assert (r.exitflag[ok] == 1).all()
+    assert np.abs(r.u[ok] - c['u'][ok]).max() < 1e-8
+
+
+def test_edge_cases(mg, term_set, handle):
+    """batch of 1, no polytope, unbounded boxes, identical instances give identical answers."""
+    import bqp
+    lm = _lmpc(mg, term_set, 20)
+    g = golden('lmpc_N20.npz')
+    r1 = lm.solve(g['dx'][:1], handle=handle)
+    assert r1.exitflag[0] == 1
+    p = lm.prob
+    free = bqp.OcpProblem(p.A, p.B, p.W, p.N, 1, w=p.w)      # unconstrained LQ problem
+    r = bqp.solve_ocp(free, g['dx'][:3], handle=handle)
+    assert (r.exitflag == 1).all()
+    X = np.repeat(g['dx'][5:6], 300, axis=0)
+    r = lm.solve(X, handle=handle)
+    assert np.all(r.u == r.u[0]) and np.all(r.iterations == r.iterations[0])
+
+
+def test_large_batch_properties(mg, term_set, handle):
+    """Full-size batch (C2 cycled to 65536): every instance converges and equals the same
+    instance solved in a small batch (batch-size independence)."""
+    g = golden('lmpc_N20.npz')
+    lm = _lmpc(mg, term_set, 20)
+    B = 65536
+    X = g['dx'][np.arange(B) % 1000]
+    r = lm.solve(X, handle=handle)
+    assert (r.exitflag == 1).all()
+    small = lm.solve(g['dx'][:1000], handle=handle)
+    assert np.array_equal(r.u[:1000], small.u)
+    assert np.array_equal(r.u[1000:2000], small.u)

@@ -35,6 +35,33 @@ def _prep(a, shape, batch):
     return a, (size if per else 0)
 
 
+def _fixed_to_equalities(n, Aeq, beq, lb, ub, batch):
+    """quadprog accepts lb == ub (fixed variables); the kernel takes them as equality rows."""
+    if lb is None or ub is None:
+        return Aeq, beq, lb, ub, None
+    L = np.broadcast_to(np.asarray(lb, float), (batch, n))
+    U = np.broadcast_to(np.asarray(ub, float), (batch, n))
+    fixed = np.isfinite(L) & np.isfinite(U) & (L == U)
+    if not fixed.any():
+        return Aeq, beq, lb, ub, None
+    if not (fixed == fixed[0]).all():
+        raise ValueError('fixed variables (lb == ub) must be the same for every instance')
+    idx = np.flatnonzero(fixed[0])
+    E = np.zeros((idx.size, n)); E[np.arange(idx.size), idx] = 1.0
+    me0 = 0 if Aeq is None else np.shape(Aeq)[-2]
+    if Aeq is None:
+        Aeq2 = E
+        beq2 = L[:, idx]
+    else:
+        Ae = np.asarray(Aeq, float)
+        Aeq2 = np.concatenate([np.broadcast_to(Ae, (batch,) + Ae.shape[-2:]),
+                               np.broadcast_to(E, (batch,) + E.shape)], axis=1)
+        beq2 = np.concatenate([np.broadcast_to(np.asarray(beq, float), (batch, me0)), L[:, idx]], axis=1)
+    lb2 = np.where(fixed, -np.inf, L)
+    ub2 = np.where(fixed, np.inf, U)
+    return Aeq2, beq2, lb2, ub2, (idx, me0)
+
+
 def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, x0=None, options=None,
              handle=None):
     from .ocp import _default_handle
@@ -42,6 +69,11 @@ def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, x0=None
     H = np.asarray(H, float)
     f = np.asarray(f, float)
     n = H.shape[-1]
+    b0 = max(H.shape[0] if H.ndim == 3 else 1, f.shape[0] if f.ndim == 2 else 1)
+    for a_, nd in ((A, 2), (b, 1), (Aeq, 2), (beq, 1), (lb, 1), (ub, 1)):
+        if a_ is not None and np.ndim(a_) == nd + 1:
+            b0 = max(b0, np.shape(a_)[0])
+    Aeq, beq, lb, ub, fixinfo = _fixed_to_equalities(n, Aeq, beq, lb, ub, b0)
     batch = max(H.shape[0] if H.ndim == 3 else 1, f.shape[0] if f.ndim == 2 else 1)
     for a, nd in ((A, 2), (b, 1), (Aeq, 2), (beq, 1), (lb, 1), (ub, 1)):
         if a is not None and np.ndim(a) == nd + 1:
@@ -74,4 +106,11 @@ def quadprog(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, x0=None
                   constrviolation=np.array([q.constrviolation for q in out]),
                   firstorderopt=np.array([q.firstorderopt for q in out]))
     lam = dict(ineqlin=li[:, :m], eqlin=le[:, :me], lower=ll, upper=lu)
+    if fixinfo is not None:
+        idx, me0 = fixinfo
+        yf = le[:, me0:me]
+        lam['eqlin'] = le[:, :me0]
+        # multiplier of a fixed variable reported on lower/upper by sign (quadprog convention)
+        lam['upper'][:, idx] = np.maximum(yf, 0.0)
+        lam['lower'][:, idx] = np.maximum(-yf, 0.0)
     return x, fval, flag, output, lam

@@ -177,8 +177,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const double minv = 1.0 / fmax(mtot, 1.0);
 
     // ---------------------------------------------------------------- residuals
-    auto residuals = [&](double& stat, double& feas, double& csum) {
-        double fe = 0.0, cs = 0.0, st = 0.0;
+    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) {
+        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0;
         for (int r = tid; r < m; r += DT) {
             double v = tA[r] - b[r];
             for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
@@ -195,6 +195,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         for (int j = tid; j < n; j += DT) {
             double v = f[j];
             for (int i = 0; i < n; ++i) v += H[(int64_t)j * n + i] * z[i];
+            gs = fmax(gs, fabs(v));
             for (int r = 0; r < me; ++r) v += E[(int64_t)j * me + r] * y[r];
             for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * lA[r];
             riB[j] = 0.0; riB[n + j] = 0.0;
@@ -215,6 +216,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         stat = red.max(st);
         feas = red.max(fe);
         csum = red.sum(cs);
+        gscale = red.max(gs);
     };
 
     // ---------------------------------------------------------------- factorisation
@@ -378,8 +380,17 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         if (lo_present(j)) lB[n + j] = 1.0;
     }
     __syncthreads();
-    double stat, feas, csum;
-    residuals(stat, feas, csum);
+    // primal data scale for the relative feasibility test
+    double bsl = 0.0;
+    for (int r = tid; r < m; r += DT) bsl = fmax(bsl, fabs(b[r]));
+    for (int r = tid; r < me; r += DT) bsl = fmax(bsl, fabs(e[r]));
+    for (int j = tid; j < n; j += DT) {
+        if (up_present(j)) bsl = fmax(bsl, fabs(ub[j]));
+        if (lo_present(j)) bsl = fmax(bsl, fabs(lb[j]));
+    }
+    const double bscale = red.max(bsl);
+    double stat, feas, csum, gscale;
+    residuals(stat, feas, csum, gscale);
     int flag = 0;
     if (!factor()) flag = -8;
     if (flag == 0) {
@@ -409,9 +420,10 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double mu = 0.0;
     if (flag == 0) {
         for (it = 0; it <= a.max_iter; ++it) {
-            residuals(stat, feas, csum);
+            residuals(stat, feas, csum, gscale);
             mu = csum * minv;
-            if (stat <= a.tol_stat && feas <= a.tol_feas && mu <= a.tol_comp) { flag = 1; break; }
+            if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
+                mu <= a.tol_comp) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }

@@ -30,20 +30,52 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave-wide reductions on DPP lane moves (quad_perm xor1/xor2, row_half_mirror, row_mirror
+// inside each 16-lane row, then row_bcast15/31 across rows) + one readlane of lane 63: no LDS
+// traffic, result uniform (SGPR) in every lane.  EXEC must be full (all call sites are
+// wave-uniform).
+template <int CTRL, int ROWM>
+__device__ __forceinline__ double dpp_mov(double old, double v) {
+    const int2 o = __builtin_bit_cast(int2, old);
+    const int2 x = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(o.x, x.x, CTRL, ROWM, 0xf, false);
+    r.y = __builtin_amdgcn_update_dpp(o.y, x.y, CTRL, ROWM, 0xf, false);
+    return __builtin_bit_cast(double, r);
+}
+__device__ __forceinline__ double lane63(double v) {
+    const int2 x = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(x.x, 63);
+    r.y = __builtin_amdgcn_readlane(x.y, 63);
+    return __builtin_bit_cast(double, r);
+}
 __device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v += dpp_mov<0xB1, 0xf>(0.0, v);
+    v += dpp_mov<0x4E, 0xf>(0.0, v);
+    v += dpp_mov<0x141, 0xf>(0.0, v);
+    v += dpp_mov<0x140, 0xf>(0.0, v);
+    v += dpp_mov<0x142, 0xa>(0.0, v);
+    v += dpp_mov<0x143, 0xc>(0.0, v);
+    return lane63(v);
 }
 __device__ __forceinline__ double wmax(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
+    v = fmax(v, dpp_mov<0xB1, 0xf>(-INFINITY, v));
+    v = fmax(v, dpp_mov<0x4E, 0xf>(-INFINITY, v));
+    v = fmax(v, dpp_mov<0x141, 0xf>(-INFINITY, v));
+    v = fmax(v, dpp_mov<0x140, 0xf>(-INFINITY, v));
+    v = fmax(v, dpp_mov<0x142, 0xa>(-INFINITY, v));
+    v = fmax(v, dpp_mov<0x143, 0xc>(-INFINITY, v));
+    return lane63(v);
 }
 __device__ __forceinline__ double wmin(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    return v;
+    v = fmin(v, dpp_mov<0xB1, 0xf>(INFINITY, v));
+    v = fmin(v, dpp_mov<0x4E, 0xf>(INFINITY, v));
+    v = fmin(v, dpp_mov<0x141, 0xf>(INFINITY, v));
+    v = fmin(v, dpp_mov<0x140, 0xf>(INFINITY, v));
+    v = fmin(v, dpp_mov<0x142, 0xa>(INFINITY, v));
+    v = fmin(v, dpp_mov<0x143, 0xc>(INFINITY, v));
+    return lane63(v);
 }
 
 // Per-wave LDS layout (in doubles), all sized from N at run time.
@@ -236,6 +268,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     double dtu[SPL][NU][2], dlu[SPL][NU][2], dtp[RPL], dlp[RPL];
     double rcx[SPL][NX][2], rcu[SPL][NU][2], rcp[RPL];   // complementarity rhs
     double kff[SPL][NU];
+    double itx[SPL][NX][2], itu[SPL][NU][2], itp[RPL];   // 1/t, once per iteration
 
     auto xpres = [&](int j, int i, int h) -> bool { return (mx[j] >> (2 * i + h)) & 1u; };
     auto upres = [&](int j, int i, int h) -> bool { return (mu_[j] >> (2 * i + h)) & 1u; };
@@ -398,6 +431,16 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     // ======================= Riccati factorisation =========================================
     double P0inv[NP][NP];
     auto factor = [&]() -> bool {
+        // one reciprocal of t per row per iteration (reused by both solves and max_step)
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) { itx[j][i][0] = 1.0 / tx[j][i][0]; itx[j][i][1] = 1.0 / tx[j][i][1]; }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) { itu[j][i][0] = 1.0 / tu[j][i][0]; itu[j][i][1] = 1.0 / tu[j][i][1]; }
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) itp[q] = 1.0 / tp[q];
         // box diagonals -> LDS
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -406,15 +449,15 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
                     double d = 0;
-                    if (xpres(j, i, 0)) d += lx[j][i][0] / tx[j][i][0];
-                    if (xpres(j, i, 1)) d += lx[j][i][1] / tx[j][i][1];
+                    if (xpres(j, i, 0)) d += lx[j][i][0] * itx[j][i][0];
+                    if (xpres(j, i, 1)) d += lx[j][i][1] * itx[j][i][1];
                     W[L.Dx + k * NX + i] = d;
                 }
 #pragma unroll
                 for (int i = 0; i < NU; ++i) {
                     double d = 0;
-                    if (upres(j, i, 0)) d += lu[j][i][0] / tu[j][i][0];
-                    if (upres(j, i, 1)) d += lu[j][i][1] / tu[j][i][1];
+                    if (upres(j, i, 0)) d += lu[j][i][0] * itu[j][i][0];
+                    if (upres(j, i, 1)) d += lu[j][i][1] * itu[j][i][1];
                     W[L.Du + k * NU + i] = d;
                 }
             }
@@ -427,7 +470,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
             if (r < mp) {
-                const double d = lp[q] / tp[q];
+                const double d = lp[q] * itp[q];
                 double f[NV];
 #pragma unroll
                 for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
@@ -601,15 +644,15 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 double e = 0.0;
-                if (xpres(j, i, 0)) e += (lx[j][i][0] * rix[j][i][0] - rcx[j][i][0]) / tx[j][i][0];
-                if (xpres(j, i, 1)) e -= (lx[j][i][1] * rix[j][i][1] - rcx[j][i][1]) / tx[j][i][1];
+                if (xpres(j, i, 0)) e += (lx[j][i][0] * rix[j][i][0] - rcx[j][i][0]) * itx[j][i][0];
+                if (xpres(j, i, 1)) e -= (lx[j][i][1] * rix[j][i][1] - rcx[j][i][1]) * itx[j][i][1];
                 qs[j][i] += e;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 double e = ru[j][i];
-                if (upres(j, i, 0)) e += (lu[j][i][0] * riu[j][i][0] - rcu[j][i][0]) / tu[j][i][0];
-                if (upres(j, i, 1)) e -= (lu[j][i][1] * riu[j][i][1] - rcu[j][i][1]) / tu[j][i][1];
+                if (upres(j, i, 0)) e += (lu[j][i][0] * riu[j][i][0] - rcu[j][i][0]) * itu[j][i][0];
+                if (upres(j, i, 1)) e -= (lu[j][i][1] * riu[j][i][1] - rcu[j][i][1]) * itu[j][i][1];
                 qu[j][i] = e;
             }
         }
@@ -621,7 +664,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int q = 0; q < RPL; ++q) {
                 const int r = lane + WAVE * q;
                 if (r < mp) {
-                    const double e = (lp[q] * rip[q] - rcp[q]) / tp[q];
+                    const double e = (lp[q] * rip[q] - rcp[q]) * itp[q];
 #pragma unroll
                     for (int c = 0; c < NV; ++c) gpp[c] += Fs[c * mpad + r] * e;
                 }
@@ -814,11 +857,11 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 dtx[j][i][0] = dtx[j][i][1] = dlx[j][i][0] = dlx[j][i][1] = 0.0;
                 if (xpres(j, i, 0)) {
                     dtx[j][i][0] = -rix[j][i][0] - dx;
-                    dlx[j][i][0] = (-rcx[j][i][0] - lx[j][i][0] * dtx[j][i][0]) / tx[j][i][0];
+                    dlx[j][i][0] = (-rcx[j][i][0] - lx[j][i][0] * dtx[j][i][0]) * itx[j][i][0];
                 }
                 if (xpres(j, i, 1)) {
                     dtx[j][i][1] = -rix[j][i][1] + dx;
-                    dlx[j][i][1] = (-rcx[j][i][1] - lx[j][i][1] * dtx[j][i][1]) / tx[j][i][1];
+                    dlx[j][i][1] = (-rcx[j][i][1] - lx[j][i][1] * dtx[j][i][1]) * itx[j][i][1];
                 }
             }
 #pragma unroll
@@ -827,11 +870,11 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 dtu[j][i][0] = dtu[j][i][1] = dlu[j][i][0] = dlu[j][i][1] = 0.0;
                 if (upres(j, i, 0)) {
                     dtu[j][i][0] = -riu[j][i][0] - dd;
-                    dlu[j][i][0] = (-rcu[j][i][0] - lu[j][i][0] * dtu[j][i][0]) / tu[j][i][0];
+                    dlu[j][i][0] = (-rcu[j][i][0] - lu[j][i][0] * dtu[j][i][0]) * itu[j][i][0];
                 }
                 if (upres(j, i, 1)) {
                     dtu[j][i][1] = -riu[j][i][1] + dd;
-                    dlu[j][i][1] = (-rcu[j][i][1] - lu[j][i][1] * dtu[j][i][1]) / tu[j][i][1];
+                    dlu[j][i][1] = (-rcu[j][i][1] - lu[j][i][1] * dtu[j][i][1]) * itu[j][i][1];
                 }
             }
         }
@@ -849,34 +892,36 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
                 for (int c = 0; c < NV; ++c) acc += Fs[c * mpad + r] * dvp[c];
                 dtp[q] = -rip[q] - acc;
-                dlp[q] = (-rcp[q] - lp[q] * dtp[q]) / tp[q];
+                dlp[q] = (-rcp[q] - lp[q] * dtp[q]) * itp[q];
             } else {
                 dtp[q] = 0.0; dlp[q] = 0.0;
             }
         }
     };
 
+    // alpha = min(1, 1 / max(-dt/t, -dlam/lam)) (same form as oracle/cpu_ipm.c max_step)
     auto max_step = [&]() -> double {
-        double al = 1.0;
-#define BQP_RATIO(v, dv) if ((dv) < 0.0) { const double qq = -(v) / (dv); al = fmin(al, qq); }
+        double rm = 0.0;
+#define BQP_RATIO(dv, iv) { const double qq = -(dv) * (iv); rm = fmax(rm, qq); }
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
 #pragma unroll
             for (int i = 0; i < NX; ++i)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    if (xpres(j, i, h)) { BQP_RATIO(tx[j][i][h], dtx[j][i][h]); BQP_RATIO(lx[j][i][h], dlx[j][i][h]); }
+                    if (xpres(j, i, h)) { BQP_RATIO(dtx[j][i][h], itx[j][i][h]); BQP_RATIO(dlx[j][i][h], 1.0 / lx[j][i][h]); }
 #pragma unroll
             for (int i = 0; i < NU; ++i)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    if (upres(j, i, h)) { BQP_RATIO(tu[j][i][h], dtu[j][i][h]); BQP_RATIO(lu[j][i][h], dlu[j][i][h]); }
+                    if (upres(j, i, h)) { BQP_RATIO(dtu[j][i][h], itu[j][i][h]); BQP_RATIO(dlu[j][i][h], 1.0 / lu[j][i][h]); }
         }
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
-            if (lane + WAVE * q < mp) { BQP_RATIO(tp[q], dtp[q]); BQP_RATIO(lp[q], dlp[q]); }
+            if (lane + WAVE * q < mp) { BQP_RATIO(dtp[q], itp[q]); BQP_RATIO(dlp[q], 1.0 / lp[q]); }
 #undef BQP_RATIO
-        return wmin(al);
+        rm = wmax(rm);
+        return rm > 1.0 ? 1.0 / rm : 1.0;
     };
 
     auto comp_after = [&](double al) -> double {

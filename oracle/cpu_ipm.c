@@ -39,6 +39,7 @@ typedef struct {
     double *ds, *du, *dpi, *dtx, *dlx, *dtu, *dlu, *dtp, *dlp;
     double *Ptab, *Ktab, *Rinv, *p, *qs, *qu, *wv, *qt, *kff, *f;
     double *Dx, *Du, *FD;
+    double *itx, *ilx, *itu, *ilu, *itp, *ilp;   /* 1/t, 1/lam (once per iteration) */
     double P0inv[MAXNS * MAXNS];
 } work_t;
 
@@ -200,27 +201,31 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
 /* ---------------- factorisation ---------------- */
 static int factor(const prob_t* P, work_t* W) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv;
+    /* one reciprocal of t and lam per row per iteration; every later quotient is a product */
+    for (int i = 0; i < (N + 1) * nx * 2; ++i) { W->itx[i] = 1.0 / W->tx[i]; W->ilx[i] = 1.0 / W->lx[i]; }
+    for (int i = 0; i < N * nu * 2; ++i) { W->itu[i] = 1.0 / W->tu[i]; W->ilu[i] = 1.0 / W->lu[i]; }
+    for (int r = 0; r < P->mp; ++r) { W->itp[r] = 1.0 / W->tp[r]; W->ilp[r] = 1.0 / W->lp[r]; }
     /* box diagonals */
     for (int k = 0; k <= N; ++k)
         for (int i = 0; i < nx; ++i) {
             int o = (k * nx + i) * 2;
             double d = 0;
-            if (k > 0 && isfinite(W->xub[k * nx + i])) d += W->lx[o] / W->tx[o];
-            if (k > 0 && isfinite(W->xlb[k * nx + i])) d += W->lx[o + 1] / W->tx[o + 1];
+            if (k > 0 && isfinite(W->xub[k * nx + i])) d += W->lx[o] * W->itx[o];
+            if (k > 0 && isfinite(W->xlb[k * nx + i])) d += W->lx[o + 1] * W->itx[o + 1];
             W->Dx[k * nx + i] = d;
         }
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int o = (k * nu + i) * 2;
             double d = 0;
-            if (isfinite(W->uub[k * nu + i])) d += W->lu[o] / W->tu[o];
-            if (isfinite(W->ulb[k * nu + i])) d += W->lu[o + 1] / W->tu[o + 1];
+            if (isfinite(W->uub[k * nu + i])) d += W->lu[o] * W->itu[o];
+            if (isfinite(W->ulb[k * nu + i])) d += W->lu[o + 1] * W->itu[o + 1];
             W->Du[k * nu + i] = d;
         }
     memset(W->FD, 0, sizeof(double) * nv * nv);
     for (int r = 0; r < P->mp; ++r) {
         const double* F = P->Fp + (size_t)r * nv;
-        double d = W->lp[r] / W->tp[r];
+        double d = W->lp[r] * W->itp[r];
         for (int i = 0; i < nv; ++i) {
             double di = d * F[i];
             for (int j = i; j < nv; ++j) W->FD[i * nv + j] += di * F[j];
@@ -318,16 +323,16 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
         for (int i = 0; i < nx; ++i) {
             int o = (k * nx + i) * 2;
             double e = 0;
-            if (k > 0 && isfinite(W->xub[k * nx + i])) e += (W->lx[o] * W->rix[o] - rcx[o]) / W->tx[o];
-            if (k > 0 && isfinite(W->xlb[k * nx + i])) e -= (W->lx[o + 1] * W->rix[o + 1] - rcx[o + 1]) / W->tx[o + 1];
+            if (k > 0 && isfinite(W->xub[k * nx + i])) e += (W->lx[o] * W->rix[o] - rcx[o]) * W->itx[o];
+            if (k > 0 && isfinite(W->xlb[k * nx + i])) e -= (W->lx[o + 1] * W->rix[o + 1] - rcx[o + 1]) * W->itx[o + 1];
             W->qs[k * ns + i] += e;
         }
         if (k < N)
             for (int i = 0; i < nu; ++i) {
                 int o = (k * nu + i) * 2;
                 double e = W->ru[k * nu + i];
-                if (isfinite(W->uub[k * nu + i])) e += (W->lu[o] * W->riu[o] - rcu[o]) / W->tu[o];
-                if (isfinite(W->ulb[k * nu + i])) e -= (W->lu[o + 1] * W->riu[o + 1] - rcu[o + 1]) / W->tu[o + 1];
+                if (isfinite(W->uub[k * nu + i])) e += (W->lu[o] * W->riu[o] - rcu[o]) * W->itu[o];
+                if (isfinite(W->ulb[k * nu + i])) e -= (W->lu[o + 1] * W->riu[o + 1] - rcu[o + 1]) * W->itu[o + 1];
                 W->qu[k * nu + i] = e;
             }
     }
@@ -335,7 +340,7 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
         double gp[MAXNV];
         memset(gp, 0, sizeof(gp));
         for (int r = 0; r < P->mp; ++r) {
-            double e = (W->lp[r] * W->rip[r] - rcp[r]) / W->tp[r];
+            double e = (W->lp[r] * W->rip[r] - rcp[r]) * W->itp[r];
             const double* F = P->Fp + (size_t)r * nv;
             for (int j = 0; j < nv; ++j) gp[j] += F[j] * e;
         }
@@ -443,11 +448,11 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             W->dtx[o] = W->dtx[o + 1] = W->dlx[o] = W->dlx[o + 1] = 0;
             if (k > 0 && isfinite(W->xub[k * nx + i])) {
                 W->dtx[o] = -W->rix[o] - dx;
-                W->dlx[o] = (-rcx[o] - W->lx[o] * W->dtx[o]) / W->tx[o];
+                W->dlx[o] = (-rcx[o] - W->lx[o] * W->dtx[o]) * W->itx[o];
             }
             if (k > 0 && isfinite(W->xlb[k * nx + i])) {
                 W->dtx[o + 1] = -W->rix[o + 1] + dx;
-                W->dlx[o + 1] = (-rcx[o + 1] - W->lx[o + 1] * W->dtx[o + 1]) / W->tx[o + 1];
+                W->dlx[o + 1] = (-rcx[o + 1] - W->lx[o + 1] * W->dtx[o + 1]) * W->itx[o + 1];
             }
         }
     for (int k = 0; k < N; ++k)
@@ -457,11 +462,11 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             W->dtu[o] = W->dtu[o + 1] = W->dlu[o] = W->dlu[o + 1] = 0;
             if (isfinite(W->uub[k * nu + i])) {
                 W->dtu[o] = -W->riu[o] - du;
-                W->dlu[o] = (-rcu[o] - W->lu[o] * W->dtu[o]) / W->tu[o];
+                W->dlu[o] = (-rcu[o] - W->lu[o] * W->dtu[o]) * W->itu[o];
             }
             if (isfinite(W->ulb[k * nu + i])) {
                 W->dtu[o + 1] = -W->riu[o + 1] + du;
-                W->dlu[o + 1] = (-rcu[o + 1] - W->lu[o + 1] * W->dtu[o + 1]) / W->tu[o + 1];
+                W->dlu[o + 1] = (-rcu[o + 1] - W->lu[o + 1] * W->dtu[o + 1]) * W->itu[o + 1];
             }
         }
     {
@@ -474,31 +479,31 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             double a = 0;
             for (int j = 0; j < nv; ++j) a += F[j] * dv[j];
             W->dtp[r] = -W->rip[r] - a;
-            W->dlp[r] = (-rcp[r] - W->lp[r] * W->dtp[r]) / W->tp[r];
+            W->dlp[r] = (-rcp[r] - W->lp[r] * W->dtp[r]) * W->itp[r];
         }
     }
 }
 
 static double max_step(const prob_t* P, work_t* W) {
+    /* alpha = min(1, 1 / max(-dt/t, -dlam/lam)) over the present rows */
     const int N = P->N, nx = P->nx, nu = P->nu;
-    double a = 1.0;
-#define RATIO(v, dv) \
-    if ((dv) < 0) { double q = -(v) / (dv); if (q < a) a = q; }
+    double rm = 0.0;
+#define RATIO(dv, iv) { const double q = -(dv) * (iv); if (q > rm) rm = q; }
     for (int k = 1; k <= N; ++k)
         for (int i = 0; i < nx; ++i) {
             int o = (k * nx + i) * 2;
-            if (isfinite(W->xub[k * nx + i])) { RATIO(W->tx[o], W->dtx[o]); RATIO(W->lx[o], W->dlx[o]); }
-            if (isfinite(W->xlb[k * nx + i])) { RATIO(W->tx[o + 1], W->dtx[o + 1]); RATIO(W->lx[o + 1], W->dlx[o + 1]); }
+            if (isfinite(W->xub[k * nx + i])) { RATIO(W->dtx[o], W->itx[o]); RATIO(W->dlx[o], W->ilx[o]); }
+            if (isfinite(W->xlb[k * nx + i])) { RATIO(W->dtx[o + 1], W->itx[o + 1]); RATIO(W->dlx[o + 1], W->ilx[o + 1]); }
         }
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int o = (k * nu + i) * 2;
-            if (isfinite(W->uub[k * nu + i])) { RATIO(W->tu[o], W->dtu[o]); RATIO(W->lu[o], W->dlu[o]); }
-            if (isfinite(W->ulb[k * nu + i])) { RATIO(W->tu[o + 1], W->dtu[o + 1]); RATIO(W->lu[o + 1], W->dlu[o + 1]); }
+            if (isfinite(W->uub[k * nu + i])) { RATIO(W->dtu[o], W->itu[o]); RATIO(W->dlu[o], W->ilu[o]); }
+            if (isfinite(W->ulb[k * nu + i])) { RATIO(W->dtu[o + 1], W->itu[o + 1]); RATIO(W->dlu[o + 1], W->ilu[o + 1]); }
         }
-    for (int r = 0; r < P->mp; ++r) { RATIO(W->tp[r], W->dtp[r]); RATIO(W->lp[r], W->dlp[r]); }
+    for (int r = 0; r < P->mp; ++r) { RATIO(W->dtp[r], W->itp[r]); RATIO(W->dlp[r], W->ilp[r]); }
 #undef RATIO
-    return a;
+    return rm > 1.0 ? 1.0 / rm : 1.0;
 }
 
 static double comp_after(const prob_t* P, work_t* W, double a) {
@@ -689,6 +694,8 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.qs = alloc0((N + 1) * ns); W.qu = alloc0(N * nu); W.wv = alloc0(N * ns);
         W.qt = alloc0(N * ns); W.kff = alloc0(N * nu); W.f = alloc0(N * ns);
         W.Dx = alloc0((N + 1) * nx); W.Du = alloc0(N * nu); W.FD = alloc0(nv * nv);
+        W.itx = alloc0((N + 1) * nx * 2); W.ilx = alloc0((N + 1) * nx * 2);
+        W.itu = alloc0(N * nu * 2); W.ilu = alloc0(N * nu * 2); W.itp = alloc0(mp); W.ilp = alloc0(mp);
         prob_t P;
         memset(&P, 0, sizeof(P));
         P.nx = nx; P.nu = nu; P.np = np; P.ns = ns; P.nv = nv; P.N = N; P.mp = mp;
@@ -758,7 +765,8 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.ds); free(W.du); free(W.dpi); free(W.dtx); free(W.dlx); free(W.dtu); free(W.dlu);
         free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Ktab); free(W.Rinv); free(W.p);
         free(W.qs); free(W.qu); free(W.wv); free(W.qt); free(W.kff); free(W.f); free(W.Dx);
-        free(W.Du); free(W.FD);
+        free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
+        free(W.ilp);
     }
     return err;
 }

@@ -9,7 +9,7 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 TOL_Z = 1e-8          # |z - z*|_inf / max(1, |z*|_inf)  (north-star tolerance, fp64)
-TOL_ITER = 1e-9       # GPU vs C restatement of the same iteration
+TOL_ITER = 1e-8       # GPU vs C restatement of the same iteration (rounding-order differences)
 
 
 @pytest.fixture(scope='module')
@@ -49,6 +49,8 @@ def test_f1_matches_cpu_restatement(mg, term_set, handle):
     c = cpu_ref.solve(qp_forms.lmpc_ocp(mg, 20, *term_set), X0)
     assert np.abs(r.x - c['x']).max() < TOL_ITER
     assert np.abs(r.u - c['u']).max() < TOL_ITER
+    # same iterates to round-off on (almost) every instance
+    assert np.median(np.abs(r.u - c['u']).max(axis=(1, 2))) < 1e-11
     assert np.mean(r.iterations == c['iterations']) > 0.95
 
 

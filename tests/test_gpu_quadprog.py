@@ -1,0 +1,74 @@
+"""GPU parity tests of the quadprog-compatible dense entry point (bqp_quadprog_batched) on the
+reference's QPs in their own variable layout (oracle/qp_forms restates the MATLAB loops)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def handle():
+    import bqp
+    return bqp.Handle(0)
+
+
+def test_f1_dense_quadprog(mg, term_set, handle):
+    """fmincon LMPC (F1) as a dense QP: 21 vars, 806 rows; batch of fixture states."""
+    import bqp
+    from oracle import qp_forms
+    g = golden('lmpc_N20.npz')
+    sel = np.arange(16)
+    qps = [qp_forms.lmpc_dense(mg, 20, g['dx'][g['idx'][j]], *term_set) for j in sel]
+    H = qps[0]['H']
+    A = qps[0]['A']
+    f = np.stack([q['f'] for q in qps])
+    b = np.stack([q['b'] for q in qps])
+    x, fval, flag, out, lam = bqp.quadprog(H, f, A, b, handle=handle)
+    assert (flag == 1).all(), flag
+    zs = g['z_star'][sel]
+    assert np.abs(x - zs).max() / max(1, np.abs(zs).max()) < 1e-8
+    # quadprog multiplier convention: H x + f + A'lam = 0, lam >= 0
+    for i in range(len(sel)):
+        r = H @ x[i] + f[i] + A.T @ lam['ineqlin'][i]
+        assert np.abs(r).max() < 1e-6 * (1 + np.abs(f[i]).max())
+    assert (lam['ineqlin'] >= -1e-12).all()
+
+
+def test_f2_dense_with_equalities_and_fixed_vars(mg, term_set, handle):
+    """DMS tracking LMPC (F2) at N=20 in quadprog form: equality dynamics, x_0 fixed by
+    lb == ub (DMS_tracking_LMPC_casadi.m:161-162), 105 vars."""
+    import bqp
+    from oracle import dense_qp, qp_forms
+    g = golden('dms_DMS_N50_tLMPC.npz')
+    X = g['x'][g['idx'][:4]]
+    qps = [qp_forms.dms_dense(mg, 20, x, *term_set) for x in X]
+    q0 = qps[0]
+    lb = np.stack([q['lb'] for q in qps]); ub = np.stack([q['ub'] for q in qps])
+    x, fval, flag, out, lam = bqp.quadprog(q0['H'], q0['f'], q0['A'], q0['b'], q0['Aeq'],
+                                           q0['beq'], lb, ub, handle=handle)
+    assert (flag == 1).all(), flag
+    for i, q in enumerate(qps):
+        z, fv, _, _ = dense_qp.solve(q)
+        assert np.abs(x[i] - z).max() / max(1, np.abs(z).max()) < 1e-7
+
+
+def test_box_bounds_and_infeasible_free(handle):
+    """Small random strictly convex QPs with bounds and inequalities vs the dense oracle."""
+    import bqp
+    from oracle import dense_qp, qp_forms
+    rng = np.random.default_rng(7)
+    n, m, B = 12, 30, 24
+    M = rng.standard_normal((B, n, n))
+    H = M @ np.swapaxes(M, 1, 2) + n * np.eye(n)
+    f = rng.standard_normal((B, n))
+    A = rng.standard_normal((B, m, n))
+    b = rng.uniform(0.5, 2.0, (B, m))
+    lb = -np.ones(n); ub = np.ones(n)
+    x, fval, flag, out, lam = bqp.quadprog(H, f, A, b, lb=lb, ub=ub, handle=handle)
+    assert (flag == 1).all()
+    for i in range(B):
+        z, fv, _, _ = dense_qp.solve(qp_forms.dense_qp(H[i], f[i], A[i], b[i], lb=lb, ub=ub))
+        assert np.abs(x[i] - z).max() < 1e-8
+        assert abs(fval[i] - fv) < 1e-8 * max(1, abs(fv))

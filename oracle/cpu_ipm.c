@@ -21,6 +21,8 @@
 #define MAXNS 8
 #define MAXNU 4
 #define MAXNV 12
+#define PIV_FLOOR 1e-14
+#define MU_BLOWUP 1e6     /* mu > MU_BLOWUP * min(mu) with stalled feasibility: infeasible */
 
 typedef struct {
     int nx, nu, np, ns, nv, N, mp, kp;
@@ -37,7 +39,7 @@ typedef struct {
     /* work */
     double *rs, *ru, *re, *rix, *riu, *rip;
     double *ds, *du, *dpi, *dtx, *dlx, *dtu, *dlu, *dtp, *dlp;
-    double *Ptab, *Ktab, *Rinv, *p, *qs, *qu, *wv, *qt, *kff, *f;
+    double *Ptab, *Ktab, *Rinv, *Phit, *p, *qs, *qu, *wv, *qt, *kff, *f;
     double *Dx, *Du, *FD;
     double *itx, *ilx, *itu, *ilu, *itp, *ilp;   /* 1/t, 1/lam (once per iteration) */
     double P0inv[MAXNS * MAXNS];
@@ -51,13 +53,16 @@ static int perm_of(const prob_t* P, int i) {
 }
 
 /* ---------------- small dense helpers ---------------- */
-static int chol_inv(int n, const double* M, double* Minv) {
-    /* Minv = M^{-1} for SPD n x n (n <= MAXNS) via Cholesky */
-    double L[MAXNS * MAXNS];
-    memset(L, 0, sizeof(L));
+static int chol_fac(int n, const double* M, double* L) {
+    /* lower Cholesky factor (row-major n x n, n <= MAXNS) with a static pivot floor.  The
+     * factor is applied by substitution (chol_solve): an explicit inverse of the
+     * ill-conditioned Rhat near convergence loses the stationarity residual. */
+    for (int i = 0; i < n * n; ++i) L[i] = 0.0;
     for (int j = 0; j < n; ++j) {
         double d = M[j * n + j];
         for (int k = 0; k < j; ++k) d -= L[j * n + k] * L[j * n + k];
+        /* static pivot floor: cancellation near convergence must not stop the iteration */
+        if (!(d > PIV_FLOOR * M[j * n + j])) d = PIV_FLOOR * M[j * n + j];
         if (!(d > 0)) return -1;
         d = sqrt(d);
         L[j * n + j] = d;
@@ -67,24 +72,21 @@ static int chol_inv(int n, const double* M, double* Minv) {
             L[i * n + j] = v / d;
         }
     }
-    /* inverse of L, then Minv = L^-T L^-1 */
-    double Li[MAXNS * MAXNS];
-    memset(Li, 0, sizeof(Li));
-    for (int i = 0; i < n; ++i) {
-        Li[i * n + i] = 1.0 / L[i * n + i];
-        for (int j = 0; j < i; ++j) {
-            double v = 0;
-            for (int k = j; k < i; ++k) v -= L[i * n + k] * Li[k * n + j];
-            Li[i * n + j] = v / L[i * n + i];
-        }
-    }
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) {
-            double v = 0;
-            for (int k = (i > j ? i : j); k < n; ++k) v += Li[k * n + i] * Li[k * n + j];
-            Minv[i * n + j] = v;
-        }
     return 0;
+}
+
+static void chol_solve(int n, const double* L, double* b) {
+    /* b <- (L L')^{-1} b */
+    for (int i = 0; i < n; ++i) {
+        double v = b[i];
+        for (int k = 0; k < i; ++k) v -= L[i * n + k] * b[k];
+        b[i] = v / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = b[i];
+        for (int k = i + 1; k < n; ++k) v -= L[k * n + i] * b[k];
+        b[i] = v / L[i * n + i];
+    }
 }
 
 /* ---------------- residuals ---------------- */
@@ -260,18 +262,18 @@ static int factor(const prob_t* P, work_t* W) {
                 }
                 Mu[x][j] = HT(k, ns + x, j) + acc;
             }
-        double Ruu[MAXNU * MAXNU], Ri[MAXNU * MAXNU];
+        double Ruu[MAXNU * MAXNU];
+        double* Lk = W->Rinv + (size_t)k * nu * nu;    /* Cholesky factor of Rhat_k */
         for (int a = 0; a < nu; ++a)
             for (int b = 0; b < nu; ++b) Ruu[a * nu + b] = Mu[a][ns + b];
-        if (chol_inv(nu, Ruu, Ri)) return -1;
+        if (chol_fac(nu, Ruu, Lk)) return -1;
         double* Kk = W->Ktab + (size_t)k * nu * ns;
-        for (int a = 0; a < nu; ++a)
-            for (int j = 0; j < ns; ++j) {
-                double v = 0;
-                for (int b = 0; b < nu; ++b) v -= Ri[a * nu + b] * Mu[b][j];
-                Kk[a * ns + j] = v;
-            }
-        for (int a = 0; a < nu * nu; ++a) W->Rinv[(size_t)k * nu * nu + a] = Ri[a];
+        for (int j = 0; j < ns; ++j) {
+            double col[MAXNU];
+            for (int b = 0; b < nu; ++b) col[b] = -Mu[b][j];
+            chol_solve(nu, Lk, col);
+            for (int a = 0; a < nu; ++a) Kk[a * ns + j] = col[a];
+        }
         /* Joseph form: P_k = [I;K]' Ht [I;K] + Phi' Pn Phi,  Phi = Abar + Bbar K */
         double Phi[MAXNS][MAXNS];
         for (int a = 0; a < ns; ++a)
@@ -281,6 +283,9 @@ static int factor(const prob_t* P, work_t* W) {
                 Phi[a][j] = v;
             }
         double* Pk = W->Ptab + (size_t)k * ns * ns;
+        double* Phk = W->Phit + (size_t)k * ns * ns;   /* closed loop Phi_k, row-major */
+        for (int a = 0; a < ns; ++a)
+            for (int j = 0; j < ns; ++j) Phk[a * ns + j] = Phi[a][j];
         for (int i = 0; i < ns; ++i)
             for (int j = i; j < ns; ++j) {
                 double v = HT(k, i, j);
@@ -307,7 +312,7 @@ static int factor(const prob_t* P, work_t* W) {
         const double* P0 = W->Ptab;
         for (int a = 0; a < np; ++a)
             for (int b = 0; b < np; ++b) Pt[a * np + b] = P0[(nx + a) * ns + nx + b];
-        if (chol_inv(np, Pt, W->P0inv)) return -1;
+        if (chol_fac(np, Pt, W->P0inv)) return -1;    /* factor of P_0[theta,theta] */
     }
     return 0;
 }
@@ -361,21 +366,15 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             W->qt[k * ns + i] = q;
         }
     }
-    /* backward sweep: y = p_{k+1} + w_k;  p_k = Abar' y + K_k' (Bbar' y) + qt_k */
+    /* backward sweep: p_k = Phi_k' (p_{k+1} + w_k) + qt_k   (= Abar'y + K'(Bbar'y) + qt) */
     for (int i = 0; i < ns; ++i) W->p[N * ns + i] = W->qs[N * ns + i];
     for (int k = N - 1; k >= 0; --k) {
-        double y[MAXNS], by[MAXNU];
-        const double* Kk = W->Ktab + (size_t)k * nu * ns;
+        double y[MAXNS];
+        const double* Phk = W->Phit + (size_t)k * ns * ns;
         for (int i = 0; i < ns; ++i) y[i] = W->p[(k + 1) * ns + i] + W->wv[k * ns + i];
-        for (int a = 0; a < nu; ++a) {
-            double v = 0;
-            for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * y[j];
-            by[a] = v;
-        }
         for (int i = 0; i < ns; ++i) {
             double v = W->qt[k * ns + i];
-            for (int j = 0; j < ns; ++j) v += P->Abar[j][i] * y[j];
-            for (int a = 0; a < nu; ++a) v += Kk[a * ns + i] * by[a];
+            for (int j = 0; j < ns; ++j) v += Phk[j * ns + i] * y[j];
             W->p[k * ns + i] = v;
         }
     }
@@ -388,38 +387,29 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * y[j];
             r[a] = v;
         }
-        const double* Ri = W->Rinv + (size_t)k * nu * nu;
-        for (int a = 0; a < nu; ++a) {
-            double v = 0;
-            for (int b = 0; b < nu; ++b) v -= Ri[a * nu + b] * r[b];
-            W->kff[k * nu + a] = v;
-        }
+        for (int a = 0; a < nu; ++a) r[a] = -r[a];
+        chol_solve(nu, W->Rinv + (size_t)k * nu * nu, r);
+        for (int a = 0; a < nu; ++a) W->kff[k * nu + a] = r[a];
         for (int i = 0; i < ns; ++i) {
             double v = W->re[k * ns + i];
             for (int a = 0; a < nu; ++a) v += P->Bbar[i][a] * W->kff[k * nu + a];
             W->f[k * ns + i] = v;
         }
     }
-    /* theta_0 step and forward sweep: ds_{k+1} = Abar ds_k + Bbar (K_k ds_k) + f_k */
+    /* theta_0 step and forward sweep: ds_{k+1} = Phi_k ds_k + f_k */
     for (int i = 0; i < nx; ++i) W->ds[i] = 0.0;
-    for (int a = 0; a < np; ++a) {
-        double v = 0;
-        for (int b = 0; b < np; ++b) v -= W->P0inv[a * np + b] * W->p[nx + b];
-        W->ds[nx + a] = v;
+    {
+        double r[MAXNS];
+        for (int a = 0; a < np; ++a) r[a] = -W->p[nx + a];
+        chol_solve(np, W->P0inv, r);
+        for (int a = 0; a < np; ++a) W->ds[nx + a] = r[a];
     }
     for (int k = 0; k < N; ++k) {
-        const double* Kk = W->Ktab + (size_t)k * nu * ns;
+        const double* Phk = W->Phit + (size_t)k * ns * ns;
         const double* d = W->ds + k * ns;
-        double kd[MAXNU];
-        for (int a = 0; a < nu; ++a) {
-            double v = 0;
-            for (int j = 0; j < ns; ++j) v += Kk[a * ns + j] * d[j];
-            kd[a] = v;
-        }
         for (int i = 0; i < ns; ++i) {
             double v = W->f[k * ns + i];
-            for (int j = 0; j < ns; ++j) v += P->Abar[i][j] * d[j];
-            for (int a = 0; a < nu; ++a) v += P->Bbar[i][a] * kd[a];
+            for (int j = 0; j < ns; ++j) v += Phk[i * ns + j] * d[j];
             W->ds[(k + 1) * ns + i] = v;
         }
     }
@@ -608,11 +598,14 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     }
     /* main loop */
     int flag = 0, it;
-    double mu = 0;
+    double mu = 0, mu_min = INFINITY;
     for (it = 0; it <= op->max_iter; ++it) {
         residuals(P, W, &stat, &feas, &cs, &mc, &gs);
         mu = cs / (mc > 0 ? mc : 1);
         if (stat <= op->tol_stat * (1.0 + gs) && feas <= op->tol_feas * (1.0 + bs) && mu <= op->tol_comp) { flag = 1; break; }
+        if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
+        if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bs)) { flag = -2; break; }
+        if (mu < mu_min) mu_min = mu;
         if (it == op->max_iter) break;
         if (factor(P, W)) { flag = -8; break; }
         for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i];
@@ -690,6 +683,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.dtu = alloc0(N * nu * 2); W.dlu = alloc0(N * nu * 2);
         W.dtp = alloc0(mp); W.dlp = alloc0(mp);
         W.Ptab = alloc0((size_t)(N + 1) * ns * ns); W.Ktab = alloc0((size_t)N * nu * ns);
+        W.Phit = alloc0((size_t)N * ns * ns);
         W.Rinv = alloc0((size_t)N * nu * nu); W.p = alloc0((N + 1) * ns);
         W.qs = alloc0((N + 1) * ns); W.qu = alloc0(N * nu); W.wv = alloc0(N * ns);
         W.qt = alloc0(N * ns); W.kff = alloc0(N * nu); W.f = alloc0(N * ns);
@@ -763,7 +757,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.uub); free(W.hp); free(W.tx); free(W.lx); free(W.tu); free(W.lu); free(W.tp);
         free(W.lp); free(W.rs); free(W.ru); free(W.re); free(W.rix); free(W.riu); free(W.rip);
         free(W.ds); free(W.du); free(W.dpi); free(W.dtx); free(W.dlx); free(W.dtu); free(W.dlu);
-        free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Ktab); free(W.Rinv); free(W.p);
+        free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Phit); free(W.Ktab); free(W.Rinv); free(W.p);
         free(W.qs); free(W.qu); free(W.wv); free(W.qt); free(W.kff); free(W.f); free(W.Dx);
         free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
         free(W.ilp);

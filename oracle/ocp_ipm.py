@@ -138,6 +138,32 @@ def _comp_sum(o, st, dt=None, dl=None, a=0.0):
     return tot
 
 
+PIV_FLOOR = 1e-14      # static Cholesky pivot floor (relative to the diagonal entry)
+MU_BLOWUP = 1e6        # mu growing by this factor with stalled feasibility -> infeasible (-2)
+
+
+def chol_floor(M):
+    n = M.shape[0]
+    L = np.zeros_like(M)
+    for j in range(n):
+        d = M[j, j] - L[j, :j] @ L[j, :j]
+        if not d > PIV_FLOOR * M[j, j]:
+            d = PIV_FLOOR * M[j, j]
+        if not d > 0:
+            raise np.linalg.LinAlgError('not positive definite')
+        L[j, j] = np.sqrt(d)
+        for i in range(j + 1, n):
+            L[i, j] = (M[i, j] - L[i, :j] @ L[j, :j]) / L[j, j]
+    return L
+
+
+def chol_solve(L, b):
+    """(L L')^{-1} b by substitution (never an explicit inverse: see oracle/cpu_ipm.c)."""
+    import scipy.linalg as sla
+    y = sla.solve_triangular(L, b, lower=True)
+    return sla.solve_triangular(L.T, y, lower=False)
+
+
 def riccati_factor(o, st):
     """Backward factorisation of the reduced KKT; returns per-stage (Rhat chol, K, Hs, P)."""
     N, nx, ns, nu = o.N, o.nx, o.ns, o.nu
@@ -166,8 +192,8 @@ def riccati_factor(o, st):
         PB = P[k + 1] @ B
         Rh = R + B.T @ PB
         Shat = S + B.T @ PA
-        Lk = np.linalg.cholesky(Rh)
-        Kk = -np.linalg.solve(Rh, Shat)
+        Lk = chol_floor(Rh)
+        Kk = -chol_solve(Lk, Shat)
         # stabilised (Joseph) form: sum of PSD terms, no cancellation near convergence
         Phi = A + B @ Kk
         P[k] = Q + S.T @ Kk + Kk.T @ S + Kk.T @ R @ Kk + Phi.T @ P[k + 1] @ Phi
@@ -203,12 +229,12 @@ def riccati_solve(o, st, fac, rs, ru, re, ri, rc):
     for k in range(N - 1, -1, -1):
         Pe = P[k + 1] @ re[k] + p[k + 1]
         rh = qu[k] + B.T @ Pe
-        kk = -np.linalg.solve(fac['L'][k] @ fac['L'][k].T, rh)
+        kk = -chol_solve(fac['L'][k], rh)
         p[k] = qs[k] + A.T @ Pe + fac['Sh'][k].T @ kk
         kff[k] = kk
     ds = np.zeros((N + 1, ns)); du = np.zeros((N, nu)); dpi = np.zeros((N + 1, ns))
     th = slice(nx, ns)
-    ds[0, th] = -np.linalg.solve(P[0][th, th], p[0][th])
+    ds[0, th] = -chol_solve(chol_floor(P[0][th, th]), p[0][th])
     for k in range(N):
         du[k] = fac['K'][k] @ ds[k] + kff[k]
         ds[k + 1] = A @ ds[k] + B @ du[k] + re[k]
@@ -287,6 +313,7 @@ def solve(d, x0, w=None, opts=None, trace=None):
     m = max(o.m, 1)
     exitflag = 0
     it = 0
+    mu_min = np.inf
     for it in range(op['max_iter'] + 1):
         rs, ru, re, ri = residuals(o, st)
         mu = _comp_sum(o, st) / m
@@ -299,6 +326,10 @@ def solve(d, x0, w=None, opts=None, trace=None):
                 and mu <= op['tol_comp']):
             exitflag = 1
             break
+        if mu > MU_BLOWUP * mu_min and r_feas > 1e-6 * (1.0 + o.bscale):
+            exitflag = -2
+            break
+        mu_min = min(mu_min, mu)
         if it == op['max_iter']:
             break
         fac = riccati_factor(o, st)

@@ -42,6 +42,7 @@ struct bqp_handle_s {
     DevBuf work;   // tables + stats (device entry points)
     DevBuf stage;  // staging of host-pointer calls
     DevBuf dwork;  // dense per-instance scratch
+    int last_batch = 0;
 };
 
 namespace {
@@ -189,19 +190,21 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     const int hstride = nv * nv + 1;
     const int mpad = std::max(64, ((mp + 63) / 64) * 64);
     const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;
-    const int per_wave = bqp::ocp_wave_lds_doubles(N, nx, nu, np);
+    const int per_wave = bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
     const size_t lds_budget = 160 * 1024 / sizeof(double);
     int wpb = 4;
     while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
     if ((size_t)shared_doubles + (size_t)per_wave > lds_budget) return BQP_E_UNSUPPORTED;
     // workspace: H, Fp, stats
     const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * 4;
+#ifdef BQP_STAMPS
+    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + (size_t)batch * 16)));
+#else
     HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8)));
+#endif
     double* Hd = (double*)h->work.p;
     double* Fd = Hd + nH;
     double* Sd = Fd + nF;
-    static const double zero = 0.0;
-    (void)zero;
     HIP_TRY(bqp::launch_ocp_prep(D->W, mp > 0 ? D->Fp : D->W, nx, nu, np, N, mp, d->poly_stage,
                                  hstride, mpad, Hd, Fd, st));
     bqp::OcpKernelArgs a;
@@ -220,6 +223,10 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         a.pi_out = duals->pi; a.lamx_out = duals->lam_x; a.lamu_out = duals->lam_u;
         a.lamp_out = duals->lam_p;
     }
+#ifdef BQP_STAMPS
+    a.stamps = Sd + nS + 8;
+    h->last_batch = batch;
+#endif
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
     HIP_TRY(hipEventRecord(h->ev1, st));
@@ -425,5 +432,20 @@ int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_s
     HIP_TRY(hipStreamSynchronize(h->stream));
     return BQP_OK;
 }
+
+#ifdef BQP_STAMPS
+// diagnostic build only: per-instance phase cycle counts of the last structured solve
+int bqp_debug_stamps(bqp_handle h, int N, int nv, int mp, double* out) {
+    if (!h || !out) return BQP_E_ARG;
+    DevScope ds(h->device);
+    const int hstride = nv * nv + 1;
+    const int mpad = std::max(64, ((mp + 63) / 64) * 64);
+    const size_t off = (size_t)(N + 1) * hstride + (size_t)nv * mpad + (size_t)h->last_batch * 4 + 8;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, (double*)h->work.p + off, sizeof(double) * h->last_batch * 16, hipMemcpyDeviceToHost));
+    return BQP_OK;
+}
+#endif
 
 }  // extern "C"

@@ -21,11 +21,12 @@ struct OcpKernelArgs {
     int* exitflag;
     double* stats;  // batch x 4: iterations, stationarity, feasibility, mu
     double *pi_out, *lamx_out, *lamu_out, *lamp_out;
+    double* stamps;  // diagnostic build (BQP_STAMPS): batch x 16 phase cycle counts
 };
 
 bool ocp_supported(int nx, int nu, int np);
 int ocp_rpl_for(int mp);
-int ocp_wave_lds_doubles(int N, int nx, int nu, int np);
+int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad);
 hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,

@@ -3,16 +3,19 @@
 // One wavefront (64 lanes) solves one MPC instance; a workgroup holds WPB instances that share
 // the stage-cost table H_k and the polytope (terminal-set) matrix in LDS.  Inside a wave the
 // lanes are re-assigned per phase:
-//   * stage phases   lane k (and k+64 when SPL=2) owns stage k: s_k=[x_k;theta], u_k, pi_k,
-//                    the box rows of stage k (residuals, Newton right-hand sides, recoveries);
-//   * polytope rows  lane l owns rows l, l+64, ... (RPL rows): slacks/duals in registers,
-//                    F_T'DF_T and F_T'e reduced with wave shuffles;
-//   * Riccati factor lane (i,j) owns entry (i,j) of the (NS+NU)^2 stage matrix; P_{k+1} is
-//                    broadcast from LDS each stage (sequential over k);
-//   * Riccati solves every lane runs the (NS)-vector recursion redundantly (no cross-lane
-//                    traffic on the sequential critical path), streaming K_k / vectors from LDS.
-// The algorithm (and its operation order) is the one stated in oracle/ocp_ipm.py and restated
-// in C in oracle/cpu_ipm.c; the QP is the stage-wise form of the reference's per-step OCPs
+//   * stage phases   lane k (and k+64 when SPL=2) owns stage k: s_k=[x_k;theta], u_k, pi_k
+//                    and the slacks/duals of the box rows of stage k;
+//   * polytope rows  lane l owns rows l, l+64, ... (RPL rows): slack, dual, 1/slack in
+//                    registers; F'DF and F'e are reduced with DPP lane moves;
+//   * Riccati factor lane (i,j) owns entry (i,j) of the stage matrices (Joseph form); P_{k+1}
+//                    is broadcast from LDS at each stage (sequential over k);
+//   * Riccati solves every lane runs the NS-vector closed-loop recursion redundantly (no
+//                    cross-lane traffic on the sequential critical path).
+// Register budget (one wave per SIMD at the C2 batch): per-row residuals and steps are
+// recomputed from the stage vectors when needed instead of being kept live, so the kernel
+// holds ~85 fp64 values per lane.
+// The algorithm (and its operation order) is stated in oracle/ocp_ipm.py and restated in C in
+// oracle/cpu_ipm.c; the QP is the stage-wise form of the reference's per-step OCPs
 // (costLMPC.m / constraintsLMPC.m, DMS_tracking_LMPC_casadi.m:223-287, trackingMPC/costFunction.m).
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -23,6 +26,8 @@
 namespace bqp {
 
 #define WAVE 64
+#define PIV_FLOOR 1e-14
+#define MU_BLOWUP 1e6
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -31,9 +36,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // Wave-wide reductions on DPP lane moves (quad_perm xor1/xor2, row_half_mirror, row_mirror
-// inside each 16-lane row, then row_bcast15/31 across rows) + one readlane of lane 63: no LDS
-// traffic, result uniform (SGPR) in every lane.  EXEC must be full (all call sites are
-// wave-uniform).
+// inside each 16-lane row, then row_bcast15/31 across rows) + a readlane of lane 63: no LDS
+// traffic, result uniform in every lane.  EXEC must be full (all call sites are wave-uniform).
 template <int CTRL, int ROWM>
 __device__ __forceinline__ double dpp_mov(double old, double v) {
     const int2 o = __builtin_bit_cast(int2, old);
@@ -68,40 +72,70 @@ __device__ __forceinline__ double wmax(double v) {
     v = fmax(v, dpp_mov<0x143, 0xc>(-INFINITY, v));
     return lane63(v);
 }
-__device__ __forceinline__ double wmin(double v) {
-    v = fmin(v, dpp_mov<0xB1, 0xf>(INFINITY, v));
-    v = fmin(v, dpp_mov<0x4E, 0xf>(INFINITY, v));
-    v = fmin(v, dpp_mov<0x141, 0xf>(INFINITY, v));
-    v = fmin(v, dpp_mov<0x140, 0xf>(INFINITY, v));
-    v = fmin(v, dpp_mov<0x142, 0xa>(INFINITY, v));
-    v = fmin(v, dpp_mov<0x143, 0xc>(INFINITY, v));
-    return lane63(v);
+__device__ __forceinline__ double wmin(double v) { return -wmax(-v); }
+
+// Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
+template <int N>
+__device__ __forceinline__ bool chol_small(const double (&M)[N][N], double (&L)[N][N]) {
+    bool ok = true;
+    double d0 = M[0][0];
+    if (!(d0 > PIV_FLOOR * M[0][0])) d0 = PIV_FLOOR * M[0][0];
+    ok = ok && (d0 > 0.0);
+    L[0][0] = sqrt(d0);
+    if constexpr (N == 2) {
+        L[0][1] = 0.0;
+        L[1][0] = M[1][0] / L[0][0];
+        double d1 = M[1][1] - L[1][0] * L[1][0];
+        if (!(d1 > PIV_FLOOR * M[1][1])) d1 = PIV_FLOOR * M[1][1];
+        ok = ok && (d1 > 0.0);
+        L[1][1] = sqrt(d1);
+    }
+    return ok;
+}
+// b <- (L L')^{-1} b   (substitution, same order as oracle/cpu_ipm.c chol_solve); L row-major
+template <int N>
+__device__ __forceinline__ void chol_solve_small(const double* L, double (&b)[N]) {
+    if constexpr (N == 2) {
+        b[0] = b[0] / L[0];
+        b[1] = (b[1] - L[2] * b[0]) / L[3];
+        b[1] = b[1] / L[3];
+        b[0] = (b[0] - L[2] * b[1]) / L[0];
+    } else {
+        b[0] = b[0] / L[0];
+        b[0] = b[0] / L[0];
+    }
 }
 
 // Per-wave LDS layout (in doubles), all sized from N at run time.
 struct WaveLds {
-    int P, K, Ri, xs, xpi, xu, p, wv, qt, fv, dsv, duv, qu, Dx, Du, FD, M, gp, misc, total;
-    __host__ __device__ static WaveLds make(int N, int NX, int NU, int NS, int NV) {
+    int P, Phi, K, Lr, xs, xu, qt_xpi, rs, ru, re, pv, wv, qu, fv, dsv, duv, Dx, Du, FD, Mu, AB, L0, prp, misc, total;
+    __host__ __device__ static WaveLds make(int N, int NX, int NU, int NP, int mpad, bool store_phi) {
+        const int NS = NX + NP, NV = NS + NU;
         WaveLds o;
         int c = 0;
         o.P = c;   c += (N + 1) * NS * NS;
+        o.Phi = c; c += store_phi ? N * NS * NS : 0;
         o.K = c;   c += N * NU * NS;
-        o.Ri = c;  c += N * NU * NU;
+        o.Lr = c;  c += N * NU * NU;
         o.xs = c;  c += (N + 1) * NS;
-        o.xpi = c; c += (N + 1) * NS;
         o.xu = c;  c += (N + 1) * NU;
-        o.p = c;   c += (N + 1) * NS;
+        o.qt_xpi = c; c += (N + 1) * NS;   // pi exchange in residuals, qt in the solves
+        o.rs = c;  c += (N + 1) * NS;
+        o.ru = c;  c += (N + 1) * NU;
+        o.re = c;  c += (N + 1) * NS;
+        o.pv = c;  c += (N + 1) * NS;
         o.wv = c;  c += (N + 1) * NS;
-        o.qt = c;  c += (N + 1) * NS;
+        o.qu = c;  c += (N + 1) * NU;
         o.fv = c;  c += (N + 1) * NS;
         o.dsv = c; c += (N + 1) * NS;
         o.duv = c; c += (N + 1) * NU;
-        o.qu = c;  c += (N + 1) * NU;
         o.Dx = c;  c += (N + 1) * NX;
         o.Du = c;  c += (N + 1) * NU;
         o.FD = c;  c += NV * NV;
-        o.M = c;   c += NV * NV;
-        o.gp = c;  c += NV;
+        o.Mu = c;  c += NU * NV;
+        o.AB = c;  c += NS * NS + NS * NU;
+        o.L0 = c;  c += NP * NP;
+        o.prp = c; c += mpad;              // predictor dt*dlam of the polytope rows
         o.misc = c; c += 8;
         o.total = (c + 1) & ~1;
         return o;
@@ -112,90 +146,80 @@ template <int NX, int NU, int NP, int SPL, int RPL>
 __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
+    constexpr bool kPhi = (SPL == 1);     // store closed-loop Phi_k (LDS budget allows at N<64)
     extern __shared__ double lds[];
     const int N = a.N, mp = a.mp, kp = a.kp;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int hstride = a.hstride;          // padded NV*NV (+1) per stage
+    const int hstride = a.hstride;
+    const int mpad = a.mpad;
     // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
     double* Hs = lds;
     double* Fs = lds + (N + 1) * hstride;
-    const int mpad = a.mpad;
     for (int i = threadIdx.x; i < (N + 1) * hstride; i += blockDim.x) Hs[i] = a.H[i];
     for (int i = threadIdx.x; i < NV * mpad; i += blockDim.x) Fs[i] = a.Fp[i];
     __syncthreads();
     const int inst = blockIdx.x * a.wpb + wid;
     if (inst >= a.batch) return;
-    const WaveLds L = WaveLds::make(N, NX, NU, NS, NV);
+    const WaveLds L = WaveLds::make(N, NX, NU, NP, mpad, kPhi);
     double* W = lds + a.shared_doubles + wid * L.total;
+#ifdef BQP_STAMPS
+    // diagnostic build only (see tools/stamps.py): cycles per phase, summed over the solve
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+    unsigned long long st_acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) st_acc[i] = 0;
+#define STAMP(id)                                                          \
+    do {                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                     \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();        \
+        st_acc[id] += _t - st_last;                                        \
+        st_last = _t;                                                      \
+    } while (0)
+#else
+#define STAMP(id) do { } while (0)
+#endif
 
-    // ---------------- per-instance model (wave-uniform) -------------------------------------
-    double Ab[NS][NS], Bb[NS][NU], cb[NS];
+    // ---------------- per-instance model -> LDS (Abar row-major, Bbar) ---------------------
     {
         const double* A = a.A + (int64_t)inst * a.sA;
         const double* B = a.B + (int64_t)inst * a.sB;
-#pragma unroll
-        for (int i = 0; i < NS; ++i) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j)
-                Ab[i][j] = (i < NX && j < NX) ? A[j * NX + i] : (i == j ? 1.0 : 0.0);
-#pragma unroll
-            for (int j = 0; j < NU; ++j) Bb[i][j] = (i < NX) ? B[j * NX + i] : 0.0;
-            cb[i] = (i < NX && a.c) ? a.c[(int64_t)inst * a.sc + i] : 0.0;
+        if (lane < NS * NS) {
+            const int i = lane / NS, j = lane % NS;
+            W[L.AB + lane] = (i < NX && j < NX) ? A[j * NX + i] : (i == j ? 1.0 : 0.0);
+        }
+        if (lane < NS * NU) {
+            const int i = lane / NU, j = lane % NU;
+            W[L.AB + NS * NS + lane] = (i < NX) ? B[j * NX + i] : 0.0;
         }
     }
-    // Riccati-factor lane roles (columns kept in registers, constant over the stages):
-    //   phase A  lane (xa, ja), xa < NU, ja < NV : input row M_{u_xa, ja} = Ht + Bbar_xa' P F_ja
-    //   phase B  lane (ib, jb), ib <= jb < NS    : P_k(ib, jb) in Joseph form
-    const int xa = lane / NV, ja = lane % NV;
-    const bool alane = lane < NU * NV;
-    const int ib = lane / NS, jb = lane % NS;
-    const bool blane = lane < NS * NS && ib <= jb;
-    double FjA[NS], BxA[NS], AiB[NS], AjB[NS];
+    wave_sync();
+    auto Abar = [&](int i, int j) __attribute__((always_inline)) -> double { return W[L.AB + i * NS + j]; };
+    auto Bbar = [&](int i, int j) __attribute__((always_inline)) -> double { return W[L.AB + NS * NS + i * NU + j]; };
+    double cb[NS];
 #pragma unroll
-    for (int a_ = 0; a_ < NS; ++a_) {
-        double vf = 0, vb = 0, vi = 0, vj = 0;
-#pragma unroll
-        for (int c = 0; c < NV; ++c) {
-            const double f = (c < NS) ? Ab[a_][c < NS ? c : 0] : Bb[a_][c >= NS ? c - NS : 0];
-            vf = (c == ja) ? f : vf;
-        }
-#pragma unroll
-        for (int c = 0; c < NU; ++c) vb = (c == xa) ? Bb[a_][c] : vb;
-#pragma unroll
-        for (int c = 0; c < NS; ++c) {
-            vi = (c == ib) ? Ab[a_][c] : vi;
-            vj = (c == jb) ? Ab[a_][c] : vj;
-        }
-        FjA[a_] = vf; BxA[a_] = vb; AiB[a_] = vi; AjB[a_] = vj;
-    }
+    for (int i = 0; i < NS; ++i) cb[i] = (i < NX && a.c) ? a.c[(int64_t)inst * a.sc + i] : 0.0;
 
     // ---------------- stage-lane state ------------------------------------------------------
-    double s[SPL][NS], u[SPL][NU], pi[SPL][NS], g[SPL][NV];
-    double tx[SPL][NX][2], lx[SPL][NX][2], bx[SPL][NX][2];   // slack, dual, bound (ub, lb)
-    double tu[SPL][NU][2], lu[SPL][NU][2], bu[SPL][NU][2];
-    unsigned mx[SPL], mu_[SPL];                               // presence bits (2 per comp)
+    double s[SPL][NS], u[SPL][NU], pi[SPL][NS];
+    double tx[SPL][NX][2], lx[SPL][NX][2], itx[SPL][NX][2], bx[SPL][NX][2];   // ub, lb
+    double tu[SPL][NU][2], lu[SPL][NU][2], itu[SPL][NU][2], bu[SPL][NU][2];
+    double prx[SPL][NX][2], pru[SPL][NU][2];                                    // predictor dt*dlam
+    double kff[SPL][NU];
+    unsigned mx[SPL], mu_[SPL];
     const double* x0 = a.x0 + (int64_t)inst * a.sx0;
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
         const int k = lane + WAVE * j;
         const bool act = k <= N;
-        const int kk = act ? k : N;
         mx[j] = 0; mu_[j] = 0;
 #pragma unroll
         for (int i = 0; i < NS; ++i) { s[j][i] = 0.0; pi[j][i] = 0.0; }
 #pragma unroll
-        for (int i = 0; i < NU; ++i) u[j][i] = 0.0;
+        for (int i = 0; i < NU; ++i) { u[j][i] = 0.0; kff[j][i] = 0.0; }
         if (k == 0) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) s[j][i] = x0[i];
-        }
-        // linear term, permuted [x th u] from external [x u th]
-        const double* wk = a.w ? a.w + (int64_t)inst * a.sw + (int64_t)kk * NV : nullptr;
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            const int e = (i < NX) ? i : (i < NS ? NX + NU + (i - NX) : NX + (i - NS));
-            g[j][i] = (wk && act && !(k == N && i >= NS)) ? wk[e] : 0.0;
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
@@ -220,28 +244,26 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             if (isfinite(lb)) mu_[j] |= 2u << (2 * i);
         }
     }
+    auto xpres = [&](int j, int i, int h) __attribute__((always_inline)) -> bool { return (mx[j] >> (2 * i + h)) & 1u; };
+    auto upres = [&](int j, int i, int h) __attribute__((always_inline)) -> bool { return (mu_[j] >> (2 * i + h)) & 1u; };
+    // linear cost term of stage k, internal index i ([x; theta; u] from external [x; u; theta])
+    const double* wb = a.w ? a.w + (int64_t)inst * a.sw : nullptr;
+    auto gterm = [&](int k, int i) __attribute__((always_inline)) -> double {
+        if (!wb || (k == N && i >= NS)) return 0.0;
+        const int e = (i < NX) ? i : (i < NS ? NX + NU + (i - NX) : NX + (i - NS));
+        return wb[(int64_t)k * NV + e];
+    };
     // polytope rows
-    double tp[RPL], lp[RPL], hp[RPL];
+    double tp[RPL], lp[RPL], itp[RPL];
     const double* hpi = a.hp + (int64_t)inst * a.shp;
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-        const int r = lane + WAVE * q;
-        hp[q] = (r < mp) ? hpi[r] : 0.0;
-    }
-    // row count
-    double mcount = 0;
-#pragma unroll
-    for (int j = 0; j < SPL; ++j) mcount += __builtin_popcount(mx[j]) + __builtin_popcount(mu_[j]);
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) mcount += (lane + WAVE * q < mp) ? 1.0 : 0.0;
-    mcount = wsum(mcount);
-    const double minv = 1.0 / fmax(mcount, 1.0);
-    // scale of the primal data for the relative feasibility test
-    double bsl = 0.0;
+    auto prow = [&](int q) __attribute__((always_inline)) -> bool { return lane + WAVE * q < mp; };
+
+    // row count and primal data scale
+    double mcount = 0, bsl = 0;
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
-        const int k = lane + WAVE * j;
-        if (k == 0) {
+        mcount += __builtin_popcount(mx[j]) + __builtin_popcount(mu_[j]);
+        if (lane + WAVE * j == 0) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) bsl = fmax(bsl, fabs(x0[i]));
         }
@@ -249,59 +271,64 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         for (int i = 0; i < NX; ++i)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                if ((mx[j] >> (2 * i + h)) & 1u) bsl = fmax(bsl, fabs(bx[j][i][h]));
+                if (xpres(j, i, h)) bsl = fmax(bsl, fabs(bx[j][i][h]));
 #pragma unroll
         for (int i = 0; i < NU; ++i)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                if ((mu_[j] >> (2 * i + h)) & 1u) bsl = fmax(bsl, fabs(bu[j][i][h]));
+                if (upres(j, i, h)) bsl = fmax(bsl, fabs(bu[j][i][h]));
     }
 #pragma unroll
     for (int q = 0; q < RPL; ++q)
-        if (lane + WAVE * q < mp) bsl = fmax(bsl, fabs(hp[q]));
+        if (prow(q)) { mcount += 1.0; bsl = fmax(bsl, fabs(hpi[lane + WAVE * q])); }
+    mcount = wsum(mcount);
+    const double minv = 1.0 / fmax(mcount, 1.0);
     const double bscale = wmax(bsl);
 
-    // residual registers
-    double rs[SPL][NS], ru[SPL][NU], re[SPL][NS], rix[SPL][NX][2], riu[SPL][NU][2], rip[RPL];
-    // step registers
-    double ds[SPL][NS], du[SPL][NU], dpi[SPL][NS], dtx[SPL][NX][2], dlx[SPL][NX][2];
-    double dtu[SPL][NU][2], dlu[SPL][NU][2], dtp[RPL], dlp[RPL];
-    double rcx[SPL][NX][2], rcu[SPL][NU][2], rcp[RPL];   // complementarity rhs
-    double kff[SPL][NU];
-    double itx[SPL][NX][2], itu[SPL][NU][2], itp[RPL];   // 1/t, once per iteration
+    // ----- helpers: box / polytope row residuals and steps (recomputed, never stored) -------
+    auto rix = [&](int j, int i, int h) __attribute__((always_inline)) -> double {
+        return h == 0 ? s[j][i] + tx[j][i][0] - bx[j][i][0] : -s[j][i] + tx[j][i][1] + bx[j][i][1];
+    };
+    auto riu = [&](int j, int i, int h) __attribute__((always_inline)) -> double {
+        return h == 0 ? u[j][i] + tu[j][i][0] - bu[j][i][0] : -u[j][i] + tu[j][i][1] + bu[j][i][1];
+    };
+    auto load_vp = [&](double (&vp)[NV], int base_s, int base_u) {
+#pragma unroll
+        for (int c = 0; c < NS; ++c) vp[c] = W[base_s + kp * NS + c];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) vp[NS + c] = (kp < N) ? W[base_u + kp * NU + c] : 0.0;
+    };
+    auto fdot = [&](int r, const double (&v)[NV]) -> double {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) acc += Fs[c * mpad + r] * v[c];
+        return acc;
+    };
 
-    auto xpres = [&](int j, int i, int h) -> bool { return (mx[j] >> (2 * i + h)) & 1u; };
-    auto upres = [&](int j, int i, int h) -> bool { return (mu_[j] >> (2 * i + h)) & 1u; };
-
-    // ======================= residuals (stat, feas, comp sum) ==============================
-    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) {
-        // publish s, u, pi for neighbour / polytope stage access
+    // ======================= residuals =====================================================
+    // writes rs, ru, re (per stage) to LDS; returns stat, feas, comp sum, cost-gradient scale
+    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k <= N) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) { W[L.xs + k * NS + i] = s[j][i]; W[L.xpi + k * NS + i] = pi[j][i]; }
+                for (int i = 0; i < NS; ++i) { W[L.xs + k * NS + i] = s[j][i]; W[L.qt_xpi + k * NS + i] = pi[j][i]; }
 #pragma unroll
                 for (int i = 0; i < NU; ++i) W[L.xu + k * NU + i] = u[j][i];
             }
         }
         wave_sync();
         double st = 0, fe = 0, cs = 0, gs = 0;
+        double rsl[SPL][NS], rul[SPL][NU];
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
-            if (k > N) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) { rs[j][i] = 0; re[j][i] = 0; }
+            for (int i = 0; i < NS; ++i) rsl[j][i] = 0.0;
 #pragma unroll
-                for (int i = 0; i < NU; ++i) ru[j][i] = 0;
-#pragma unroll
-                for (int i = 0; i < NX; ++i) rix[j][i][0] = rix[j][i][1] = 0;
-#pragma unroll
-                for (int i = 0; i < NU; ++i) riu[j][i][0] = riu[j][i][1] = 0;
-                continue;
-            }
+            for (int i = 0; i < NU; ++i) rul[j][i] = 0.0;
+            if (k > N) continue;
             const double* Hk = Hs + k * hstride;
             double v[NV];
 #pragma unroll
@@ -311,7 +338,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             double gv[NV];
 #pragma unroll
             for (int i = 0; i < NV; ++i) {
-                double acc = g[j][i];
+                double acc = gterm(k, i);
 #pragma unroll
                 for (int c = 0; c < NV; ++c) acc += Hk[i * NV + c] * v[c];
                 gv[i] = acc;
@@ -319,61 +346,50 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             }
             double pn[NS];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) pn[i] = (k < N) ? W[L.xpi + (k + 1) * NS + i] : 0.0;
+            for (int i = 0; i < NS; ++i) pn[i] = (k < N) ? W[L.qt_xpi + (k + 1) * NS + i] : 0.0;
 #pragma unroll
             for (int i = 0; i < NS; ++i) {
                 double acc = gv[i];
                 if (k < N) {
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) acc += Ab[c][i] * pn[c];
+                    for (int c = 0; c < NS; ++c) acc += Abar(c, i) * pn[c];
                 }
                 if (k > 0) acc -= pi[j][i];
-                rs[j][i] = acc;
+                rsl[j][i] = acc;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 double acc = gv[NS + i];
 #pragma unroll
-                for (int c = 0; c < NS; ++c) acc += Bb[c][i] * pn[c];
-                ru[j][i] = (k < N) ? acc : 0.0;
+                for (int c = 0; c < NS; ++c) acc += Bbar(c, i) * pn[c];
+                rul[j][i] = (k < N) ? acc : 0.0;
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                const double xi = s[j][i];
-                double r0 = 0, r1 = 0;
-                if (xpres(j, i, 0)) { rs[j][i] += lx[j][i][0]; r0 = xi + tx[j][i][0] - bx[j][i][0]; cs += tx[j][i][0] * lx[j][i][0]; }
-                if (xpres(j, i, 1)) { rs[j][i] -= lx[j][i][1]; r1 = -xi + tx[j][i][1] + bx[j][i][1]; cs += tx[j][i][1] * lx[j][i][1]; }
-                rix[j][i][0] = r0; rix[j][i][1] = r1;
+                if (xpres(j, i, 0)) { rsl[j][i] += lx[j][i][0]; fe = fmax(fe, fabs(rix(j, i, 0))); cs += tx[j][i][0] * lx[j][i][0]; }
+                if (xpres(j, i, 1)) { rsl[j][i] -= lx[j][i][1]; fe = fmax(fe, fabs(rix(j, i, 1))); cs += tx[j][i][1] * lx[j][i][1]; }
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                const double ui = u[j][i];
-                double r0 = 0, r1 = 0;
-                if (upres(j, i, 0)) { ru[j][i] += lu[j][i][0]; r0 = ui + tu[j][i][0] - bu[j][i][0]; cs += tu[j][i][0] * lu[j][i][0]; }
-                if (upres(j, i, 1)) { ru[j][i] -= lu[j][i][1]; r1 = -ui + tu[j][i][1] + bu[j][i][1]; cs += tu[j][i][1] * lu[j][i][1]; }
-                riu[j][i][0] = r0; riu[j][i][1] = r1;
+                if (upres(j, i, 0)) { rul[j][i] += lu[j][i][0]; fe = fmax(fe, fabs(riu(j, i, 0))); cs += tu[j][i][0] * lu[j][i][0]; }
+                if (upres(j, i, 1)) { rul[j][i] -= lu[j][i][1]; fe = fmax(fe, fabs(riu(j, i, 1))); cs += tu[j][i][1] * lu[j][i][1]; }
             }
             if (k < N) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     double acc = cb[i] - W[L.xs + (k + 1) * NS + i];
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) acc += Ab[i][c] * s[j][c];
+                    for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) acc += Bb[i][c] * u[j][c];
-                    re[j][i] = acc;
+                    for (int c = 0; c < NU; ++c) acc += Bbar(i, c) * u[j][c];
+                    W[L.re + k * NS + i] = acc;
+                    fe = fmax(fe, fabs(acc));
                 }
-            } else {
-#pragma unroll
-                for (int i = 0; i < NS; ++i) re[j][i] = 0.0;
             }
         }
         // polytope rows: ri and F'lam partials
         double vp[NV];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) vp[i] = W[L.xs + kp * NS + i];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) vp[NS + i] = (kp < N) ? W[L.xu + kp * NU + i] : 0.0;
+        load_vp(vp, L.xs, L.xu);
         double gpp[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
@@ -381,17 +397,11 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         for (int q = 0; q < RPL; ++q) {
             const int r = lane + WAVE * q;
             if (r < mp) {
-                double acc = tp[q] - hp[q];
+                const double ri = fdot(r, vp) + tp[q] - hpi[r];
 #pragma unroll
-                for (int c = 0; c < NV; ++c) {
-                    const double f = Fs[c * mpad + r];
-                    acc += f * vp[c];
-                    gpp[c] += f * lp[q];
-                }
-                rip[q] = acc;
+                for (int c = 0; c < NV; ++c) gpp[c] += Fs[c * mpad + r] * lp[q];
+                fe = fmax(fe, fabs(ri));
                 cs += tp[q] * lp[q];
-            } else {
-                rip[q] = 0.0;
             }
         }
 #pragma unroll
@@ -399,29 +409,24 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
+            if (k > N) continue;
             if (k == kp) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) rs[j][i] += gpp[i];
+                for (int i = 0; i < NS; ++i) rsl[j][i] += gpp[i];
                 if (kp < N) {
 #pragma unroll
-                    for (int i = 0; i < NU; ++i) ru[j][i] += gpp[NS + i];
+                    for (int i = 0; i < NU; ++i) rul[j][i] += gpp[NS + i];
                 }
             }
             if (k == 0) {
 #pragma unroll
-                for (int i = 0; i < NX; ++i) rs[j][i] = 0.0;
+                for (int i = 0; i < NX; ++i) rsl[j][i] = 0.0;
             }
 #pragma unroll
-            for (int i = 0; i < NS; ++i) { st = fmax(st, fabs(rs[j][i])); fe = fmax(fe, fabs(re[j][i])); }
+            for (int i = 0; i < NS; ++i) { st = fmax(st, fabs(rsl[j][i])); W[L.rs + k * NS + i] = rsl[j][i]; }
 #pragma unroll
-            for (int i = 0; i < NU; ++i) st = fmax(st, fabs(ru[j][i]));
-#pragma unroll
-            for (int i = 0; i < NX; ++i) fe = fmax(fe, fmax(fabs(rix[j][i][0]), fabs(rix[j][i][1])));
-#pragma unroll
-            for (int i = 0; i < NU; ++i) fe = fmax(fe, fmax(fabs(riu[j][i][0]), fabs(riu[j][i][1])));
+            for (int i = 0; i < NU; ++i) { st = fmax(st, fabs(rul[j][i])); W[L.ru + k * NU + i] = rul[j][i]; }
         }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) fe = fmax(fe, fabs(rip[q]));
         stat = wmax(st);
         feas = wmax(fe);
         csum = wsum(cs);
@@ -429,21 +434,21 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     };
 
     // ======================= Riccati factorisation =========================================
-    double P0inv[NP][NP];
-    auto factor = [&]() -> bool {
-        // one reciprocal of t per row per iteration (reused by both solves and max_step)
+    // Riccati-factor lane roles:
+    //   phase A  lane (xa, ja), xa < NU, ja < NV : input row M_{u_xa, ja} = Ht + Bbar_xa' P F_ja
+    //   phase B  lane (ib, jb), ib <= jb < NS    : K columns, Phi = Abar + Bbar K, P_k(ib, jb)
+    const int xa = lane / NV, ja = lane % NV;
+    const bool alane = lane < NU * NV;
+    const int ib = lane / NS, jb = lane % NS;
+    const bool blane = lane < NS * NS && ib <= jb;
+    auto factor = [&]() __attribute__((always_inline)) -> bool {
+        // one reciprocal of t per row per iteration (reused by both solves and the steps)
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) { itx[j][i][0] = 1.0 / tx[j][i][0]; itx[j][i][1] = 1.0 / tx[j][i][1]; }
 #pragma unroll
             for (int i = 0; i < NU; ++i) { itu[j][i][0] = 1.0 / tu[j][i][0]; itu[j][i][1] = 1.0 / tu[j][i][1]; }
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) itp[q] = 1.0 / tp[q];
-        // box diagonals -> LDS
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k <= N) {
 #pragma unroll
@@ -462,12 +467,14 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 }
             }
         }
-        // polytope F'DF (upper triangle, reduced over the wave)
+        STAMP(1);
+        // polytope F'DF (upper triangle), reduced over the wave
         double fd[NV * (NV + 1) / 2];
 #pragma unroll
         for (int c = 0; c < NV * (NV + 1) / 2; ++c) fd[c] = 0.0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
+            itp[q] = 1.0 / tp[q];
             const int r = lane + WAVE * q;
             if (r < mp) {
                 const double d = lp[q] * itp[q];
@@ -497,8 +504,22 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 }
         }
         wave_sync();
+        // per-lane columns of F = [Abar Bbar] used by the two phases (constant over stages)
+        double FjA[NS], BxA[NS], AiB[NS], AjB[NS];
+#pragma unroll
+        for (int a_ = 0; a_ < NS; ++a_) {
+            FjA[a_] = alane ? (ja < NS ? Abar(a_, ja) : Bbar(a_, ja - NS)) : 0.0;
+            BxA[a_] = alane ? Bbar(a_, xa) : 0.0;
+            AiB[a_] = (lane < NS * NS) ? Abar(a_, ib) : 0.0;
+            AjB[a_] = (lane < NS * NS) ? Abar(a_, jb) : 0.0;
+        }
+        double Bl[NS][NU];
+#pragma unroll
+        for (int a_ = 0; a_ < NS; ++a_)
+#pragma unroll
+            for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
         // Htilde entry (i, j) of stage k
-        auto ht = [&](int k, int i, int j) -> double {
+        auto ht = [&](int k, int i, int j) __attribute__((always_inline)) -> double {
             double h = Hs[k * hstride + i * NV + j];
             if (i == j) {
                 if (i < NX) h += W[L.Dx + k * NX + i];
@@ -507,7 +528,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             if (k == kp) h += W[L.FD + i * NV + j];
             return h;
         };
-        // P_N
         if (lane < NS * NS) W[L.P + N * NS * NS + ib * NS + jb] = ht(N, ib, jb);
         wave_sync();
         double Pr[NS][NS];
@@ -515,9 +535,9 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         for (int i = 0; i < NS; ++i)
 #pragma unroll
             for (int c = 0; c < NS; ++c) Pr[i][c] = W[L.P + N * NS * NS + i * NS + c];
+        STAMP(2);
         bool ok = true;
         for (int k = N - 1; k >= 0; --k) {
-            // phase A: input rows of M = Ht + F' P F
             if (alane) {
                 double acc = 0.0;
 #pragma unroll
@@ -527,50 +547,32 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     for (int b = 0; b < NS; ++b) pf += Pr[a_][b] * FjA[b];
                     acc += BxA[a_] * pf;
                 }
-                W[L.M + xa * NV + ja] = ht(k, NS + xa, ja) + acc;
+                W[L.Mu + xa * NV + ja] = ht(k, NS + xa, ja) + acc;
             }
             wave_sync();
-            double Ruu[NU][NU], Ri[NU][NU];
+            double Ruu[NU][NU], Lc[NU][NU];
 #pragma unroll
             for (int x = 0; x < NU; ++x)
 #pragma unroll
-                for (int y = 0; y < NU; ++y) Ruu[x][y] = W[L.M + x * NV + NS + y];
-            if constexpr (NU == 1) {
-                ok = ok && (Ruu[0][0] > 0.0);
-                Ri[0][0] = 1.0 / Ruu[0][0];
-            } else if constexpr (NU == 2) {
-                // Cholesky-based inverse, same order as oracle/cpu_ipm.c chol_inv
-                const double l00 = sqrt(Ruu[0][0]);
-                const double l10 = Ruu[1][0] / l00;
-                const double d1 = Ruu[1][1] - l10 * l10;
-                ok = ok && (Ruu[0][0] > 0.0) && (d1 > 0.0);
-                const double l11 = sqrt(d1);
-                const double i00 = 1.0 / l00, i11 = 1.0 / l11;
-                const double i10 = -(l10 * i00) / l11;
-                Ri[0][0] = i00 * i00 + i10 * i10;
-                Ri[0][1] = i10 * i11;
-                Ri[1][0] = i11 * i10;
-                Ri[1][1] = i11 * i11;
-            }
-            // phase B: K columns ib, jb; Phi = Abar + Bbar K; Joseph-form P_k(ib, jb)
+                for (int y = 0; y < NU; ++y) Ruu[x][y] = W[L.Mu + x * NV + NS + y];
+            ok = chol_small<NU>(Ruu, Lc) && ok;
+            double Lf[NU * NU];
+#pragma unroll
+            for (int x = 0; x < NU; ++x)
+#pragma unroll
+                for (int y = 0; y < NU; ++y) Lf[x * NU + y] = Lc[x][y];
             if (blane) {
                 double Ki[NU], Kj[NU];
 #pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    double vi = 0.0, vj = 0.0;
-#pragma unroll
-                    for (int y = 0; y < NU; ++y) {
-                        vi -= Ri[x][y] * W[L.M + y * NV + ib];
-                        vj -= Ri[x][y] * W[L.M + y * NV + jb];
-                    }
-                    Ki[x] = vi; Kj[x] = vj;
-                }
+                for (int x = 0; x < NU; ++x) { Ki[x] = -W[L.Mu + x * NV + ib]; Kj[x] = -W[L.Mu + x * NV + jb]; }
+                chol_solve_small<NU>(Lf, Ki);
+                chol_solve_small<NU>(Lf, Kj);
                 double Phi_i[NS], Phi_j[NS];
 #pragma unroll
                 for (int a_ = 0; a_ < NS; ++a_) {
                     double vi = AiB[a_], vj = AjB[a_];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) { vi += Bb[a_][x] * Ki[x]; vj += Bb[a_][x] * Kj[x]; }
+                    for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vj += Bl[a_][x] * Kj[x]; }
                     Phi_i[a_] = vi; Phi_j[a_] = vj;
                 }
                 double v = ht(k, ib, jb);
@@ -594,13 +596,15 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 if (ib == 0) {
 #pragma unroll
                     for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + jb] = Kj[x];
+                    if (kPhi) {
+#pragma unroll
+                        for (int a_ = 0; a_ < NS; ++a_) W[L.Phi + k * NS * NS + a_ * NS + jb] = Phi_j[a_];
+                    }
                 }
             }
             if (lane == 0) {
 #pragma unroll
-                for (int x = 0; x < NU; ++x)
-#pragma unroll
-                    for (int y = 0; y < NU; ++y) W[L.Ri + k * NU * NU + x * NU + y] = Ri[x][y];
+                for (int x = 0; x < NU * NU; ++x) W[L.Lr + k * NU * NU + x] = Lf[x];
             }
             wave_sync();
 #pragma unroll
@@ -608,55 +612,59 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
                 for (int c = 0; c < NS; ++c) Pr[i][c] = W[L.P + k * NS * NS + i * NS + c];
         }
-        // theta block of P_0
-        double Pt[NP][NP];
+        STAMP(3);
+        // Cholesky factor of the theta block of P_0
+        double Pt[NP][NP], L0[NP][NP];
 #pragma unroll
         for (int x = 0; x < NP; ++x)
 #pragma unroll
             for (int y = 0; y < NP; ++y) Pt[x][y] = Pr[NX + x][NX + y];
-        if constexpr (NP == 1) {
-            ok = ok && (Pt[0][0] > 0.0);
-            P0inv[0][0] = 1.0 / Pt[0][0];
-        } else if constexpr (NP == 2) {
-            const double l00 = sqrt(Pt[0][0]);
-            const double l10 = Pt[1][0] / l00;
-            const double d1 = Pt[1][1] - l10 * l10;
-            ok = ok && (Pt[0][0] > 0.0) && (d1 > 0.0);
-            const double l11 = sqrt(d1);
-            const double i00 = 1.0 / l00, i11 = 1.0 / l11;
-            const double i10 = -(l10 * i00) / l11;
-            P0inv[0][0] = i00 * i00 + i10 * i10;
-            P0inv[0][1] = i10 * i11;
-            P0inv[1][0] = i11 * i10;
-            P0inv[1][1] = i11 * i11;
+        ok = chol_small<NP>(Pt, L0) && ok;
+        if (lane == 0) {
+#pragma unroll
+            for (int x = 0; x < NP; ++x)
+#pragma unroll
+                for (int y = 0; y < NP; ++y) W[L.L0 + x * NP + y] = L0[x][y];
         }
+        wave_sync();
         return ok;
     };
 
-    // ======================= Newton solve for a given rc ===================================
-    auto solve = [&]() {
-        // q = r_v + C'((lam o ri - rc)/t); stage parts -> registers, then LDS
+    // complementarity right-hand side of a row: predictor t*lam, corrector + dt_a*dlam_a - sigma*mu
+    auto rcv = [&](double t, double l, double pr, bool corr, double smu) __attribute__((always_inline)) -> double {
+        return corr ? t * l + pr - smu : t * l;
+    };
+
+    // ======================= Newton solve ==================================================
+    auto solve = [&](bool corr, double smu) __attribute__((always_inline)) {
+        // q = r_v + C'((lam o ri - rc)/t)
         double qs[SPL][NS], qu[SPL][NU];
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            const int kk = k <= N ? k : N;
 #pragma unroll
-            for (int i = 0; i < NS; ++i) qs[j][i] = rs[j][i];
+            for (int i = 0; i < NS; ++i) qs[j][i] = W[L.rs + kk * NS + i];
+#pragma unroll
+            for (int i = 0; i < NU; ++i) qu[j][i] = W[L.ru + kk * NU + i];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 double e = 0.0;
-                if (xpres(j, i, 0)) e += (lx[j][i][0] * rix[j][i][0] - rcx[j][i][0]) * itx[j][i][0];
-                if (xpres(j, i, 1)) e -= (lx[j][i][1] * rix[j][i][1] - rcx[j][i][1]) * itx[j][i][1];
+                if (xpres(j, i, 0)) e += (lx[j][i][0] * rix(j, i, 0) - rcv(tx[j][i][0], lx[j][i][0], prx[j][i][0], corr, smu)) * itx[j][i][0];
+                if (xpres(j, i, 1)) e -= (lx[j][i][1] * rix(j, i, 1) - rcv(tx[j][i][1], lx[j][i][1], prx[j][i][1], corr, smu)) * itx[j][i][1];
                 qs[j][i] += e;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                double e = ru[j][i];
-                if (upres(j, i, 0)) e += (lu[j][i][0] * riu[j][i][0] - rcu[j][i][0]) * itu[j][i][0];
-                if (upres(j, i, 1)) e -= (lu[j][i][1] * riu[j][i][1] - rcu[j][i][1]) * itu[j][i][1];
+                double e = qu[j][i];
+                if (upres(j, i, 0)) e += (lu[j][i][0] * riu(j, i, 0) - rcv(tu[j][i][0], lu[j][i][0], pru[j][i][0], corr, smu)) * itu[j][i][0];
+                if (upres(j, i, 1)) e -= (lu[j][i][1] * riu(j, i, 1) - rcv(tu[j][i][1], lu[j][i][1], pru[j][i][1], corr, smu)) * itu[j][i][1];
                 qu[j][i] = e;
             }
         }
         {
+            double vp[NV];
+            load_vp(vp, L.xs, L.xu);
             double gpp[NV];
 #pragma unroll
             for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
@@ -664,7 +672,9 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int q = 0; q < RPL; ++q) {
                 const int r = lane + WAVE * q;
                 if (r < mp) {
-                    const double e = (lp[q] * rip[q] - rcp[q]) * itp[q];
+                    const double ri = fdot(r, vp) + tp[q] - hpi[r];
+                    const double pr = corr ? W[L.prp + r] : 0.0;
+                    const double e = (lp[q] * ri - rcv(tp[q], lp[q], pr, corr, smu)) * itp[q];
 #pragma unroll
                     for (int c = 0; c < NV; ++c) gpp[c] += Fs[c * mpad + r] * e;
                 }
@@ -683,6 +693,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 }
             }
         }
+        STAMP(4);
         // pre-pass: wv_k = P_{k+1} re_k, qt_k = qs_k + K_k' qu_k ; p_N = qs_N
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -690,259 +701,291 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             if (k < N) {
                 const double* Pn = W + L.P + (k + 1) * NS * NS;
                 const double* Kk = W + L.K + k * NU * NS;
+                double rek[NS];
+#pragma unroll
+                for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     double v = 0.0;
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Pn[i * NS + c] * re[j][c];
+                    for (int c = 0; c < NS; ++c) v += Pn[i * NS + c] * rek[c];
                     W[L.wv + k * NS + i] = v;
                     double qq = qs[j][i];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) qq += Kk[x * NS + i] * qu[j][x];
-                    W[L.qt + k * NS + i] = qq;
+                    W[L.qt_xpi + k * NS + i] = qq;
                 }
 #pragma unroll
                 for (int x = 0; x < NU; ++x) W[L.qu + k * NU + x] = qu[j][x];
             } else if (k == N) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) W[L.p + N * NS + i] = qs[j][i];
+                for (int i = 0; i < NS; ++i) W[L.pv + N * NS + i] = qs[j][i];
             }
         }
         wave_sync();
-        // backward sweep (redundant in every lane)
-        double pv[NS];
+        STAMP(5);
+        // backward sweep (redundant in every lane): p_k = Phi_k' (p_{k+1} + w_k) + qt_k
+        {
+            double pv[NS];
 #pragma unroll
-        for (int i = 0; i < NS; ++i) pv[i] = W[L.p + N * NS + i];
-        for (int k = N - 1; k >= 0; --k) {
-            const double* Kk = W + L.K + k * NU * NS;
-            double y[NS], by[NU];
+            for (int i = 0; i < NS; ++i) pv[i] = W[L.pv + N * NS + i];
+            for (int k = N - 1; k >= 0; --k) {
+                double y[NS];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) y[i] = pv[i] + W[L.wv + k * NS + i];
+                for (int i = 0; i < NS; ++i) y[i] = pv[i] + W[L.wv + k * NS + i];
+                if constexpr (kPhi) {
+                    const double* Ph = W + L.Phi + k * NS * NS;
 #pragma unroll
-            for (int x = 0; x < NU; ++x) {
-                double v = 0.0;
+                    for (int i = 0; i < NS; ++i) {
+                        double v = W[L.qt_xpi + k * NS + i];
 #pragma unroll
-                for (int c = 0; c < NS; ++c) v += Bb[c][x] * y[c];
-                by[x] = v;
-            }
+                        for (int c = 0; c < NS; ++c) v += Ph[c * NS + i] * y[c];
+                        pv[i] = v;
+                    }
+                } else {
+                    const double* Kk = W + L.K + k * NU * NS;
+                    double by[NU];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                double v = W[L.qt + k * NS + i];
+                    for (int x = 0; x < NU; ++x) {
+                        double v = 0.0;
 #pragma unroll
-                for (int c = 0; c < NS; ++c) v += Ab[c][i] * y[c];
+                        for (int c = 0; c < NS; ++c) v += Bbar(c, x) * y[c];
+                        by[x] = v;
+                    }
 #pragma unroll
-                for (int x = 0; x < NU; ++x) v += Kk[x * NS + i] * by[x];
-                pv[i] = v;
-            }
-            if (lane == 0) {
+                    for (int i = 0; i < NS; ++i) {
+                        double v = W[L.qt_xpi + k * NS + i];
 #pragma unroll
-                for (int i = 0; i < NS; ++i) W[L.p + k * NS + i] = pv[i];
+                        for (int c = 0; c < NS; ++c) v += Abar(c, i) * y[c];
+#pragma unroll
+                        for (int x = 0; x < NU; ++x) v += Kk[x * NS + i] * by[x];
+                        pv[i] = v;
+                    }
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) W[L.pv + k * NS + i] = pv[i];
+                }
             }
         }
         wave_sync();
-        // post-backward: kff, f
+        STAMP(6);
+        // post-backward: kff_k = -Rhat^{-1}(qu_k + Bbar'(p_{k+1} + w_k)); f_k = Bbar kff_k + re_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
                 double y[NS], r[NU];
 #pragma unroll
-                for (int i = 0; i < NS; ++i) y[i] = W[L.p + (k + 1) * NS + i] + W[L.wv + k * NS + i];
+                for (int i = 0; i < NS; ++i) y[i] = W[L.pv + (k + 1) * NS + i] + W[L.wv + k * NS + i];
 #pragma unroll
                 for (int x = 0; x < NU; ++x) {
                     double v = qu[j][x];
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Bb[c][x] * y[c];
-                    r[x] = v;
+                    for (int c = 0; c < NS; ++c) v += Bbar(c, x) * y[c];
+                    r[x] = -v;
                 }
-                const double* Ri = W + L.Ri + k * NU * NU;
+                chol_solve_small<NU>(W + L.Lr + k * NU * NU, r);
 #pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    double v = 0.0;
-#pragma unroll
-                    for (int y2 = 0; y2 < NU; ++y2) v -= Ri[x * NU + y2] * r[y2];
-                    kff[j][x] = v;
-                }
+                for (int x = 0; x < NU; ++x) kff[j][x] = r[x];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double v = re[j][i];
+                    double v = W[L.re + k * NS + i];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) v += Bb[i][x] * kff[j][x];
+                    for (int x = 0; x < NU; ++x) v += Bbar(i, x) * kff[j][x];
                     W[L.fv + k * NS + i] = v;
                 }
             }
         }
         wave_sync();
-        // theta_0 step + forward sweep (redundant)
-        double dv0[NS];
+        STAMP(7);
+        // theta_0 step + forward sweep (redundant): ds_{k+1} = Phi_k ds_k + f_k
+        {
+            double d[NS];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dv0[i] = 0.0;
+            for (int i = 0; i < NX; ++i) d[i] = 0.0;
+            double r0[NP];
 #pragma unroll
-        for (int x = 0; x < NP; ++x) {
-            double v = 0.0;
+            for (int x = 0; x < NP; ++x) r0[x] = -W[L.pv + NX + x];
+            chol_solve_small<NP>(W + L.L0, r0);
 #pragma unroll
-            for (int y2 = 0; y2 < NP; ++y2) v -= P0inv[x][y2] * W[L.p + NX + y2];
-            dv0[NX + x] = v;
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int i = 0; i < NS; ++i) W[L.dsv + i] = dv0[i];
-        }
-        for (int k = 0; k < N; ++k) {
-            const double* Kk = W + L.K + k * NU * NS;
-            double kd[NU];
-#pragma unroll
-            for (int x = 0; x < NU; ++x) {
-                double v = 0.0;
-#pragma unroll
-                for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * dv0[c];
-                kd[x] = v;
-            }
-            double nd[NS];
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                double v = W[L.fv + k * NS + i];
-#pragma unroll
-                for (int c = 0; c < NS; ++c) v += Ab[i][c] * dv0[c];
-#pragma unroll
-                for (int x = 0; x < NU; ++x) v += Bb[i][x] * kd[x];
-                nd[i] = v;
-            }
-#pragma unroll
-            for (int i = 0; i < NS; ++i) dv0[i] = nd[i];
+            for (int x = 0; x < NP; ++x) d[NX + x] = r0[x];
             if (lane == 0) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) W[L.dsv + (k + 1) * NS + i] = nd[i];
+                for (int i = 0; i < NS; ++i) W[L.dsv + i] = d[i];
+            }
+            for (int k = 0; k < N; ++k) {
+                double nd[NS];
+                if constexpr (kPhi) {
+                    const double* Ph = W + L.Phi + k * NS * NS;
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) {
+                        double v = W[L.fv + k * NS + i];
+#pragma unroll
+                        for (int c = 0; c < NS; ++c) v += Ph[i * NS + c] * d[c];
+                        nd[i] = v;
+                    }
+                } else {
+                    const double* Kk = W + L.K + k * NU * NS;
+                    double kd[NU];
+#pragma unroll
+                    for (int x = 0; x < NU; ++x) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * d[c];
+                        kd[x] = v;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) {
+                        double v = W[L.fv + k * NS + i];
+#pragma unroll
+                        for (int c = 0; c < NS; ++c) v += Abar(i, c) * d[c];
+#pragma unroll
+                        for (int x = 0; x < NU; ++x) v += Bbar(i, x) * kd[x];
+                        nd[i] = v;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < NS; ++i) d[i] = nd[i];
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) W[L.dsv + (k + 1) * NS + i] = nd[i];
+                }
             }
         }
         wave_sync();
-        // post-forward: ds, du, dpi, box steps; publish polytope-stage step
+        STAMP(8);
+        // post-forward: du_k = K_k ds_k + kff_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
-            if (k > N) continue;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) ds[j][i] = W[L.dsv + k * NS + i];
             if (k < N) {
                 const double* Kk = W + L.K + k * NU * NS;
 #pragma unroll
                 for (int x = 0; x < NU; ++x) {
                     double v = kff[j][x];
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * ds[j][c];
-                    du[j][x] = v;
+                    for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * W[L.dsv + k * NS + c];
+                    W[L.duv + k * NU + x] = v;
                 }
-            } else {
+            } else if (k == N) {
 #pragma unroll
-                for (int x = 0; x < NU; ++x) du[j][x] = 0.0;
+                for (int x = 0; x < NU; ++x) W[L.duv + N * NU + x] = 0.0;
             }
+        }
+        wave_sync();
+    };
+
+    // ======================= row passes over the step (dt, dlam recomputed) ================
+    // mode 0: max ratio (returns max of -dt/t, -dlam/lam); mode 1: comp sum after alpha and
+    // store predictor products; mode 2: apply the step alpha to t, lam.
+    auto row_pass = [&](int mode, bool corr, double smu, double al) __attribute__((always_inline)) -> double {
+        double acc = 0.0;
 #pragma unroll
-            for (int x = 0; x < NU; ++x) W[L.duv + k * NU + x] = du[j][x];
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+            double dsk[NS], duk[NU];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) dsk[i] = W[L.dsv + k * NS + i];
+#pragma unroll
+            for (int i = 0; i < NU; ++i) duk[i] = W[L.duv + k * NU + i];
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (!xpres(j, i, h)) continue;
+                    const double rc = rcv(tx[j][i][h], lx[j][i][h], prx[j][i][h], corr, smu);
+                    const double dt = -rix(j, i, h) - (h == 0 ? dsk[i] : -dsk[i]);
+                    const double dl = (-rc - lx[j][i][h] * dt) * itx[j][i][h];
+                    if (mode == 0) {
+                        acc = fmax(acc, -dt * itx[j][i][h]);
+                        acc = fmax(acc, -dl / lx[j][i][h]);
+                    } else if (mode == 1) {
+                        acc += (tx[j][i][h] + al * dt) * (lx[j][i][h] + al * dl);
+                        prx[j][i][h] = dt * dl;
+                    } else {
+                        tx[j][i][h] += al * dt;
+                        lx[j][i][h] += al * dl;
+                    }
+                }
+#pragma unroll
+            for (int i = 0; i < NU; ++i)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (!upres(j, i, h)) continue;
+                    const double rc = rcv(tu[j][i][h], lu[j][i][h], pru[j][i][h], corr, smu);
+                    const double dt = -riu(j, i, h) - (h == 0 ? duk[i] : -duk[i]);
+                    const double dl = (-rc - lu[j][i][h] * dt) * itu[j][i][h];
+                    if (mode == 0) {
+                        acc = fmax(acc, -dt * itu[j][i][h]);
+                        acc = fmax(acc, -dl / lu[j][i][h]);
+                    } else if (mode == 1) {
+                        acc += (tu[j][i][h] + al * dt) * (lu[j][i][h] + al * dl);
+                        pru[j][i][h] = dt * dl;
+                    } else {
+                        tu[j][i][h] += al * dt;
+                        lu[j][i][h] += al * dl;
+                    }
+                }
+        }
+        double vp[NV], dvp[NV];
+        load_vp(vp, L.xs, L.xu);
+        load_vp(dvp, L.dsv, L.duv);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            if (r >= mp) continue;
+            const double ri = fdot(r, vp) + tp[q] - hpi[r];
+            const double pr = corr ? W[L.prp + r] : 0.0;
+            const double rc = rcv(tp[q], lp[q], pr, corr, smu);
+            const double dt = -ri - fdot(r, dvp);
+            const double dl = (-rc - lp[q] * dt) * itp[q];
+            if (mode == 0) {
+                acc = fmax(acc, -dt * itp[q]);
+                acc = fmax(acc, -dl / lp[q]);
+            } else if (mode == 1) {
+                acc += (tp[q] + al * dt) * (lp[q] + al * dl);
+                W[L.prp + r] = dt * dl;
+            } else {
+                tp[q] += al * dt;
+                lp[q] += al * dl;
+            }
+        }
+        if (mode == 0) return wmax(acc);
+        if (mode == 1) return wsum(acc);
+        return 0.0;
+    };
+    auto step_len = [&](bool corr, double smu) __attribute__((always_inline)) -> double {
+        const double rm = row_pass(0, corr, smu, 0.0);
+        return rm > 1.0 ? 1.0 / rm : 1.0;
+    };
+    // primal/dual stage update by alpha (dpi_k = P_k ds_k + p_k)
+    auto update_stage = [&](double al) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+            double dsk[NS];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) dsk[i] = W[L.dsv + k * NS + i];
             if (k >= 1) {
                 const double* Pk = W + L.P + k * NS * NS;
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double v = W[L.p + k * NS + i];
+                    double v = W[L.pv + k * NS + i];
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Pk[i * NS + c] * ds[j][c];
-                    dpi[j][i] = v;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < NS; ++i) dpi[j][i] = 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                const double dx = ds[j][i];
-                dtx[j][i][0] = dtx[j][i][1] = dlx[j][i][0] = dlx[j][i][1] = 0.0;
-                if (xpres(j, i, 0)) {
-                    dtx[j][i][0] = -rix[j][i][0] - dx;
-                    dlx[j][i][0] = (-rcx[j][i][0] - lx[j][i][0] * dtx[j][i][0]) * itx[j][i][0];
-                }
-                if (xpres(j, i, 1)) {
-                    dtx[j][i][1] = -rix[j][i][1] + dx;
-                    dlx[j][i][1] = (-rcx[j][i][1] - lx[j][i][1] * dtx[j][i][1]) * itx[j][i][1];
+                    for (int c = 0; c < NS; ++c) v += Pk[i * NS + c] * dsk[c];
+                    pi[j][i] += al * v;
                 }
             }
 #pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                const double dd = du[j][i];
-                dtu[j][i][0] = dtu[j][i][1] = dlu[j][i][0] = dlu[j][i][1] = 0.0;
-                if (upres(j, i, 0)) {
-                    dtu[j][i][0] = -riu[j][i][0] - dd;
-                    dlu[j][i][0] = (-rcu[j][i][0] - lu[j][i][0] * dtu[j][i][0]) * itu[j][i][0];
-                }
-                if (upres(j, i, 1)) {
-                    dtu[j][i][1] = -riu[j][i][1] + dd;
-                    dlu[j][i][1] = (-rcu[j][i][1] - lu[j][i][1] * dtu[j][i][1]) * itu[j][i][1];
-                }
+            for (int i = 0; i < NS; ++i) s[j][i] += al * dsk[i];
+            if (k < N) {
+#pragma unroll
+                for (int i = 0; i < NU; ++i) u[j][i] += al * W[L.duv + k * NU + i];
             }
         }
-        wave_sync();
-        double dvp[NV];
-#pragma unroll
-        for (int i = 0; i < NS; ++i) dvp[i] = W[L.dsv + kp * NS + i];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) dvp[NS + i] = (kp < N) ? W[L.duv + kp * NU + i] : 0.0;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const int r = lane + WAVE * q;
-            if (r < mp) {
-                double acc = 0.0;
-#pragma unroll
-                for (int c = 0; c < NV; ++c) acc += Fs[c * mpad + r] * dvp[c];
-                dtp[q] = -rip[q] - acc;
-                dlp[q] = (-rcp[q] - lp[q] * dtp[q]) * itp[q];
-            } else {
-                dtp[q] = 0.0; dlp[q] = 0.0;
-            }
-        }
-    };
-
-    // alpha = min(1, 1 / max(-dt/t, -dlam/lam)) (same form as oracle/cpu_ipm.c max_step)
-    auto max_step = [&]() -> double {
-        double rm = 0.0;
-#define BQP_RATIO(dv, iv) { const double qq = -(dv) * (iv); rm = fmax(rm, qq); }
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (xpres(j, i, h)) { BQP_RATIO(dtx[j][i][h], itx[j][i][h]); BQP_RATIO(dlx[j][i][h], 1.0 / lx[j][i][h]); }
-#pragma unroll
-            for (int i = 0; i < NU; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (upres(j, i, h)) { BQP_RATIO(dtu[j][i][h], itu[j][i][h]); BQP_RATIO(dlu[j][i][h], 1.0 / lu[j][i][h]); }
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if (lane + WAVE * q < mp) { BQP_RATIO(dtp[q], itp[q]); BQP_RATIO(dlp[q], 1.0 / lp[q]); }
-#undef BQP_RATIO
-        rm = wmax(rm);
-        return rm > 1.0 ? 1.0 / rm : 1.0;
-    };
-
-    auto comp_after = [&](double al) -> double {
-        double c = 0.0;
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (xpres(j, i, h)) c += (tx[j][i][h] + al * dtx[j][i][h]) * (lx[j][i][h] + al * dlx[j][i][h]);
-#pragma unroll
-            for (int i = 0; i < NU; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (upres(j, i, h)) c += (tu[j][i][h] + al * dtu[j][i][h]) * (lu[j][i][h] + al * dlu[j][i][h]);
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if (lane + WAVE * q < mp) c += (tp[q] + al * dtp[q]) * (lp[q] + al * dlp[q]);
-        return wsum(c);
     };
 
     // ======================= initial point ==================================================
@@ -951,42 +994,40 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
         for (int i = 0; i < NX; ++i)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) { tx[j][i][h] = 1.0; lx[j][i][h] = 1.0; rcx[j][i][h] = 1.0; }
+            for (int h = 0; h < 2; ++h) { tx[j][i][h] = 1.0; lx[j][i][h] = 1.0; prx[j][i][h] = 0.0; }
 #pragma unroll
         for (int i = 0; i < NU; ++i)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) { tu[j][i][h] = 1.0; lu[j][i][h] = 1.0; rcu[j][i][h] = 1.0; }
+            for (int h = 0; h < 2; ++h) { tu[j][i][h] = 1.0; lu[j][i][h] = 1.0; pru[j][i][h] = 0.0; }
     }
 #pragma unroll
-    for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; rcp[q] = 1.0; }
+    for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; }
     double stat = 0, feas = 0, csum = 0, gscale = 0;
     residuals(stat, feas, csum, gscale);
     int flag = 0;
-    bool ok = factor();
-    if (!ok) flag = -8;
-    solve();
+    if (!factor()) flag = -8;
+    solve(false, 0.0);
     {
+        // tt = t + dt (t = 1) at the unit-scaled least-squares point; lam~ = -tt; shift
         double tmin = INFINITY, tmax = -INFINITY;
+        row_pass(2, false, 0.0, 1.0);      // t <- 1 + dt (lam is reset below)
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-            for (int i = 0; i < NS; ++i) { s[j][i] += ds[j][i]; pi[j][i] += dpi[j][i]; }
-#pragma unroll
-            for (int i = 0; i < NU; ++i) u[j][i] += du[j][i];
 #pragma unroll
             for (int i = 0; i < NX; ++i)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    if (xpres(j, i, h)) { const double t = 1.0 + dtx[j][i][h]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+                    if (xpres(j, i, h)) { tmin = fmin(tmin, tx[j][i][h]); tmax = fmax(tmax, tx[j][i][h]); }
 #pragma unroll
             for (int i = 0; i < NU; ++i)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
-                    if (upres(j, i, h)) { const double t = 1.0 + dtu[j][i][h]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+                    if (upres(j, i, h)) { tmin = fmin(tmin, tu[j][i][h]); tmax = fmax(tmax, tu[j][i][h]); }
         }
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
-            if (lane + WAVE * q < mp) { const double t = 1.0 + dtp[q]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+            if (prow(q)) { tmin = fmin(tmin, tp[q]); tmax = fmax(tmax, tp[q]); }
+        update_stage(1.0);
         tmin = wmin(tmin);
         tmax = wmax(tmax);
         const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
@@ -997,7 +1038,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int i = 0; i < NX; ++i)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const double t = 1.0 + dtx[j][i][h];
+                    const double t = tx[j][i][h];
                     const bool pr = xpres(j, i, h);
                     tx[j][i][h] = pr ? t + shp : 1.0;
                     lx[j][i][h] = pr ? -t + shd : 0.0;
@@ -1006,7 +1047,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int i = 0; i < NU; ++i)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const double t = 1.0 + dtu[j][i][h];
+                    const double t = tu[j][i][h];
                     const bool pr = upres(j, i, h);
                     tu[j][i][h] = pr ? t + shp : 1.0;
                     lu[j][i][h] = pr ? -t + shd : 0.0;
@@ -1014,8 +1055,8 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         }
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            const double t = 1.0 + dtp[q];
-            const bool pr = lane + WAVE * q < mp;
+            const double t = tp[q];
+            const bool pr = prow(q);
             tp[q] = pr ? t + shp : 1.0;
             lp[q] = pr ? -t + shd : 0.0;
         }
@@ -1023,74 +1064,39 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 
     // ======================= main loop ======================================================
     int it = 0;
-    double mu = 0.0;
+    double mu = 0.0, mu_min = INFINITY;
     const int max_iter = a.max_iter;
     if (flag == 0) {
         for (it = 0; it <= max_iter; ++it) {
+            STAMP(14);
             residuals(stat, feas, csum, gscale);
+            STAMP(0);
             mu = csum * minv;
             if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
                 mu <= a.tol_comp) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
+            if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) { flag = -2; break; }
+            mu_min = fmin(mu_min, mu);
             if (it == max_iter) break;
             if (!factor()) { flag = -8; break; }
-            // predictor
-#pragma unroll
-            for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) rcx[j][i][h] = tx[j][i][h] * lx[j][i][h];
-#pragma unroll
-                for (int i = 0; i < NU; ++i)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) rcu[j][i][h] = tu[j][i][h] * lu[j][i][h];
-            }
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) rcp[q] = tp[q] * lp[q];
-            solve();
-            double al = max_step();
-            const double mua = comp_after(al) * minv;
+            solve(false, 0.0);                                  // predictor
+            STAMP(9);
+            const double al_aff = step_len(false, 0.0);
+            STAMP(10);
+            const double mua = row_pass(1, false, 0.0, al_aff) * minv;
+            STAMP(11);
             double sg = mua / mu;
             sg = sg * sg * sg;
             const double smu = sg * mu;
-            // corrector rhs
-#pragma unroll
-            for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) rcx[j][i][h] = tx[j][i][h] * lx[j][i][h] + dtx[j][i][h] * dlx[j][i][h] - smu;
-#pragma unroll
-                for (int i = 0; i < NU; ++i)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) rcu[j][i][h] = tu[j][i][h] * lu[j][i][h] + dtu[j][i][h] * dlu[j][i][h] - smu;
-            }
-#pragma unroll
-            for (int q = 0; q < RPL; ++q) rcp[q] = tp[q] * lp[q] + dtp[q] * dlp[q] - smu;
-            solve();
-            al = max_step() * a.tau;
+            solve(true, smu);                                   // corrector
+            STAMP(9);
+            double al = step_len(true, smu) * a.tau;
+            STAMP(10);
             if (al > 1.0) al = 1.0;
-#pragma unroll
-            for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-                for (int i = 0; i < NS; ++i) { s[j][i] += al * ds[j][i]; pi[j][i] += al * dpi[j][i]; }
-#pragma unroll
-                for (int i = 0; i < NU; ++i) u[j][i] += al * du[j][i];
-#pragma unroll
-                for (int i = 0; i < NX; ++i)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        if (xpres(j, i, h)) { tx[j][i][h] += al * dtx[j][i][h]; lx[j][i][h] += al * dlx[j][i][h]; }
-#pragma unroll
-                for (int i = 0; i < NU; ++i)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        if (upres(j, i, h)) { tu[j][i][h] += al * dtu[j][i][h]; lu[j][i][h] += al * dlu[j][i][h]; }
-            }
-#pragma unroll
-            for (int q = 0; q < RPL; ++q)
-                if (lane + WAVE * q < mp) { tp[q] += al * dtp[q]; lp[q] += al * dlp[q]; }
+            row_pass(2, true, smu, al);
+            STAMP(12);
+            update_stage(al);
+            STAMP(13);
         }
     }
 
@@ -1112,7 +1118,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int i = 0; i < NP; ++i) a.theta[(int64_t)inst * NP + i] = s[j][NX + i];
         }
-        // objective 0.5 v'Hv + g'v of this stage
         const double* Hk = Hs + k * hstride;
         double v[NV];
 #pragma unroll
@@ -1124,7 +1129,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             double hv = 0.0;
 #pragma unroll
             for (int c = 0; c < NV; ++c) hv += Hk[i * NV + c] * v[c];
-            fv += v[i] * (0.5 * hv + g[j][i]);
+            fv += v[i] * (0.5 * hv + gterm(k, i));
         }
         if (a.pi_out && k >= 1) {
             double* po = a.pi_out + ((int64_t)inst * N + (k - 1)) * NX;
@@ -1156,6 +1161,12 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         }
     }
     fv = wsum(fv);
+#ifdef BQP_STAMPS
+    if (lane == 0 && a.stamps) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a.stamps[(int64_t)inst * 16 + i] = (double)st_acc[i];
+    }
+#endif
     if (lane == 0) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
@@ -1169,9 +1180,8 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 // ------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------------
-int ocp_wave_lds_doubles(int N, int nx, int nu, int np) {
-    const int ns = nx + np, nv = ns + nu;
-    return WaveLds::make(N, nx, nu, ns, nv).total;
+int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad) {
+    return WaveLds::make(N, nx, nu, np, mpad, N + 1 <= 64).total;
 }
 
 template <int NX, int NU, int NP, int SPL, int RPL>
@@ -1219,7 +1229,8 @@ hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_
     const int spl = (a.N + 1 <= 64) ? 1 : 2;
     const int rpl = ocp_rpl_for(a.mp);
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
-    const size_t lds = sizeof(double) * ((size_t)a.shared_doubles + (size_t)a.wpb * ocp_wave_lds_doubles(a.N, nx, nu, np));
+    const size_t lds = sizeof(double) * ((size_t)a.shared_doubles +
+                                         (size_t)a.wpb * ocp_wave_lds_doubles(a.N, nx, nu, np, a.mpad));
     if (nx == 4 && nu == 1 && np == 1) return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);
     if (nx == 2 && nu == 2 && np == 2) return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st);
     return hipErrorInvalidValue;

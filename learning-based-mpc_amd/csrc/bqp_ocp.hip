@@ -73,6 +73,22 @@ __device__ __forceinline__ double wmax(double v) {
     return lane63(v);
 }
 __device__ __forceinline__ double wmin(double v) { return -wmax(-v); }
+// value of lane `src` broadcast to the wave (scalar register pair): the sequential Riccati
+// sweeps pass their NS-vector from stage to stage this way instead of through LDS
+__device__ __forceinline__ double rl(double v, int src) {
+    const int2 x = __builtin_bit_cast(int2, v);
+    int2 r;
+    r.x = __builtin_amdgcn_readlane(x.x, src);
+    r.y = __builtin_amdgcn_readlane(x.y, src);
+    return __builtin_bit_cast(double, r);
+}
+template <int N>
+__device__ __forceinline__ double sel(const double (&row)[N], int idx) {
+    double r = row[0];
+#pragma unroll
+    for (int c = 1; c < N; ++c) r = (idx == c) ? row[c] : r;
+    return r;
+}
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
 template <int N>
@@ -528,69 +544,99 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             if (k == kp) h += W[L.FD + i * NV + j];
             return h;
         };
-        if (lane < NS * NS) W[L.P + N * NS * NS + ib * NS + jb] = ht(N, ib, jb);
-        wave_sync();
-        double Pr[NS][NS];
+        // stage-k entries each lane needs (prefetched one stage ahead of the recursion)
+        struct StageH { double hA, hij, huj[NU], hiu[NU], huu[NU][NU]; };
+        auto load_h = [&](int k, StageH& sh) __attribute__((always_inline)) {
+            const int xa_ = alane ? xa : 0, ja_ = alane ? ja : 0;
+            const int ib_ = (lane < NS * NS) ? ib : 0, jb_ = (lane < NS * NS) ? jb : 0;
+            sh.hA = ht(k, NS + xa_, ja_);
+            sh.hij = ht(k, ib_, jb_);
 #pragma unroll
-        for (int i = 0; i < NS; ++i)
+            for (int x = 0; x < NU; ++x) {
+                sh.huj[x] = ht(k, NS + x, jb_);
+                sh.hiu[x] = ht(k, ib_, NS + x);
 #pragma unroll
-            for (int c = 0; c < NS; ++c) Pr[i][c] = W[L.P + N * NS * NS + i * NS + c];
+                for (int y = 0; y < NU; ++y) sh.huu[x][y] = ht(k, NS + x, NS + y);
+            }
+        };
+        // P_N (uniform copy in every lane, stored for the solves)
+        double Pu[NS][NS];
+        {
+            const int ib_ = (lane < NS * NS) ? ib : 0, jb_ = (lane < NS * NS) ? jb : 0;
+            const double v = ht(N, ib_, jb_);
+            if (lane < NS * NS) W[L.P + N * NS * NS + ib * NS + jb] = v;
+#pragma unroll
+            for (int i = 0; i < NS; ++i)
+#pragma unroll
+                for (int c = 0; c < NS; ++c) Pu[i][c] = rl(v, i * NS + c);
+        }
         STAMP(2);
         bool ok = true;
+        StageH cur, nxt;
+        load_h(N - 1, cur);
         for (int k = N - 1; k >= 0; --k) {
-            if (alane) {
+            if (k > 0) load_h(k - 1, nxt);
+            // phase A: input rows M_u = Ht_u + Bbar' P F  (lane (xa, ja))
+            double mA;
+            {
                 double acc = 0.0;
 #pragma unroll
                 for (int a_ = 0; a_ < NS; ++a_) {
                     double pf = 0.0;
 #pragma unroll
-                    for (int b = 0; b < NS; ++b) pf += Pr[a_][b] * FjA[b];
+                    for (int b = 0; b < NS; ++b) pf += Pu[a_][b] * FjA[b];
                     acc += BxA[a_] * pf;
                 }
-                W[L.Mu + xa * NV + ja] = ht(k, NS + xa, ja) + acc;
+                mA = cur.hA + acc;
             }
-            wave_sync();
+            double Mu[NU][NV];
+#pragma unroll
+            for (int x = 0; x < NU; ++x)
+#pragma unroll
+                for (int c = 0; c < NV; ++c) Mu[x][c] = rl(mA, x * NV + c);
             double Ruu[NU][NU], Lc[NU][NU];
 #pragma unroll
             for (int x = 0; x < NU; ++x)
 #pragma unroll
-                for (int y = 0; y < NU; ++y) Ruu[x][y] = W[L.Mu + x * NV + NS + y];
+                for (int y = 0; y < NU; ++y) Ruu[x][y] = Mu[x][NS + y];
             ok = chol_small<NU>(Ruu, Lc) && ok;
             double Lf[NU * NU];
 #pragma unroll
             for (int x = 0; x < NU; ++x)
 #pragma unroll
                 for (int y = 0; y < NU; ++y) Lf[x * NU + y] = Lc[x][y];
+            // phase B: K columns ib, jb; Phi = Abar + Bbar K; Joseph-form P_k(ib, jb)
+            double Ki[NU], Kj[NU];
+#pragma unroll
+            for (int x = 0; x < NU; ++x) { Ki[x] = -sel<NV>(Mu[x], ib); Kj[x] = -sel<NV>(Mu[x], jb); }
+            chol_solve_small<NU>(Lf, Ki);
+            chol_solve_small<NU>(Lf, Kj);
+            double Phi_i[NS], Phi_j[NS];
+#pragma unroll
+            for (int a_ = 0; a_ < NS; ++a_) {
+                double vi = AiB[a_], vj = AjB[a_];
+#pragma unroll
+                for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vj += Bl[a_][x] * Kj[x]; }
+                Phi_i[a_] = vi; Phi_j[a_] = vj;
+            }
+            double v = cur.hij;
+#pragma unroll
+            for (int x = 0; x < NU; ++x) {
+                v += Ki[x] * cur.huj[x] + cur.hiu[x] * Kj[x];
+#pragma unroll
+                for (int y = 0; y < NU; ++y) v += Ki[x] * cur.huu[x][y] * Kj[y];
+            }
+            double acc = 0.0;
+#pragma unroll
+            for (int a_ = 0; a_ < NS; ++a_) {
+                double pf = 0.0;
+#pragma unroll
+                for (int b = 0; b < NS; ++b) pf += Pu[a_][b] * Phi_j[b];
+                acc += Phi_i[a_] * pf;
+            }
+            v += acc;
+            // tables for the solves (stores only; nothing below waits on them)
             if (blane) {
-                double Ki[NU], Kj[NU];
-#pragma unroll
-                for (int x = 0; x < NU; ++x) { Ki[x] = -W[L.Mu + x * NV + ib]; Kj[x] = -W[L.Mu + x * NV + jb]; }
-                chol_solve_small<NU>(Lf, Ki);
-                chol_solve_small<NU>(Lf, Kj);
-                double Phi_i[NS], Phi_j[NS];
-#pragma unroll
-                for (int a_ = 0; a_ < NS; ++a_) {
-                    double vi = AiB[a_], vj = AjB[a_];
-#pragma unroll
-                    for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vj += Bl[a_][x] * Kj[x]; }
-                    Phi_i[a_] = vi; Phi_j[a_] = vj;
-                }
-                double v = ht(k, ib, jb);
-#pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    v += Ki[x] * ht(k, NS + x, jb) + ht(k, ib, NS + x) * Kj[x];
-#pragma unroll
-                    for (int y = 0; y < NU; ++y) v += Ki[x] * ht(k, NS + x, NS + y) * Kj[y];
-                }
-                double acc = 0.0;
-#pragma unroll
-                for (int a_ = 0; a_ < NS; ++a_) {
-                    double pf = 0.0;
-#pragma unroll
-                    for (int b = 0; b < NS; ++b) pf += Pr[a_][b] * Phi_j[b];
-                    acc += Phi_i[a_] * pf;
-                }
-                v += acc;
                 W[L.P + k * NS * NS + ib * NS + jb] = v;
                 W[L.P + k * NS * NS + jb * NS + ib] = v;
                 if (ib == 0) {
@@ -606,12 +652,22 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
                 for (int x = 0; x < NU * NU; ++x) W[L.Lr + k * NU * NU + x] = Lf[x];
             }
-            wave_sync();
+            // P_k to every lane (upper-triangle lanes hold the values)
 #pragma unroll
             for (int i = 0; i < NS; ++i)
 #pragma unroll
-                for (int c = 0; c < NS; ++c) Pr[i][c] = W[L.P + k * NS * NS + i * NS + c];
+                for (int c = i; c < NS; ++c) {
+                    const double pv_ = rl(v, i * NS + c);
+                    Pu[i][c] = pv_;
+                    Pu[c][i] = pv_;
+                }
+            cur = nxt;
         }
+        double Pr[NS][NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i)
+#pragma unroll
+            for (int c = 0; c < NS; ++c) Pr[i][c] = Pu[i][c];
         STAMP(3);
         // Cholesky factor of the theta block of P_0
         double Pt[NP][NP], L0[NP][NP];
@@ -637,6 +693,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 
     // ======================= Newton solve ==================================================
     auto solve = [&](bool corr, double smu) __attribute__((always_inline)) {
+        STAMP(15);
         // q = r_v + C'((lam o ri - rc)/t)
         double qs[SPL][NS], qu[SPL][NU];
 #pragma unroll
@@ -694,14 +751,16 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             }
         }
         STAMP(4);
-        // pre-pass: wv_k = P_{k+1} re_k, qt_k = qs_k + K_k' qu_k ; p_N = qs_N
+        // pre-pass: wv_k = P_{k+1} re_k, qt_k = qs_k + K_k' qu_k, qh_k = qt_k + Phi_k' wv_k ;
+        // p_N = qs_N.  qh carries everything of the backward recursion that does not depend on
+        // p_{k+1}, so the sequential sweep is one NS x NS mat-vec per stage.
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
                 const double* Pn = W + L.P + (k + 1) * NS * NS;
                 const double* Kk = W + L.K + k * NU * NS;
-                double rek[NS];
+                double rek[NS], wk[NS], qtk[NS];
 #pragma unroll
                 for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
 #pragma unroll
@@ -709,11 +768,40 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     double v = 0.0;
 #pragma unroll
                     for (int c = 0; c < NS; ++c) v += Pn[i * NS + c] * rek[c];
+                    wk[i] = v;
                     W[L.wv + k * NS + i] = v;
                     double qq = qs[j][i];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) qq += Kk[x * NS + i] * qu[j][x];
-                    W[L.qt_xpi + k * NS + i] = qq;
+                    qtk[i] = qq;
+                }
+                if constexpr (kPhi) {
+                    const double* Ph = W + L.Phi + k * NS * NS;
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) {
+                        double v = qtk[i];
+#pragma unroll
+                        for (int c = 0; c < NS; ++c) v += Ph[c * NS + i] * wk[c];
+                        W[L.qt_xpi + k * NS + i] = v;
+                    }
+                } else {
+                    double bw[NU];
+#pragma unroll
+                    for (int x = 0; x < NU; ++x) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int c = 0; c < NS; ++c) v += Bbar(c, x) * wk[c];
+                        bw[x] = v;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) {
+                        double v = qtk[i];
+#pragma unroll
+                        for (int c = 0; c < NS; ++c) v += Abar(c, i) * wk[c];
+#pragma unroll
+                        for (int x = 0; x < NU; ++x) v += Kk[x * NS + i] * bw[x];
+                        W[L.qt_xpi + k * NS + i] = v;
+                    }
                 }
 #pragma unroll
                 for (int x = 0; x < NU; ++x) W[L.qu + k * NU + x] = qu[j][x];
@@ -724,48 +812,41 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         }
         wave_sync();
         STAMP(5);
-        // backward sweep (redundant in every lane): p_k = Phi_k' (p_{k+1} + w_k) + qt_k
+        // backward sweep: lane i < NS computes entry i of p_k = Phi_k' p_{k+1} + qh_k; the new
+        // vector is broadcast with readlane (scalar registers), stage data prefetched a stage ahead
         {
-            double pv[NS];
+            const int li = lane < NS ? lane : NS - 1;
+            double p[NS];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) pv[i] = W[L.pv + N * NS + i];
-            for (int k = N - 1; k >= 0; --k) {
-                double y[NS];
-#pragma unroll
-                for (int i = 0; i < NS; ++i) y[i] = pv[i] + W[L.wv + k * NS + i];
+            for (int i = 0; i < NS; ++i) p[i] = W[L.pv + N * NS + i];
+            double cc[NS], cq, nc[NS], nq;
+            auto load_b = [&](int k, double (&col)[NS], double& q) __attribute__((always_inline)) {
+                q = W[L.qt_xpi + k * NS + li];
                 if constexpr (kPhi) {
-                    const double* Ph = W + L.Phi + k * NS * NS;
 #pragma unroll
-                    for (int i = 0; i < NS; ++i) {
-                        double v = W[L.qt_xpi + k * NS + i];
-#pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Ph[c * NS + i] * y[c];
-                        pv[i] = v;
-                    }
+                    for (int c = 0; c < NS; ++c) col[c] = W[L.Phi + k * NS * NS + c * NS + li];
                 } else {
-                    const double* Kk = W + L.K + k * NU * NS;
-                    double by[NU];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) {
-                        double v = 0.0;
+                    for (int c = 0; c < NS; ++c) {
+                        double v = Abar(c, li);
 #pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Bbar(c, x) * y[c];
-                        by[x] = v;
-                    }
-#pragma unroll
-                    for (int i = 0; i < NS; ++i) {
-                        double v = W[L.qt_xpi + k * NS + i];
-#pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Abar(c, i) * y[c];
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) v += Kk[x * NS + i] * by[x];
-                        pv[i] = v;
+                        for (int x = 0; x < NU; ++x) v += Bbar(c, x) * W[L.K + k * NU * NS + x * NS + li];
+                        col[c] = v;
                     }
                 }
-                if (lane == 0) {
+            };
+            load_b(N - 1, cc, cq);
+            for (int k = N - 1; k >= 0; --k) {
+                if (k > 0) load_b(k - 1, nc, nq);
+                double acc = cq;
 #pragma unroll
-                    for (int i = 0; i < NS; ++i) W[L.pv + k * NS + i] = pv[i];
-                }
+                for (int c = 0; c < NS; ++c) acc += cc[c] * p[c];
+                if (lane < NS) W[L.pv + k * NS + lane] = acc;
+#pragma unroll
+                for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
+#pragma unroll
+                for (int c = 0; c < NS; ++c) cc[c] = nc[c];
+                cq = nq;
             }
         }
         wave_sync();
@@ -799,7 +880,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         }
         wave_sync();
         STAMP(7);
-        // theta_0 step + forward sweep (redundant): ds_{k+1} = Phi_k ds_k + f_k
+        // theta_0 step + forward sweep: lane i < NS computes entry i of ds_{k+1} = Phi_k ds_k + f_k
         {
             double d[NS];
 #pragma unroll
@@ -814,43 +895,35 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) W[L.dsv + i] = d[i];
             }
-            for (int k = 0; k < N; ++k) {
-                double nd[NS];
+            const int li = lane < NS ? lane : NS - 1;
+            double cr[NS], cf, nr[NS], nf;
+            auto load_f = [&](int k, double (&row)[NS], double& f) __attribute__((always_inline)) {
+                f = W[L.fv + k * NS + li];
                 if constexpr (kPhi) {
-                    const double* Ph = W + L.Phi + k * NS * NS;
 #pragma unroll
-                    for (int i = 0; i < NS; ++i) {
-                        double v = W[L.fv + k * NS + i];
-#pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Ph[i * NS + c] * d[c];
-                        nd[i] = v;
-                    }
+                    for (int c = 0; c < NS; ++c) row[c] = W[L.Phi + k * NS * NS + li * NS + c];
                 } else {
-                    const double* Kk = W + L.K + k * NU * NS;
-                    double kd[NU];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) {
-                        double v = 0.0;
+                    for (int c = 0; c < NS; ++c) {
+                        double v = Abar(li, c);
 #pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * d[c];
-                        kd[x] = v;
-                    }
-#pragma unroll
-                    for (int i = 0; i < NS; ++i) {
-                        double v = W[L.fv + k * NS + i];
-#pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Abar(i, c) * d[c];
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) v += Bbar(i, x) * kd[x];
-                        nd[i] = v;
+                        for (int x = 0; x < NU; ++x) v += Bbar(li, x) * W[L.K + k * NU * NS + x * NS + c];
+                        row[c] = v;
                     }
                 }
+            };
+            load_f(0, cr, cf);
+            for (int k = 0; k < N; ++k) {
+                if (k + 1 < N) load_f(k + 1, nr, nf);
+                double acc = cf;
 #pragma unroll
-                for (int i = 0; i < NS; ++i) d[i] = nd[i];
-                if (lane == 0) {
+                for (int c = 0; c < NS; ++c) acc += cr[c] * d[c];
+                if (lane < NS) W[L.dsv + (k + 1) * NS + lane] = acc;
 #pragma unroll
-                    for (int i = 0; i < NS; ++i) W[L.dsv + (k + 1) * NS + i] = nd[i];
-                }
+                for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
+#pragma unroll
+                for (int c = 0; c < NS; ++c) cr[c] = nr[c];
+                cf = nf;
             }
         }
         wave_sync();

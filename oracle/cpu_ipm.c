@@ -39,7 +39,7 @@ typedef struct {
     /* work */
     double *rs, *ru, *re, *rix, *riu, *rip;
     double *ds, *du, *dpi, *dtx, *dlx, *dtu, *dlu, *dtp, *dlp;
-    double *Ptab, *Ktab, *Rinv, *Phit, *p, *qs, *qu, *wv, *qt, *kff, *f;
+    double *Ptab, *Ktab, *Rinv, *Phit, *p, *qs, *qu, *wv, *qt, *qh, *kff, *f;
     double *Dx, *Du, *FD;
     double *itx, *ilx, *itu, *ilu, *itp, *ilp;   /* 1/t, 1/lam (once per iteration) */
     double P0inv[MAXNS * MAXNS];
@@ -366,15 +366,22 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             W->qt[k * ns + i] = q;
         }
     }
-    /* backward sweep: p_k = Phi_k' (p_{k+1} + w_k) + qt_k   (= Abar'y + K'(Bbar'y) + qt) */
-    for (int i = 0; i < ns; ++i) W->p[N * ns + i] = W->qs[N * ns + i];
-    for (int k = N - 1; k >= 0; --k) {
-        double y[MAXNS];
+    /* qh_k = qt_k + Phi_k' w_k (parallel over k), then the backward sweep
+     * p_k = Phi_k' p_{k+1} + qh_k   (= Phi_k'(p_{k+1} + w_k) + qt_k) */
+    for (int k = 0; k < N; ++k) {
         const double* Phk = W->Phit + (size_t)k * ns * ns;
-        for (int i = 0; i < ns; ++i) y[i] = W->p[(k + 1) * ns + i] + W->wv[k * ns + i];
         for (int i = 0; i < ns; ++i) {
             double v = W->qt[k * ns + i];
-            for (int j = 0; j < ns; ++j) v += Phk[j * ns + i] * y[j];
+            for (int j = 0; j < ns; ++j) v += Phk[j * ns + i] * W->wv[k * ns + j];
+            W->qh[k * ns + i] = v;
+        }
+    }
+    for (int i = 0; i < ns; ++i) W->p[N * ns + i] = W->qs[N * ns + i];
+    for (int k = N - 1; k >= 0; --k) {
+        const double* Phk = W->Phit + (size_t)k * ns * ns;
+        for (int i = 0; i < ns; ++i) {
+            double v = W->qh[k * ns + i];
+            for (int j = 0; j < ns; ++j) v += Phk[j * ns + i] * W->p[(k + 1) * ns + j];
             W->p[k * ns + i] = v;
         }
     }
@@ -686,7 +693,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.Phit = alloc0((size_t)N * ns * ns);
         W.Rinv = alloc0((size_t)N * nu * nu); W.p = alloc0((N + 1) * ns);
         W.qs = alloc0((N + 1) * ns); W.qu = alloc0(N * nu); W.wv = alloc0(N * ns);
-        W.qt = alloc0(N * ns); W.kff = alloc0(N * nu); W.f = alloc0(N * ns);
+        W.qt = alloc0(N * ns); W.qh = alloc0(N * ns); W.kff = alloc0(N * nu); W.f = alloc0(N * ns);
         W.Dx = alloc0((N + 1) * nx); W.Du = alloc0(N * nu); W.FD = alloc0(nv * nv);
         W.itx = alloc0((N + 1) * nx * 2); W.ilx = alloc0((N + 1) * nx * 2);
         W.itu = alloc0(N * nu * 2); W.ilu = alloc0(N * nu * 2); W.itp = alloc0(mp); W.ilp = alloc0(mp);
@@ -758,7 +765,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.lp); free(W.rs); free(W.ru); free(W.re); free(W.rix); free(W.riu); free(W.rip);
         free(W.ds); free(W.du); free(W.dpi); free(W.dtx); free(W.dlx); free(W.dtu); free(W.dlu);
         free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Phit); free(W.Ktab); free(W.Rinv); free(W.p);
-        free(W.qs); free(W.qu); free(W.wv); free(W.qt); free(W.kff); free(W.f); free(W.Dx);
+        free(W.qs); free(W.qu); free(W.wv); free(W.qt); free(W.qh); free(W.kff); free(W.f); free(W.Dx);
         free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
         free(W.ilp);
     }

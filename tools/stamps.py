@@ -26,7 +26,7 @@ st = np.zeros((B, 16))
 _lib.check(lib.bqp_debug_stamps(h.value, 20, 6, 616, _lib.ptr(st)), 'stamps')
 names = ['residuals', 'factor:recip+Dx', 'factor:F\'DF', 'factor:riccati', 'solve:q+F\'e',
          'solve:prepass', 'solve:backward', 'solve:post-bwd', 'solve:forward', 'solve:post-fwd',
-         'step_len', 'comp_after', 'row update', 'stage update', '', 'loop top']
+         'step_len', 'comp_after', 'row update', 'stage update', 'loop top', 'factor tail']
 tot = st.sum(axis=1).mean()
 print('batch %d kernel %.3f ms, mean iterations %.2f, cycles/instance (stamped) %.0f' % (B, ms, r.iterations.mean(), tot))
 for i, n in enumerate(names):

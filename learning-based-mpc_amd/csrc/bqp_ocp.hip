@@ -108,7 +108,8 @@ __device__ __forceinline__ bool chol_small(const double (&M)[N][N], double (&L)[
     }
     return ok;
 }
-// b <- (L L')^{-1} b   (substitution, same order as oracle/cpu_ipm.c chol_solve); L row-major
+// b <- M^{-1} b with M = L L' (substitution, same order as oracle/cpu_ipm.c spd_solve); L row-major.
+// For n = 1 the factor slot holds 1/M instead (one reciprocal, no square root).
 template <int N>
 __device__ __forceinline__ void chol_solve_small(const double* L, double (&b)[N]) {
     if constexpr (N == 2) {
@@ -117,19 +118,27 @@ __device__ __forceinline__ void chol_solve_small(const double* L, double (&b)[N]
         b[1] = b[1] / L[3];
         b[0] = (b[0] - L[2] * b[1]) / L[0];
     } else {
-        b[0] = b[0] / L[0];
-        b[0] = b[0] / L[0];
+        b[0] = b[0] * L[0];     // n = 1: L holds the reciprocal of the 1x1 matrix
     }
+}
+
+// Packed upper-triangular storage of the symmetric NS x NS Riccati matrices P_k: entry (i, j),
+// i <= j, at pk_idx(i, j); each stage slot is padded to an even number of doubles so that a
+// slot starts 16-byte aligned and is read back with ds_read_b128.
+__host__ __device__ constexpr int pk_len(int NS) { return NS * (NS + 1) / 2; }
+__host__ __device__ constexpr int pk_stride(int NS) { return (pk_len(NS) + 1) & ~1; }
+__host__ __device__ constexpr int pk_idx(int NS, int i, int j) {
+    return i <= j ? i * NS - i * (i - 1) / 2 + (j - i) : j * NS - j * (j - 1) / 2 + (i - j);
 }
 
 // Per-wave LDS layout (in doubles), all sized from N at run time.
 struct WaveLds {
-    int P, Phi, K, Lr, xs, xu, qt_xpi, rs, ru, re, pv, wv, qu, fv, dsv, duv, Dx, Du, FD, Mu, AB, L0, prp, misc, total;
+    int P, Phi, K, Lr, xs, xu, qt_xpi, rs, ru, re, pv, wv, qu, fv, dsv, duv, Dx, Du, FD, Mu, AB, L0, prp, hp, misc, total;
     __host__ __device__ static WaveLds make(int N, int NX, int NU, int NP, int mpad, bool store_phi) {
         const int NS = NX + NP, NV = NS + NU;
         WaveLds o;
         int c = 0;
-        o.P = c;   c += (N + 1) * NS * NS;
+        o.P = c;   c += (N + 1) * pk_stride(NS);
         o.Phi = c; c += store_phi ? N * NS * NS : 0;
         o.K = c;   c += N * NU * NS;
         o.Lr = c;  c += N * NU * NU;
@@ -152,6 +161,7 @@ struct WaveLds {
         o.AB = c;  c += NS * NS + NS * NU;
         o.L0 = c;  c += NP * NP;
         o.prp = c; c += mpad;              // predictor dt*dlam of the polytope rows
+        o.hp = c;  c += mpad;              // this instance's polytope right-hand side
         o.misc = c; c += 8;
         o.total = (c + 1) & ~1;
         return o;
@@ -271,7 +281,13 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     };
     // polytope rows
     double tp[RPL], lp[RPL], itp[RPL];
-    const double* hpi = a.hp + (int64_t)inst * a.shp;
+    // polytope right-hand side: one coalesced read into this wave's LDS slot
+    double* hpi = W + L.hp;
+    {
+        const double* hg = a.hp + (int64_t)inst * a.shp;
+        for (int r = lane; r < mp; r += WAVE) hpi[r] = hg[r];
+        wave_sync();
+    }
     auto prow = [&](int q) __attribute__((always_inline)) -> bool { return lane + WAVE * q < mp; };
 
     // row count and primal data scale
@@ -450,12 +466,11 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     };
 
     // ======================= Riccati factorisation =========================================
-    // Riccati-factor lane roles:
-    //   phase A  lane (xa, ja), xa < NU, ja < NV : input row M_{u_xa, ja} = Ht + Bbar_xa' P F_ja
-    //   phase B  lane (ib, jb), ib <= jb < NS    : K columns, Phi = Abar + Bbar K, P_k(ib, jb)
-    const int xa = lane / NV, ja = lane % NV;
-    const bool alane = lane < NU * NV;
-    const int ib = lane / NS, jb = lane % NS;
+    // Riccati-factor lane roles: lane (ib, jb) = (lane / NS, lane % NS), ib <= jb < NS, owns
+    // entry (ib, jb) of P_k.  Every lane forms the input-row quantities of ITS two columns
+    // itself (g = P_{k+1} Bbar, M_u(:, ib), M_u(:, jb), Rhat, K_ib, K_jb), so the only
+    // cross-lane traffic per stage is P_k itself, broadcast through the packed LDS table.
+    const int ib = (lane < NS * NS) ? lane / NS : 0, jb = (lane < NS * NS) ? lane % NS : 0;
     const bool blane = lane < NS * NS && ib <= jb;
     auto factor = [&]() __attribute__((always_inline)) -> bool {
         // one reciprocal of t per row per iteration (reused by both solves and the steps)
@@ -520,20 +535,15 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 }
         }
         wave_sync();
-        // per-lane columns of F = [Abar Bbar] used by the two phases (constant over stages)
-        double FjA[NS], BxA[NS], AiB[NS], AjB[NS];
+        // per-lane columns ib, jb of Abar and the (uniform) Bbar, constant over the stages
+        double Ai[NS], Aj[NS], Bl[NS][NU];
 #pragma unroll
         for (int a_ = 0; a_ < NS; ++a_) {
-            FjA[a_] = alane ? (ja < NS ? Abar(a_, ja) : Bbar(a_, ja - NS)) : 0.0;
-            BxA[a_] = alane ? Bbar(a_, xa) : 0.0;
-            AiB[a_] = (lane < NS * NS) ? Abar(a_, ib) : 0.0;
-            AjB[a_] = (lane < NS * NS) ? Abar(a_, jb) : 0.0;
-        }
-        double Bl[NS][NU];
-#pragma unroll
-        for (int a_ = 0; a_ < NS; ++a_)
+            Ai[a_] = Abar(a_, ib);
+            Aj[a_] = Abar(a_, jb);
 #pragma unroll
             for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
+        }
         // Htilde entry (i, j) of stage k
         auto ht = [&](int k, int i, int j) __attribute__((always_inline)) -> double {
             double h = Hs[k * hstride + i * NV + j];
@@ -545,137 +555,145 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             return h;
         };
         // stage-k entries each lane needs (prefetched one stage ahead of the recursion)
-        struct StageH { double hA, hij, huj[NU], hiu[NU], huu[NU][NU]; };
+        struct StageH { double hij, hui[NU], huj[NU], huu[NU][NU]; };
         auto load_h = [&](int k, StageH& sh) __attribute__((always_inline)) {
-            const int xa_ = alane ? xa : 0, ja_ = alane ? ja : 0;
-            const int ib_ = (lane < NS * NS) ? ib : 0, jb_ = (lane < NS * NS) ? jb : 0;
-            sh.hA = ht(k, NS + xa_, ja_);
-            sh.hij = ht(k, ib_, jb_);
+            sh.hij = ht(k, ib, jb);
 #pragma unroll
             for (int x = 0; x < NU; ++x) {
-                sh.huj[x] = ht(k, NS + x, jb_);
-                sh.hiu[x] = ht(k, ib_, NS + x);
+                sh.hui[x] = ht(k, NS + x, ib);
+                sh.huj[x] = ht(k, NS + x, jb);
 #pragma unroll
                 for (int y = 0; y < NU; ++y) sh.huu[x][y] = ht(k, NS + x, NS + y);
             }
         };
-        // P_N (uniform copy in every lane, stored for the solves)
-        double Pu[NS][NS];
-        {
-            const int ib_ = (lane < NS * NS) ? ib : 0, jb_ = (lane < NS * NS) ? jb : 0;
-            const double v = ht(N, ib_, jb_);
-            if (lane < NS * NS) W[L.P + N * NS * NS + ib * NS + jb] = v;
+        // P_k broadcast: the owning lanes store the packed upper triangle, every lane reads the
+        // stage slot back (ds_read_b128, same address in all lanes)
+        constexpr int PST = pk_stride(NS);
+        double pu[PST];
+        auto bcast_p = [&](int k) __attribute__((always_inline)) {
+            wave_sync();
+            const double2* src = reinterpret_cast<const double2*>(W + L.P + k * PST);
 #pragma unroll
-            for (int i = 0; i < NS; ++i)
-#pragma unroll
-                for (int c = 0; c < NS; ++c) Pu[i][c] = rl(v, i * NS + c);
-        }
+            for (int q = 0; q < PST / 2; ++q) {
+                const double2 t2 = src[q];
+                pu[2 * q] = t2.x;
+                pu[2 * q + 1] = t2.y;
+            }
+        };
+        auto Pm = [&](int a_, int b_) __attribute__((always_inline)) -> double { return pu[pk_idx(NS, a_, b_)]; };
+        if (blane) W[L.P + N * PST + pk_idx(NS, ib, jb)] = ht(N, ib, jb);
+        bcast_p(N);
         STAMP(2);
         bool ok = true;
         StageH cur, nxt;
         load_h(N - 1, cur);
         for (int k = N - 1; k >= 0; --k) {
             if (k > 0) load_h(k - 1, nxt);
-            // phase A: input rows M_u = Ht_u + Bbar' P F  (lane (xa, ja))
-            double mA;
-            {
-                double acc = 0.0;
-#pragma unroll
-                for (int a_ = 0; a_ < NS; ++a_) {
-                    double pf = 0.0;
-#pragma unroll
-                    for (int b = 0; b < NS; ++b) pf += Pu[a_][b] * FjA[b];
-                    acc += BxA[a_] * pf;
-                }
-                mA = cur.hA + acc;
-            }
-            double Mu[NU][NV];
-#pragma unroll
-            for (int x = 0; x < NU; ++x)
-#pragma unroll
-                for (int c = 0; c < NV; ++c) Mu[x][c] = rl(mA, x * NV + c);
-            double Ruu[NU][NU], Lc[NU][NU];
-#pragma unroll
-            for (int x = 0; x < NU; ++x)
-#pragma unroll
-                for (int y = 0; y < NU; ++y) Ruu[x][y] = Mu[x][NS + y];
-            ok = chol_small<NU>(Ruu, Lc) && ok;
-            double Lf[NU * NU];
-#pragma unroll
-            for (int x = 0; x < NU; ++x)
-#pragma unroll
-                for (int y = 0; y < NU; ++y) Lf[x * NU + y] = Lc[x][y];
-            // phase B: K columns ib, jb; Phi = Abar + Bbar K; Joseph-form P_k(ib, jb)
-            double Ki[NU], Kj[NU];
-#pragma unroll
-            for (int x = 0; x < NU; ++x) { Ki[x] = -sel<NV>(Mu[x], ib); Kj[x] = -sel<NV>(Mu[x], jb); }
-            chol_solve_small<NU>(Lf, Ki);
-            chol_solve_small<NU>(Lf, Kj);
-            double Phi_i[NS], Phi_j[NS];
+            // g = P_{k+1} Bbar (uniform) and G_jb = P_{k+1} Abar(:, jb)
+            double g[NS][NU], Gj[NS];
 #pragma unroll
             for (int a_ = 0; a_ < NS; ++a_) {
-                double vi = AiB[a_], vj = AjB[a_];
+                double gj = 0.0;
 #pragma unroll
-                for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vj += Bl[a_][x] * Kj[x]; }
-                Phi_i[a_] = vi; Phi_j[a_] = vj;
+                for (int b = 0; b < NS; ++b) gj += Pm(a_, b) * Aj[b];
+                Gj[a_] = gj;
+#pragma unroll
+                for (int x = 0; x < NU; ++x) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int b = 0; b < NS; ++b) acc += Pm(a_, b) * Bl[b][x];
+                    g[a_][x] = acc;
+                }
             }
+            // input rows of M = Ht + F' P F for columns ib, jb and Rhat = M_uu
+            double mi[NU], mj[NU], Ruu[NU][NU];
+#pragma unroll
+            for (int x = 0; x < NU; ++x) {
+                double vi = cur.hui[x], vj = cur.huj[x];
+#pragma unroll
+                for (int a_ = 0; a_ < NS; ++a_) { vi += g[a_][x] * Ai[a_]; vj += g[a_][x] * Aj[a_]; }
+                mi[x] = vi;
+                mj[x] = vj;
+#pragma unroll
+                for (int y = 0; y < NU; ++y) {
+                    double r = cur.huu[x][y];
+#pragma unroll
+                    for (int a_ = 0; a_ < NS; ++a_) r += g[a_][x] * Bl[a_][y];
+                    Ruu[x][y] = r;
+                }
+            }
+            // K columns ib, jb:  K = -Rhat^{-1} M_us  (nu = 1: one reciprocal; else Cholesky)
+            double Ki[NU], Kj[NU], Lf[NU * NU];
+            if constexpr (NU == 1) {
+                ok = ok && (Ruu[0][0] > 0.0);
+                const double rinv = 1.0 / Ruu[0][0];
+                Lf[0] = rinv;
+                Ki[0] = -mi[0] * rinv;
+                Kj[0] = -mj[0] * rinv;
+            } else {
+                double Lc[NU][NU];
+                ok = chol_small<NU>(Ruu, Lc) && ok;
+#pragma unroll
+                for (int x = 0; x < NU; ++x)
+#pragma unroll
+                    for (int y = 0; y < NU; ++y) Lf[x * NU + y] = Lc[x][y];
+#pragma unroll
+                for (int x = 0; x < NU; ++x) { Ki[x] = -mi[x]; Kj[x] = -mj[x]; }
+                chol_solve_small<NU>(Lf, Ki);
+                chol_solve_small<NU>(Lf, Kj);
+            }
+            // Phi(:, ib) = Abar(:, ib) + Bbar K_ib ; T_jb = P Phi(:, jb) = G_jb + g K_jb
+            double Phi_i[NS], Tj[NS];
+#pragma unroll
+            for (int a_ = 0; a_ < NS; ++a_) {
+                double vi = Ai[a_], vt = Gj[a_];
+#pragma unroll
+                for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vt += g[a_][x] * Kj[x]; }
+                Phi_i[a_] = vi;
+                Tj[a_] = vt;
+            }
+            // Joseph form  P_k(ib, jb) = [I;K]' Ht [I;K] + Phi(:, ib)' P Phi(:, jb)
             double v = cur.hij;
 #pragma unroll
             for (int x = 0; x < NU; ++x) {
-                v += Ki[x] * cur.huj[x] + cur.hiu[x] * Kj[x];
+                v += Ki[x] * cur.huj[x] + cur.hui[x] * Kj[x];
 #pragma unroll
                 for (int y = 0; y < NU; ++y) v += Ki[x] * cur.huu[x][y] * Kj[y];
             }
             double acc = 0.0;
 #pragma unroll
-            for (int a_ = 0; a_ < NS; ++a_) {
-                double pf = 0.0;
-#pragma unroll
-                for (int b = 0; b < NS; ++b) pf += Pu[a_][b] * Phi_j[b];
-                acc += Phi_i[a_] * pf;
-            }
+            for (int a_ = 0; a_ < NS; ++a_) acc += Phi_i[a_] * Tj[a_];
             v += acc;
-            // tables for the solves (stores only; nothing below waits on them)
-            if (blane) {
-                W[L.P + k * NS * NS + ib * NS + jb] = v;
-                W[L.P + k * NS * NS + jb * NS + ib] = v;
-                if (ib == 0) {
+            // tables for the solves
+            if (blane) W[L.P + k * PST + pk_idx(NS, ib, jb)] = v;
+            if (lane < NS) {        // lane (0, jb): column jb of K
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + jb] = Kj[x];
-                    if (kPhi) {
+                for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + jb] = Kj[x];
+            }
+            if (kPhi && blane && ib == jb) {   // diagonal lane (ib, ib): column ib of Phi
 #pragma unroll
-                        for (int a_ = 0; a_ < NS; ++a_) W[L.Phi + k * NS * NS + a_ * NS + jb] = Phi_j[a_];
-                    }
-                }
+                for (int a_ = 0; a_ < NS; ++a_) W[L.Phi + k * NS * NS + a_ * NS + ib] = Phi_i[a_];
             }
             if (lane == 0) {
 #pragma unroll
                 for (int x = 0; x < NU * NU; ++x) W[L.Lr + k * NU * NU + x] = Lf[x];
             }
-            // P_k to every lane (upper-triangle lanes hold the values)
-#pragma unroll
-            for (int i = 0; i < NS; ++i)
-#pragma unroll
-                for (int c = i; c < NS; ++c) {
-                    const double pv_ = rl(v, i * NS + c);
-                    Pu[i][c] = pv_;
-                    Pu[c][i] = pv_;
-                }
+            bcast_p(k);
             cur = nxt;
         }
-        double Pr[NS][NS];
-#pragma unroll
-        for (int i = 0; i < NS; ++i)
-#pragma unroll
-            for (int c = 0; c < NS; ++c) Pr[i][c] = Pu[i][c];
         STAMP(3);
-        // Cholesky factor of the theta block of P_0
+        // factor of the theta block of P_0 (np = 1: its reciprocal)
         double Pt[NP][NP], L0[NP][NP];
 #pragma unroll
         for (int x = 0; x < NP; ++x)
 #pragma unroll
-            for (int y = 0; y < NP; ++y) Pt[x][y] = Pr[NX + x][NX + y];
-        ok = chol_small<NP>(Pt, L0) && ok;
+            for (int y = 0; y < NP; ++y) Pt[x][y] = Pm(NX + x, NX + y);
+        if constexpr (NP == 1) {
+            ok = ok && (Pt[0][0] > 0.0);
+            L0[0][0] = 1.0 / Pt[0][0];
+        } else {
+            ok = chol_small<NP>(Pt, L0) && ok;
+        }
         if (lane == 0) {
 #pragma unroll
             for (int x = 0; x < NP; ++x)
@@ -758,7 +776,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
-                const double* Pn = W + L.P + (k + 1) * NS * NS;
+                const double* Pn = W + L.P + (k + 1) * pk_stride(NS);
                 const double* Kk = W + L.K + k * NU * NS;
                 double rek[NS], wk[NS], qtk[NS];
 #pragma unroll
@@ -767,7 +785,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 for (int i = 0; i < NS; ++i) {
                     double v = 0.0;
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Pn[i * NS + c] * rek[c];
+                    for (int c = 0; c < NS; ++c) v += Pn[pk_idx(NS, i, c)] * rek[c];
                     wk[i] = v;
                     W[L.wv + k * NS + i] = v;
                     double qq = qs[j][i];
@@ -1043,12 +1061,12 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int i = 0; i < NS; ++i) dsk[i] = W[L.dsv + k * NS + i];
             if (k >= 1) {
-                const double* Pk = W + L.P + k * NS * NS;
+                const double* Pk = W + L.P + k * pk_stride(NS);
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     double v = W[L.pv + k * NS + i];
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Pk[i * NS + c] * dsk[c];
+                    for (int c = 0; c < NS; ++c) v += Pk[pk_idx(NS, i, c)] * dsk[c];
                     pi[j][i] += al * v;
                 }
             }

@@ -53,10 +53,16 @@ static int perm_of(const prob_t* P, int i) {
 }
 
 /* ---------------- small dense helpers ---------------- */
-static int chol_fac(int n, const double* M, double* L) {
-    /* lower Cholesky factor (row-major n x n, n <= MAXNS) with a static pivot floor.  The
-     * factor is applied by substitution (chol_solve): an explicit inverse of the
-     * ill-conditioned Rhat near convergence loses the stationarity residual. */
+static int spd_fac(int n, const double* M, double* L) {
+    /* factor of a small SPD matrix for spd_solve.  n = 1: L holds 1/M (one reciprocal, as the
+     * kernel stores it); n > 1: lower Cholesky factor (row-major) with a static pivot floor,
+     * applied by substitution: an explicit inverse of the ill-conditioned Rhat near convergence
+     * loses the stationarity residual. */
+    if (n == 1) {
+        if (!(M[0] > 0)) return -1;
+        L[0] = 1.0 / M[0];
+        return 0;
+    }
     for (int i = 0; i < n * n; ++i) L[i] = 0.0;
     for (int j = 0; j < n; ++j) {
         double d = M[j * n + j];
@@ -75,8 +81,12 @@ static int chol_fac(int n, const double* M, double* L) {
     return 0;
 }
 
-static void chol_solve(int n, const double* L, double* b) {
-    /* b <- (L L')^{-1} b */
+static void spd_solve(int n, const double* L, double* b) {
+    /* b <- M^{-1} b from spd_fac's factor */
+    if (n == 1) {
+        b[0] = b[0] * L[0];
+        return;
+    }
     for (int i = 0; i < n; ++i) {
         double v = b[i];
         for (int k = 0; k < i; ++k) v -= L[i * n + k] * b[k];
@@ -245,42 +255,59 @@ static int factor(const prob_t* P, work_t* W) {
         for (int j = 0; j < ns; ++j) PN[i * ns + j] = HT(N, i, j);
     for (int k = N - 1; k >= 0; --k) {
         const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
-        /* input rows of M = Ht + F' Pn F, F = [Abar Bbar]:  Rhat = M_uu, Shat = M_us */
-        double F[MAXNS][MAXNV];
+        /* g = Pn Bbar, G = Pn Abar;  input rows of M = Ht + F' Pn F, F = [Abar Bbar]:
+         * M_us(:, j) = Ht_us(:, j) + g' Abar(:, j),  Rhat = M_uu = Ht_uu + g' Bbar  (the kernel
+         * forms the same products in the same association, bqp_ocp.hip factor()) */
+        double g[MAXNS][MAXNU], G[MAXNS][MAXNS];
         for (int a = 0; a < ns; ++a) {
-            for (int j = 0; j < ns; ++j) F[a][j] = P->Abar[a][j];
-            for (int j = 0; j < nu; ++j) F[a][ns + j] = P->Bbar[a][j];
+            for (int j = 0; j < ns; ++j) {
+                double acc = 0;
+                for (int b = 0; b < ns; ++b) acc += Pn[a * ns + b] * P->Abar[b][j];
+                G[a][j] = acc;
+            }
+            for (int x = 0; x < nu; ++x) {
+                double acc = 0;
+                for (int b = 0; b < ns; ++b) acc += Pn[a * ns + b] * P->Bbar[b][x];
+                g[a][x] = acc;
+            }
         }
         double Mu[MAXNU][MAXNV];
-        for (int x = 0; x < nu; ++x)
-            for (int j = 0; j < nv; ++j) {
-                double acc = 0;
-                for (int a = 0; a < ns; ++a) {
-                    double pf = 0;
-                    for (int b = 0; b < ns; ++b) pf += Pn[a * ns + b] * F[b][j];
-                    acc += P->Bbar[a][x] * pf;
-                }
-                Mu[x][j] = HT(k, ns + x, j) + acc;
+        for (int x = 0; x < nu; ++x) {
+            for (int j = 0; j < ns; ++j) {
+                double acc = HT(k, ns + x, j);
+                for (int a = 0; a < ns; ++a) acc += g[a][x] * P->Abar[a][j];
+                Mu[x][j] = acc;
             }
+            for (int y = 0; y < nu; ++y) {
+                double acc = HT(k, ns + x, ns + y);
+                for (int a = 0; a < ns; ++a) acc += g[a][x] * P->Bbar[a][y];
+                Mu[x][ns + y] = acc;
+            }
+        }
         double Ruu[MAXNU * MAXNU];
-        double* Lk = W->Rinv + (size_t)k * nu * nu;    /* Cholesky factor of Rhat_k */
+        double* Lk = W->Rinv + (size_t)k * nu * nu;    /* factor of Rhat_k (spd_fac) */
         for (int a = 0; a < nu; ++a)
             for (int b = 0; b < nu; ++b) Ruu[a * nu + b] = Mu[a][ns + b];
-        if (chol_fac(nu, Ruu, Lk)) return -1;
+        if (spd_fac(nu, Ruu, Lk)) return -1;
         double* Kk = W->Ktab + (size_t)k * nu * ns;
         for (int j = 0; j < ns; ++j) {
             double col[MAXNU];
             for (int b = 0; b < nu; ++b) col[b] = -Mu[b][j];
-            chol_solve(nu, Lk, col);
+            spd_solve(nu, Lk, col);
             for (int a = 0; a < nu; ++a) Kk[a * ns + j] = col[a];
         }
-        /* Joseph form: P_k = [I;K]' Ht [I;K] + Phi' Pn Phi,  Phi = Abar + Bbar K */
-        double Phi[MAXNS][MAXNS];
+        /* Joseph form: P_k = [I;K]' Ht [I;K] + Phi' Pn Phi,  Phi = Abar + Bbar K, with
+         * Pn Phi(:, j) = G(:, j) + g K(:, j) */
+        double Phi[MAXNS][MAXNS], T[MAXNS][MAXNS];
         for (int a = 0; a < ns; ++a)
             for (int j = 0; j < ns; ++j) {
-                double v = P->Abar[a][j];
-                for (int x = 0; x < nu; ++x) v += P->Bbar[a][x] * Kk[x * ns + j];
+                double v = P->Abar[a][j], t = G[a][j];
+                for (int x = 0; x < nu; ++x) {
+                    v += P->Bbar[a][x] * Kk[x * ns + j];
+                    t += g[a][x] * Kk[x * ns + j];
+                }
                 Phi[a][j] = v;
+                T[a][j] = t;
             }
         double* Pk = W->Ptab + (size_t)k * ns * ns;
         double* Phk = W->Phit + (size_t)k * ns * ns;   /* closed loop Phi_k, row-major */
@@ -294,11 +321,7 @@ static int factor(const prob_t* P, work_t* W) {
                     for (int y = 0; y < nu; ++y) v += Kk[x * ns + i] * HT(k, ns + x, ns + y) * Kk[y * ns + j];
                 }
                 double acc = 0;
-                for (int a = 0; a < ns; ++a) {
-                    double pf = 0;
-                    for (int b = 0; b < ns; ++b) pf += Pn[a * ns + b] * Phi[b][j];
-                    acc += Phi[a][i] * pf;
-                }
+                for (int a = 0; a < ns; ++a) acc += Phi[a][i] * T[a][j];
                 v += acc;
                 Pk[i * ns + j] = v;
                 Pk[j * ns + i] = v;
@@ -312,7 +335,7 @@ static int factor(const prob_t* P, work_t* W) {
         const double* P0 = W->Ptab;
         for (int a = 0; a < np; ++a)
             for (int b = 0; b < np; ++b) Pt[a * np + b] = P0[(nx + a) * ns + nx + b];
-        if (chol_fac(np, Pt, W->P0inv)) return -1;    /* factor of P_0[theta,theta] */
+        if (spd_fac(np, Pt, W->P0inv)) return -1;    /* factor of P_0[theta,theta] */
     }
     return 0;
 }
@@ -395,7 +418,7 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             r[a] = v;
         }
         for (int a = 0; a < nu; ++a) r[a] = -r[a];
-        chol_solve(nu, W->Rinv + (size_t)k * nu * nu, r);
+        spd_solve(nu, W->Rinv + (size_t)k * nu * nu, r);
         for (int a = 0; a < nu; ++a) W->kff[k * nu + a] = r[a];
         for (int i = 0; i < ns; ++i) {
             double v = W->re[k * ns + i];
@@ -408,7 +431,7 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
     {
         double r[MAXNS];
         for (int a = 0; a < np; ++a) r[a] = -W->p[nx + a];
-        chol_solve(np, W->P0inv, r);
+        spd_solve(np, W->P0inv, r);
         for (int a = 0; a < np; ++a) W->ds[nx + a] = r[a];
     }
     for (int k = 0; k < N; ++k) {

@@ -1,7 +1,16 @@
 #!/bin/bash
-# quick GPU iteration: parity tests, stamps breakdown, short bench
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
-tail -n 6 gpurun_out/pytest_gpu.log
-timeout -k 10 200 python tools/stamps.py 1024 > gpurun_out/stamps.log 2>&1; tail -n 18 gpurun_out/stamps.log
-timeout -k 10 300 python bench.py --steps 30 --warmup 3 --no-cpu > gpurun_out/bench.log 2>&1; tail -c 900 gpurun_out/bench.log
+# Quick GPU iteration: parity tests, per-phase stamps breakdown, short bench (no CPU leg).
+# Each GPU step has its own limit; steps are chained with && so the first failure ends the call.
+# usage: tools/gpu_iter.sh TAG
+set -o pipefail
+TAG=${1:-iter}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
+timeout -k 10 200 python tools/stamps.py 1024 > $OUT/stamps.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 30 --warmup 3 --no-cpu > $OUT/bench.log 2>&1
+rc=$?
+tail -n 4 $OUT/pytest_gpu.log
+[ -f $OUT/stamps.log ] && tail -n 18 $OUT/stamps.log
+[ -f $OUT/bench.log ] && tail -c 900 $OUT/bench.log
+exit $rc

@@ -154,8 +154,8 @@ struct WaveLds {
         o.fv = c;  c += (N + 1) * NS;
         o.dsv = c; c += (N + 1) * NS;
         o.duv = c; c += (N + 1) * NU;
-        o.Dx = c;  c += (N + 1) * NX;
-        o.Du = c;  c += (N + 1) * NU;
+        o.Dx = c;  c += (N + 1) * NV;      // box diagonal of stage k in internal order (theta 0)
+        o.Du = o.Dx;
         o.FD = c;  c += NV * NV;
         o.Mu = c;  c += NU * NV;
         o.AB = c;  c += NS * NS + NS * NU;
@@ -487,15 +487,17 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     double d = 0;
                     if (xpres(j, i, 0)) d += lx[j][i][0] * itx[j][i][0];
                     if (xpres(j, i, 1)) d += lx[j][i][1] * itx[j][i][1];
-                    W[L.Dx + k * NX + i] = d;
+                    W[L.Dx + k * NV + i] = d;
                 }
 #pragma unroll
                 for (int i = 0; i < NU; ++i) {
                     double d = 0;
                     if (upres(j, i, 0)) d += lu[j][i][0] * itu[j][i][0];
                     if (upres(j, i, 1)) d += lu[j][i][1] * itu[j][i][1];
-                    W[L.Du + k * NU + i] = d;
+                    W[L.Dx + k * NV + NS + i] = d;
                 }
+#pragma unroll
+                for (int i = NX; i < NS; ++i) W[L.Dx + k * NV + i] = 0.0;
             }
         }
         STAMP(1);
@@ -545,25 +547,51 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
         }
         // Htilde entry (i, j) of stage k
+        // (branch-free: every operand is loaded unconditionally and selected, so the loads of a
+        // stage issue back to back and are waited for once)
         auto ht = [&](int k, int i, int j) __attribute__((always_inline)) -> double {
-            double h = Hs[k * hstride + i * NV + j];
-            if (i == j) {
-                if (i < NX) h += W[L.Dx + k * NX + i];
-                else if (i >= NS) h += W[L.Du + k * NU + (i - NS)];
-            }
-            if (k == kp) h += W[L.FD + i * NV + j];
-            return h;
+            const double h = Hs[k * hstride + i * NV + j];
+            const double d = W[L.Dx + k * NV + i];
+            const double f = W[L.FD + i * NV + j];
+            return (h + (i == j ? d : 0.0)) + (k == kp ? f : 0.0);
         };
-        // stage-k entries each lane needs (prefetched one stage ahead of the recursion)
-        struct StageH { double hij, hui[NU], huj[NU], huu[NU][NU]; };
+        // stage-k entries each lane needs, prefetched one stage ahead of the recursion as RAW
+        // operands (cost entry, box diagonal): they are combined only when the stage is
+        // processed, so the prefetch loads are not waited for inside the stage that issues them.
+        // The polytope term F'DF enters at stage kp only (a uniform branch).
+        struct StageH { double hij, dij, hui[NU], huj[NU], huu[NU][NU], duu[NU]; };
         auto load_h = [&](int k, StageH& sh) __attribute__((always_inline)) {
-            sh.hij = ht(k, ib, jb);
+            const double* Hk = Hs + k * hstride;
+            sh.hij = Hk[ib * NV + jb];
+            sh.dij = W[L.Dx + k * NV + ib];
 #pragma unroll
             for (int x = 0; x < NU; ++x) {
-                sh.hui[x] = ht(k, NS + x, ib);
-                sh.huj[x] = ht(k, NS + x, jb);
+                sh.hui[x] = Hk[(NS + x) * NV + ib];
+                sh.huj[x] = Hk[(NS + x) * NV + jb];
+                sh.duu[x] = W[L.Dx + k * NV + NS + x];
 #pragma unroll
-                for (int y = 0; y < NU; ++y) sh.huu[x][y] = ht(k, NS + x, NS + y);
+                for (int y = 0; y < NU; ++y) sh.huu[x][y] = Hk[(NS + x) * NV + NS + y];
+            }
+        };
+        // Htilde entries of the stage (same operation order as ht())
+        auto combine_h = [&](int k, const StageH& sh, StageH& o) __attribute__((always_inline)) {
+            o.hij = sh.hij + (ib == jb ? sh.dij : 0.0);
+#pragma unroll
+            for (int x = 0; x < NU; ++x) {
+                o.hui[x] = sh.hui[x];
+                o.huj[x] = sh.huj[x];
+#pragma unroll
+                for (int y = 0; y < NU; ++y) o.huu[x][y] = sh.huu[x][y] + (x == y ? sh.duu[x] : 0.0);
+            }
+            if (k == kp) {
+                o.hij += W[L.FD + ib * NV + jb];
+#pragma unroll
+                for (int x = 0; x < NU; ++x) {
+                    o.hui[x] += W[L.FD + (NS + x) * NV + ib];
+                    o.huj[x] += W[L.FD + (NS + x) * NV + jb];
+#pragma unroll
+                    for (int y = 0; y < NU; ++y) o.huu[x][y] += W[L.FD + (NS + x) * NV + NS + y];
+                }
             }
         };
         // P_k broadcast: the owning lanes store the packed upper triangle, every lane reads the
@@ -585,9 +613,10 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         bcast_p(N);
         STAMP(2);
         bool ok = true;
-        StageH cur, nxt;
-        load_h(N - 1, cur);
+        StageH raw, nxt, cur;
+        load_h(N - 1, raw);
         for (int k = N - 1; k >= 0; --k) {
+            combine_h(k, raw, cur);
             if (k > 0) load_h(k - 1, nxt);
             // g = P_{k+1} Bbar (uniform) and G_jb = P_{k+1} Abar(:, jb)
             double g[NS][NU], Gj[NS];
@@ -679,7 +708,7 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 for (int x = 0; x < NU * NU; ++x) W[L.Lr + k * NU * NU + x] = Lf[x];
             }
             bcast_p(k);
-            cur = nxt;
+            raw = nxt;
         }
         STAMP(3);
         // factor of the theta block of P_0 (np = 1: its reciprocal)
@@ -837,7 +866,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             double p[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) p[i] = W[L.pv + N * NS + i];
-            double cc[NS], cq, nc[NS], nq;
             auto load_b = [&](int k, double (&col)[NS], double& q) __attribute__((always_inline)) {
                 q = W[L.qt_xpi + k * NS + li];
                 if constexpr (kPhi) {
@@ -853,18 +881,24 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     }
                 }
             };
-            load_b(N - 1, cc, cq);
-            for (int k = N - 1; k >= 0; --k) {
-                if (k > 0) load_b(k - 1, nc, nq);
-                double acc = cq;
+            // two register sets used alternately (stages k, k-1), each refilled two stages ahead
+            double c0[NS], q0, c1[NS], q1;
+            load_b(N - 1, c0, q0);
+            if (N >= 2) load_b(N - 2, c1, q1);
+            auto step_b = [&](int k, const double (&col)[NS], double q) __attribute__((always_inline)) {
+                double acc = q;
 #pragma unroll
-                for (int c = 0; c < NS; ++c) acc += cc[c] * p[c];
+                for (int c = 0; c < NS; ++c) acc += col[c] * p[c];
                 if (lane < NS) W[L.pv + k * NS + lane] = acc;
 #pragma unroll
                 for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
-#pragma unroll
-                for (int c = 0; c < NS; ++c) cc[c] = nc[c];
-                cq = nq;
+            };
+            for (int k = N - 1; k >= 0; k -= 2) {
+                step_b(k, c0, q0);
+                if (k >= 2) load_b(k - 2, c0, q0);
+                if (k == 0) break;
+                step_b(k - 1, c1, q1);
+                if (k >= 3) load_b(k - 3, c1, q1);
             }
         }
         wave_sync();
@@ -914,7 +948,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 for (int i = 0; i < NS; ++i) W[L.dsv + i] = d[i];
             }
             const int li = lane < NS ? lane : NS - 1;
-            double cr[NS], cf, nr[NS], nf;
             auto load_f = [&](int k, double (&row)[NS], double& f) __attribute__((always_inline)) {
                 f = W[L.fv + k * NS + li];
                 if constexpr (kPhi) {
@@ -930,18 +963,23 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     }
                 }
             };
-            load_f(0, cr, cf);
-            for (int k = 0; k < N; ++k) {
-                if (k + 1 < N) load_f(k + 1, nr, nf);
-                double acc = cf;
+            double r0_[NS], f0, r1_[NS], f1;
+            load_f(0, r0_, f0);
+            if (N >= 2) load_f(1, r1_, f1);
+            auto step_f = [&](int k, const double (&row)[NS], double f) __attribute__((always_inline)) {
+                double acc = f;
 #pragma unroll
-                for (int c = 0; c < NS; ++c) acc += cr[c] * d[c];
+                for (int c = 0; c < NS; ++c) acc += row[c] * d[c];
                 if (lane < NS) W[L.dsv + (k + 1) * NS + lane] = acc;
 #pragma unroll
                 for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
-#pragma unroll
-                for (int c = 0; c < NS; ++c) cr[c] = nr[c];
-                cf = nf;
+            };
+            for (int k = 0; k < N; k += 2) {
+                step_f(k, r0_, f0);
+                if (k + 2 < N) load_f(k + 2, r0_, f0);
+                if (k + 1 >= N) break;
+                step_f(k + 1, r1_, f1);
+                if (k + 3 < N) load_f(k + 3, r1_, f1);
             }
         }
         wave_sync();
@@ -1322,8 +1360,14 @@ hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
     const size_t lds = sizeof(double) * ((size_t)a.shared_doubles +
                                          (size_t)a.wpb * ocp_wave_lds_doubles(a.N, nx, nu, np, a.mpad));
+#ifdef BQP_ISA_ONLY_MG10
+    // codegen inspection build (make isa): the MG N<64, 616-row instance only
+    if (nx == 4 && nu == 1 && np == 1 && spl == 1 && rpl == 10) return launch_t<4, 1, 1, 1, 10>(a, blocks, lds, st);
+    return hipErrorInvalidValue;
+#else
     if (nx == 4 && nu == 1 && np == 1) return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);
     if (nx == 2 && nu == 2 && np == 2) return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st);
+#endif
     return hipErrorInvalidValue;
 }
 

@@ -188,17 +188,17 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     const int nv = nx + nu + np;
     const int mp = d->n_poly;
     const int hstride = nv * nv + 1;
-    const int mpad = std::max(64, ((mp + 63) / 64) * 64);
+    const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));   // = the kernel's RPL * 64
     const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;
     const int per_wave = bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
     const size_t lds_budget = 160 * 1024 / sizeof(double);
-    int wpb = 4;
+    int wpb = 4;   // instances per workgroup (two waves each)
     while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
     if ((size_t)shared_doubles + (size_t)per_wave > lds_budget) return BQP_E_UNSUPPORTED;
     // workspace: H, Fp, stats
     const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * 4;
 #ifdef BQP_STAMPS
-    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + (size_t)batch * 16)));
+    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + (size_t)batch * 32)));
 #else
     HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8)));
 #endif
@@ -435,15 +435,16 @@ int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_s
 
 #ifdef BQP_STAMPS
 // diagnostic build only: per-instance phase cycle counts of the last structured solve
+// (32 per instance: 16 stage-wave phases, 16 row-wave phases)
 int bqp_debug_stamps(bqp_handle h, int N, int nv, int mp, double* out) {
     if (!h || !out) return BQP_E_ARG;
     DevScope ds(h->device);
     const int hstride = nv * nv + 1;
-    const int mpad = std::max(64, ((mp + 63) / 64) * 64);
+    const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));
     const size_t off = (size_t)(N + 1) * hstride + (size_t)nv * mpad + (size_t)h->last_batch * 4 + 8;
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(out, (double*)h->work.p + off, sizeof(double) * h->last_batch * 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out, (double*)h->work.p + off, sizeof(double) * h->last_batch * 32, hipMemcpyDeviceToHost));
     return BQP_OK;
 }
 #endif

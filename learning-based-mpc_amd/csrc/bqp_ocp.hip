@@ -1,19 +1,25 @@
 // bqp_ocp.hip — batched structured Mehrotra predictor-corrector IPM for MPC QPs, gfx950.
 //
-// One wavefront (64 lanes) solves one MPC instance; a workgroup holds WPB instances that share
-// the stage-cost table H_k and the polytope (terminal-set) matrix in LDS.  Inside a wave the
-// lanes are re-assigned per phase:
-//   * stage phases   lane k (and k+64 when SPL=2) owns stage k: s_k=[x_k;theta], u_k, pi_k
-//                    and the slacks/duals of the box rows of stage k;
-//   * polytope rows  lane l owns rows l, l+64, ... (RPL rows): slack, dual, 1/slack in
-//                    registers; F'DF and F'e are reduced with DPP lane moves;
-//   * Riccati factor lane (i,j) owns entry (i,j) of the stage matrices (Joseph form); P_{k+1}
-//                    is broadcast from LDS at each stage (sequential over k);
-//   * Riccati solves every lane runs the NS-vector closed-loop recursion redundantly (no
-//                    cross-lane traffic on the sequential critical path).
-// Register budget (one wave per SIMD at the C2 batch): per-row residuals and steps are
-// recomputed from the stage vectors when needed instead of being kept live, so the kernel
-// holds ~85 fp64 values per lane.
+// Two wavefronts solve one MPC instance; a workgroup holds QPB instances (2*QPB waves) that
+// share the stage-cost table H_k and the polytope (terminal-set) matrix in LDS.
+//
+//   stage wave  lane k (and k+64 when SPL=2) owns stage k: s_k=[x_k;theta], u_k, pi_k.  It
+//               forms the stage residuals, runs the backward Riccati factorisation (lane (i,j)
+//               owns entry (i,j) of P_k, Joseph form) and the two Newton solves (closed-loop
+//               sweeps, readlane broadcast), and applies the primal/dual step.
+//   row wave    owns every inequality row: the box rows of stage k in lane k, and polytope rows
+//               l, l+64, ... (RPL per lane).  It forms the row residuals, the diagonal weights
+//               D = lam/t and F'DF, the complementarity right-hand sides, the step-length ratio
+//               tests, mu_aff / sigma, and the slack/multiplier updates.
+//
+// The waves exchange per-stage tables and scalars through the instance's LDS slot and meet at
+// seven workgroup barriers per iteration (B0..B6 below; I0..I3 for the starting point); both waves take the same decisions
+// from the same exchanged values, so the barrier sequence is identical and an instance whose
+// iteration ends leaves the loop on both waves at the same barrier (terminated waves drop out
+// of s_barrier).  Each wave keeps only its own state in registers, and the row work that does
+// not depend on the factorisation (F'DF, the predictor right-hand side) overlaps the stage
+// wave's Riccati recursion.
+//
 // The algorithm (and its operation order) is stated in oracle/ocp_ipm.py and restated in C in
 // oracle/cpu_ipm.c; the QP is the stage-wise form of the reference's per-step OCPs
 // (costLMPC.m / constraintsLMPC.m, DMS_tracking_LMPC_casadi.m:223-287, trackingMPC/costFunction.m).
@@ -82,13 +88,6 @@ __device__ __forceinline__ double rl(double v, int src) {
     r.y = __builtin_amdgcn_readlane(x.y, src);
     return __builtin_bit_cast(double, r);
 }
-template <int N>
-__device__ __forceinline__ double sel(const double (&row)[N], int idx) {
-    double r = row[0];
-#pragma unroll
-    for (int c = 1; c < N; ++c) r = (idx == c) ? row[c] : r;
-    return r;
-}
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
 template <int N>
@@ -118,7 +117,7 @@ __device__ __forceinline__ void chol_solve_small(const double* L, double (&b)[N]
         b[1] = b[1] / L[3];
         b[0] = (b[0] - L[2] * b[1]) / L[0];
     } else {
-        b[0] = b[0] * L[0];     // n = 1: L holds the reciprocal of the 1x1 matrix
+        b[0] = b[0] * L[0];
     }
 }
 
@@ -131,70 +130,62 @@ __host__ __device__ constexpr int pk_idx(int NS, int i, int j) {
     return i <= j ? i * NS - i * (i - 1) / 2 + (j - i) : j * NS - j * (j - 1) / 2 + (i - j);
 }
 
-// Per-wave LDS layout (in doubles), all sized from N at run time.
-struct WaveLds {
-    int P, Phi, K, Lr, xs, xu, qt_xpi, rs, ru, re, pv, wv, qu, fv, dsv, duv, Dx, Du, FD, Mu, AB, L0, prp, hp, misc, total;
-    __host__ __device__ static WaveLds make(int N, int NX, int NU, int NP, int mpad, bool store_phi) {
-        const int NS = NX + NP, NV = NS + NU;
-        WaveLds o;
+// Exchange scalars between the two waves of an instance (slots of the LDS xch block).
+enum : int {
+    X_CNT = 0,   // number of inequality rows (row wave, once)
+    X_BSR,       // max |finite bound| over the rows (row wave, once)
+    X_FEASB,     // max |row residual| (row wave, per iteration)
+    X_CS,        // sum t.lam over the rows (row wave, per iteration)
+    X_STOP,      // 1: leave the loop at B2 (stage wave)
+    X_ALPHA,     // corrector step length (row wave)
+    X_NXCH = 8
+};
+
+// Per-instance LDS layout (in doubles), sized from N at run time.
+struct QpLds {
+    int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, qu, fv, dsv, duv, dsc, duc, Dx, FD,
+        blam, ebox, bnd, gpp, gpe, prp, hp, xch, total;
+    __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad) {
+        const int NS = NX + NP, NV = NS + NU, NB = NX + NU;
+        QpLds o;
         int c = 0;
-        o.P = c;   c += (N + 1) * pk_stride(NS);
-        o.Phi = c; c += store_phi ? N * NS * NS : 0;
-        o.K = c;   c += N * NU * NS;
-        o.Lr = c;  c += N * NU * NU;
-        o.xs = c;  c += (N + 1) * NS;
-        o.xu = c;  c += (N + 1) * NU;
-        o.qt_xpi = c; c += (N + 1) * NS;   // pi exchange in residuals, qt in the solves
-        o.rs = c;  c += (N + 1) * NS;
-        o.ru = c;  c += (N + 1) * NU;
-        o.re = c;  c += (N + 1) * NS;
-        o.pv = c;  c += (N + 1) * NS;
-        o.wv = c;  c += (N + 1) * NS;
-        o.qu = c;  c += (N + 1) * NU;
-        o.fv = c;  c += (N + 1) * NS;
-        o.dsv = c; c += (N + 1) * NS;
-        o.duv = c; c += (N + 1) * NU;
-        o.Dx = c;  c += (N + 1) * NV;      // box diagonal of stage k in internal order (theta 0)
-        o.Du = o.Dx;
-        o.FD = c;  c += NV * NV;
-        o.Mu = c;  c += NU * NV;
-        o.AB = c;  c += NS * NS + NS * NU;
-        o.L0 = c;  c += NP * NP;
-        o.prp = c; c += mpad;              // predictor dt*dlam of the polytope rows
-        o.hp = c;  c += mpad;              // this instance's polytope right-hand side
-        o.misc = c; c += 8;
+        o.P = c;      c += (N + 1) * pk_stride(NS);  // Riccati P_k (packed)
+        o.K = c;      c += N * NU * NS;              // feedback K_k (row-major NU x NS)
+        o.Lr = c;     c += N * NU * NU;              // factor of Rhat_k (nu = 1: its reciprocal)
+        o.L0 = c;     c += NP * NP;                  // factor of P_0[theta, theta]
+        o.AB = c;     c += NS * NS + NS * NU;        // Abar (row-major), Bbar
+        o.xs = c;     c += (N + 1) * NS;             // s_k
+        o.xu = c;     c += (N + 1) * NU;             // u_k (u_N = 0)
+        o.qt_xpi = c; c += (N + 1) * NS;             // pi_k in the residuals, qhat_k in the solves
+        o.rs = c;     c += (N + 1) * NS;             // stationarity residual (s part)
+        o.ru = c;     c += (N + 1) * NU;             // stationarity residual (u part)
+        o.re = c;     c += (N + 1) * NS;             // dynamics residual
+        o.pv = c;     c += (N + 1) * NS;             // p_k of the backward sweep
+        o.wv = c;     c += (N + 1) * NS;             // P_{k+1} re_k
+        o.qu = c;     c += (N + 1) * NU;             // u right-hand side
+        o.fv = c;     c += (N + 1) * NS;             // forward-sweep drift f_k
+        o.dsv = c;    c += (N + 1) * NS;             // predictor direction (s)
+        o.duv = c;    c += (N + 1) * NU;             //                     (u)
+        o.dsc = c;    c += (N + 1) * NS;             // corrector direction (s)
+        o.duc = c;    c += (N + 1) * NU;             //                     (u)
+        o.Dx = c;     c += (N + 1) * NV;             // box diagonal of stage k (internal order, theta 0)
+        o.FD = c;     c += NV * NV;                  // polytope F'DF
+        o.blam = c;   c += (N + 1) * NB * 2;         // box multipliers [upper, lower] (0 if absent)
+        o.ebox = c;   c += (N + 1) * NB * 2;         // box right-hand-side terms [upper, lower]
+        o.bnd = c;    c += (N + 1) * NB * 2;         // box bounds [upper, lower]
+        o.gpp = c;    c += NV;                       // Fp' lam
+        o.gpe = c;    c += NV;                       // Fp' e
+        o.prp = c;    c += mpad;                     // predictor dt*dlam of the polytope rows
+        o.hp = c;     c += mpad;                     // polytope right-hand side
+        o.xch = c;    c += X_NXCH;
         o.total = (c + 1) & ~1;
         return o;
     }
 };
 
-template <int NX, int NU, int NP, int SPL, int RPL>
-__global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
-    constexpr int NS = NX + NP;
-    constexpr int NV = NS + NU;
-    constexpr bool kPhi = (SPL == 1);     // store closed-loop Phi_k (LDS budget allows at N<64)
-    extern __shared__ double lds[];
-    const int N = a.N, mp = a.mp, kp = a.kp;
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const int hstride = a.hstride;
-    const int mpad = a.mpad;
-    // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
-    double* Hs = lds;
-    double* Fs = lds + (N + 1) * hstride;
-    for (int i = threadIdx.x; i < (N + 1) * hstride; i += blockDim.x) Hs[i] = a.H[i];
-    for (int i = threadIdx.x; i < NV * mpad; i += blockDim.x) Fs[i] = a.Fp[i];
-    __syncthreads();
-    const int inst = blockIdx.x * a.wpb + wid;
-    if (inst >= a.batch) return;
-    const WaveLds L = WaveLds::make(N, NX, NU, NP, mpad, kPhi);
-    double* W = lds + a.shared_doubles + wid * L.total;
 #ifdef BQP_STAMPS
-    // diagnostic build only (see tools/stamps.py): cycles per phase, summed over the solve
-    unsigned long long st_last = __builtin_amdgcn_s_memtime();
-    unsigned long long st_acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) st_acc[i] = 0;
+// diagnostic build only (see tools/stamps.py): cycles per phase and per wave role, summed over
+// the solve; slots 0..15 stage wave, 16..31 row wave
 #define STAMP(id)                                                          \
     do {                                                                   \
         __builtin_amdgcn_s_waitcnt(0);                                     \
@@ -202,9 +193,44 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         st_acc[id] += _t - st_last;                                        \
         st_last = _t;                                                      \
     } while (0)
+#define STAMP_DECL                                                         \
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();             \
+    unsigned long long st_acc[16];                                         \
+    _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_) st_acc[i_] = 0
+#define STAMP_STORE(base)                                                  \
+    do {                                                                   \
+        if (lane == 0 && a.stamps) {                                       \
+            _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_)              \
+                a.stamps[(int64_t)inst * 32 + (base) + i_] = (double)st_acc[i_]; \
+        }                                                                  \
+    } while (0)
+#elif defined(BQP_ISA_ONLY_MG10)
+#define STAMP(id) asm volatile(";BQP_PHASE " #id)
+#define STAMP_DECL do { } while (0)
+#define STAMP_STORE(base) do { } while (0)
 #else
 #define STAMP(id) do { } while (0)
+#define STAMP_DECL do { } while (0)
+#define STAMP_STORE(base) do { } while (0)
 #endif
+
+#define BARRIER() __syncthreads()
+// scheduling fence between polytope rows of the row wave: keeps the scheduler from hoisting the
+// Fp loads of all RPL rows to the top of a phase (register pressure at two waves per SIMD)
+#define ROW_FENCE(q) do { if ((q) & 1) __builtin_amdgcn_sched_barrier(0); } while (0)
+
+// ==========================================================================================
+// stage wave
+// ==========================================================================================
+template <int NX, int NU, int NP, int SPL>
+__device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, const QpLds& L,
+                                           const double* Hs, int lane, int inst) {
+    constexpr int NS = NX + NP;
+    constexpr int NV = NS + NU;
+    constexpr int NB = NX + NU;
+    const int N = a.N, kp = a.kp, hstride = a.hstride;
+    double* X = W + L.xch;
+    STAMP_DECL;
 
     // ---------------- per-instance model -> LDS (Abar row-major, Bbar) ---------------------
     {
@@ -225,20 +251,22 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     double cb[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) cb[i] = (i < NX && a.c) ? a.c[(int64_t)inst * a.sc + i] : 0.0;
+    const double* wb = a.w ? a.w + (int64_t)inst * a.sw : nullptr;
+    // linear cost term of stage k, internal index i ([x; theta; u] from external [x; u; theta])
+    auto gterm = [&](int k, int i) __attribute__((always_inline)) -> double {
+        if (!wb || (k == N && i >= NS)) return 0.0;
+        const int e = (i < NX) ? i : (i < NS ? NX + NU + (i - NX) : NX + (i - NS));
+        return wb[(int64_t)k * NV + e];
+    };
 
-    // ---------------- stage-lane state ------------------------------------------------------
-    double s[SPL][NS], u[SPL][NU], pi[SPL][NS];
-    double tx[SPL][NX][2], lx[SPL][NX][2], itx[SPL][NX][2], bx[SPL][NX][2];   // ub, lb
-    double tu[SPL][NU][2], lu[SPL][NU][2], itu[SPL][NU][2], bu[SPL][NU][2];
-    double prx[SPL][NX][2], pru[SPL][NU][2];                                    // predictor dt*dlam
-    double kff[SPL][NU];
-    unsigned mx[SPL], mu_[SPL];
+    double s[SPL][NS], u[SPL][NU], pi[SPL][NS], kff[SPL][NU];
     const double* x0 = a.x0 + (int64_t)inst * a.sx0;
+    double x0max = 0.0;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) x0max = fmax(x0max, fabs(x0[i]));
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
         const int k = lane + WAVE * j;
-        const bool act = k <= N;
-        mx[j] = 0; mu_[j] = 0;
 #pragma unroll
         for (int i = 0; i < NS; ++i) { s[j][i] = 0.0; pi[j][i] = 0.0; }
 #pragma unroll
@@ -247,99 +275,10 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) s[j][i] = x0[i];
         }
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double ub = INFINITY, lb = -INFINITY;
-            if (act && k > 0) {
-                if (a.xub) ub = a.xub[(int64_t)inst * a.sxb + (int64_t)k * NX + i];
-                if (a.xlb) lb = a.xlb[(int64_t)inst * a.sxb + (int64_t)k * NX + i];
-            }
-            bx[j][i][0] = ub; bx[j][i][1] = lb;
-            if (isfinite(ub)) mx[j] |= 1u << (2 * i);
-            if (isfinite(lb)) mx[j] |= 2u << (2 * i);
-        }
-#pragma unroll
-        for (int i = 0; i < NU; ++i) {
-            double ub = INFINITY, lb = -INFINITY;
-            if (act && k < N) {
-                if (a.uub) ub = a.uub[(int64_t)inst * a.sub + (int64_t)k * NU + i];
-                if (a.ulb) lb = a.ulb[(int64_t)inst * a.sub + (int64_t)k * NU + i];
-            }
-            bu[j][i][0] = ub; bu[j][i][1] = lb;
-            if (isfinite(ub)) mu_[j] |= 1u << (2 * i);
-            if (isfinite(lb)) mu_[j] |= 2u << (2 * i);
-        }
     }
-    auto xpres = [&](int j, int i, int h) __attribute__((always_inline)) -> bool { return (mx[j] >> (2 * i + h)) & 1u; };
-    auto upres = [&](int j, int i, int h) __attribute__((always_inline)) -> bool { return (mu_[j] >> (2 * i + h)) & 1u; };
-    // linear cost term of stage k, internal index i ([x; theta; u] from external [x; u; theta])
-    const double* wb = a.w ? a.w + (int64_t)inst * a.sw : nullptr;
-    auto gterm = [&](int k, int i) __attribute__((always_inline)) -> double {
-        if (!wb || (k == N && i >= NS)) return 0.0;
-        const int e = (i < NX) ? i : (i < NS ? NX + NU + (i - NX) : NX + (i - NS));
-        return wb[(int64_t)k * NV + e];
-    };
-    // polytope rows
-    double tp[RPL], lp[RPL], itp[RPL];
-    // polytope right-hand side: one coalesced read into this wave's LDS slot
-    double* hpi = W + L.hp;
-    {
-        const double* hg = a.hp + (int64_t)inst * a.shp;
-        for (int r = lane; r < mp; r += WAVE) hpi[r] = hg[r];
-        wave_sync();
-    }
-    auto prow = [&](int q) __attribute__((always_inline)) -> bool { return lane + WAVE * q < mp; };
 
-    // row count and primal data scale
-    double mcount = 0, bsl = 0;
-#pragma unroll
-    for (int j = 0; j < SPL; ++j) {
-        mcount += __builtin_popcount(mx[j]) + __builtin_popcount(mu_[j]);
-        if (lane + WAVE * j == 0) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) bsl = fmax(bsl, fabs(x0[i]));
-        }
-#pragma unroll
-        for (int i = 0; i < NX; ++i)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (xpres(j, i, h)) bsl = fmax(bsl, fabs(bx[j][i][h]));
-#pragma unroll
-        for (int i = 0; i < NU; ++i)
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (upres(j, i, h)) bsl = fmax(bsl, fabs(bu[j][i][h]));
-    }
-#pragma unroll
-    for (int q = 0; q < RPL; ++q)
-        if (prow(q)) { mcount += 1.0; bsl = fmax(bsl, fabs(hpi[lane + WAVE * q])); }
-    mcount = wsum(mcount);
-    const double minv = 1.0 / fmax(mcount, 1.0);
-    const double bscale = wmax(bsl);
-
-    // ----- helpers: box / polytope row residuals and steps (recomputed, never stored) -------
-    auto rix = [&](int j, int i, int h) __attribute__((always_inline)) -> double {
-        return h == 0 ? s[j][i] + tx[j][i][0] - bx[j][i][0] : -s[j][i] + tx[j][i][1] + bx[j][i][1];
-    };
-    auto riu = [&](int j, int i, int h) __attribute__((always_inline)) -> double {
-        return h == 0 ? u[j][i] + tu[j][i][0] - bu[j][i][0] : -u[j][i] + tu[j][i][1] + bu[j][i][1];
-    };
-    auto load_vp = [&](double (&vp)[NV], int base_s, int base_u) {
-#pragma unroll
-        for (int c = 0; c < NS; ++c) vp[c] = W[base_s + kp * NS + c];
-#pragma unroll
-        for (int c = 0; c < NU; ++c) vp[NS + c] = (kp < N) ? W[base_u + kp * NU + c] : 0.0;
-    };
-    auto fdot = [&](int r, const double (&v)[NV]) -> double {
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < NV; ++c) acc += Fs[c * mpad + r] * v[c];
-        return acc;
-    };
-
-    // ======================= residuals =====================================================
-    // writes rs, ru, re (per stage) to LDS; returns stat, feas, comp sum, cost-gradient scale
-    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) __attribute__((always_inline)) {
+    // ---- stage vectors to LDS (s, u, pi) ----
+    auto write_state = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -347,19 +286,19 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) { W[L.xs + k * NS + i] = s[j][i]; W[L.qt_xpi + k * NS + i] = pi[j][i]; }
 #pragma unroll
-                for (int i = 0; i < NU; ++i) W[L.xu + k * NU + i] = u[j][i];
+                for (int i = 0; i < NU; ++i) W[L.xu + k * NU + i] = (k < N) ? u[j][i] : 0.0;
             }
         }
         wave_sync();
-        double st = 0, fe = 0, cs = 0, gs = 0;
-        double rsl[SPL][NS], rul[SPL][NU];
+    };
+
+    // ---- stage residuals without the row multipliers: rs' = g + Abar' pi_{k+1} - pi_k,
+    //      ru' = g_u + Bbar' pi_{k+1}, re = Abar s + Bbar u + c - s_{k+1}; returns max|re|, max|g|
+    auto stage_partials = [&](double& feasA, double& gsA) __attribute__((always_inline)) {
+        double fe = 0, gs = 0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) rsl[j][i] = 0.0;
-#pragma unroll
-            for (int i = 0; i < NU; ++i) rul[j][i] = 0.0;
             if (k > N) continue;
             const double* Hk = Hs + k * hstride;
             double v[NV];
@@ -387,24 +326,14 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     for (int c = 0; c < NS; ++c) acc += Abar(c, i) * pn[c];
                 }
                 if (k > 0) acc -= pi[j][i];
-                rsl[j][i] = acc;
+                W[L.rs + k * NS + i] = acc;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 double acc = gv[NS + i];
 #pragma unroll
                 for (int c = 0; c < NS; ++c) acc += Bbar(c, i) * pn[c];
-                rul[j][i] = (k < N) ? acc : 0.0;
-            }
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                if (xpres(j, i, 0)) { rsl[j][i] += lx[j][i][0]; fe = fmax(fe, fabs(rix(j, i, 0))); cs += tx[j][i][0] * lx[j][i][0]; }
-                if (xpres(j, i, 1)) { rsl[j][i] -= lx[j][i][1]; fe = fmax(fe, fabs(rix(j, i, 1))); cs += tx[j][i][1] * lx[j][i][1]; }
-            }
-#pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                if (upres(j, i, 0)) { rul[j][i] += lu[j][i][0]; fe = fmax(fe, fabs(riu(j, i, 0))); cs += tu[j][i][0] * lu[j][i][0]; }
-                if (upres(j, i, 1)) { rul[j][i] -= lu[j][i][1]; fe = fmax(fe, fabs(riu(j, i, 1))); cs += tu[j][i][1] * lu[j][i][1]; }
+                W[L.ru + k * NU + i] = (k < N) ? acc : 0.0;
             }
             if (k < N) {
 #pragma unroll
@@ -419,146 +348,77 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 }
             }
         }
-        // polytope rows: ri and F'lam partials
-        double vp[NV];
-        load_vp(vp, L.xs, L.xu);
+        feasA = wmax(fe);
+        gsA = wmax(gs);
+    };
+
+    // ---- add the row multipliers (box [upper, lower] in that order, polytope at kp) and
+    //      return the stationarity norm ----
+    auto combine = [&]() __attribute__((always_inline)) -> double {
         double gpp[NV];
 #pragma unroll
-        for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const int r = lane + WAVE * q;
-            if (r < mp) {
-                const double ri = fdot(r, vp) + tp[q] - hpi[r];
-#pragma unroll
-                for (int c = 0; c < NV; ++c) gpp[c] += Fs[c * mpad + r] * lp[q];
-                fe = fmax(fe, fabs(ri));
-                cs += tp[q] * lp[q];
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < NV; ++c) gpp[c] = wsum(gpp[c]);
+        for (int c = 0; c < NV; ++c) gpp[c] = W[L.gpp + c];
+        double st = 0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k > N) continue;
+            double r[NS], ru[NU];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) r[i] = W[L.rs + k * NS + i];
+#pragma unroll
+            for (int i = 0; i < NU; ++i) ru[i] = W[L.ru + k * NU + i];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                r[i] += W[L.blam + (k * NB + i) * 2];
+                r[i] -= W[L.blam + (k * NB + i) * 2 + 1];
+            }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                ru[i] += W[L.blam + (k * NB + NX + i) * 2];
+                ru[i] -= W[L.blam + (k * NB + NX + i) * 2 + 1];
+            }
             if (k == kp) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) rsl[j][i] += gpp[i];
+                for (int i = 0; i < NS; ++i) r[i] += gpp[i];
                 if (kp < N) {
 #pragma unroll
-                    for (int i = 0; i < NU; ++i) rul[j][i] += gpp[NS + i];
+                    for (int i = 0; i < NU; ++i) ru[i] += gpp[NS + i];
                 }
             }
             if (k == 0) {
 #pragma unroll
-                for (int i = 0; i < NX; ++i) rsl[j][i] = 0.0;
+                for (int i = 0; i < NX; ++i) r[i] = 0.0;
             }
 #pragma unroll
-            for (int i = 0; i < NS; ++i) { st = fmax(st, fabs(rsl[j][i])); W[L.rs + k * NS + i] = rsl[j][i]; }
+            for (int i = 0; i < NS; ++i) { st = fmax(st, fabs(r[i])); W[L.rs + k * NS + i] = r[i]; }
 #pragma unroll
-            for (int i = 0; i < NU; ++i) { st = fmax(st, fabs(rul[j][i])); W[L.ru + k * NU + i] = rul[j][i]; }
+            for (int i = 0; i < NU; ++i) { st = fmax(st, fabs(ru[i])); W[L.ru + k * NU + i] = ru[i]; }
         }
-        stat = wmax(st);
-        feas = wmax(fe);
-        csum = wsum(cs);
-        gscale = wmax(gs);
+        wave_sync();
+        return wmax(st);
     };
 
     // ======================= Riccati factorisation =========================================
-    // Riccati-factor lane roles: lane (ib, jb) = (lane / NS, lane % NS), ib <= jb < NS, owns
-    // entry (ib, jb) of P_k.  Every lane forms the input-row quantities of ITS two columns
-    // itself (g = P_{k+1} Bbar, M_u(:, ib), M_u(:, jb), Rhat, K_ib, K_jb), so the only
-    // cross-lane traffic per stage is P_k itself, broadcast through the packed LDS table.
+    // lane (ib, jb) = (lane / NS, lane % NS), ib <= jb < NS, owns entry (ib, jb) of P_k.  Every
+    // lane forms the input-row quantities of ITS two columns itself (g = P_{k+1} Bbar,
+    // M_u(:, ib), M_u(:, jb), Rhat, K_ib, K_jb), so the only cross-lane traffic per stage is P_k
+    // itself, broadcast through the packed LDS table.
     const int ib = (lane < NS * NS) ? lane / NS : 0, jb = (lane < NS * NS) ? lane % NS : 0;
     const bool blane = lane < NS * NS && ib <= jb;
+    double Ai[NS], Aj[NS], Bl[NS][NU];
+#pragma unroll
+    for (int a_ = 0; a_ < NS; ++a_) {
+        Ai[a_] = Abar(a_, ib);
+        Aj[a_] = Abar(a_, jb);
+#pragma unroll
+        for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
+    }
+    constexpr int PST = pk_stride(NS);
     auto factor = [&]() __attribute__((always_inline)) -> bool {
-        // one reciprocal of t per row per iteration (reused by both solves and the steps)
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) { itx[j][i][0] = 1.0 / tx[j][i][0]; itx[j][i][1] = 1.0 / tx[j][i][1]; }
-#pragma unroll
-            for (int i = 0; i < NU; ++i) { itu[j][i][0] = 1.0 / tu[j][i][0]; itu[j][i][1] = 1.0 / tu[j][i][1]; }
-            const int k = lane + WAVE * j;
-            if (k <= N) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double d = 0;
-                    if (xpres(j, i, 0)) d += lx[j][i][0] * itx[j][i][0];
-                    if (xpres(j, i, 1)) d += lx[j][i][1] * itx[j][i][1];
-                    W[L.Dx + k * NV + i] = d;
-                }
-#pragma unroll
-                for (int i = 0; i < NU; ++i) {
-                    double d = 0;
-                    if (upres(j, i, 0)) d += lu[j][i][0] * itu[j][i][0];
-                    if (upres(j, i, 1)) d += lu[j][i][1] * itu[j][i][1];
-                    W[L.Dx + k * NV + NS + i] = d;
-                }
-#pragma unroll
-                for (int i = NX; i < NS; ++i) W[L.Dx + k * NV + i] = 0.0;
-            }
-        }
-        STAMP(1);
-        // polytope F'DF (upper triangle), reduced over the wave
-        double fd[NV * (NV + 1) / 2];
-#pragma unroll
-        for (int c = 0; c < NV * (NV + 1) / 2; ++c) fd[c] = 0.0;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            itp[q] = 1.0 / tp[q];
-            const int r = lane + WAVE * q;
-            if (r < mp) {
-                const double d = lp[q] * itp[q];
-                double f[NV];
-#pragma unroll
-                for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
-                int idx = 0;
-#pragma unroll
-                for (int i2 = 0; i2 < NV; ++i2) {
-                    const double di = d * f[i2];
-#pragma unroll
-                    for (int j2 = i2; j2 < NV; ++j2) fd[idx++] += di * f[j2];
-                }
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < NV * (NV + 1) / 2; ++c) fd[c] = wsum(fd[c]);
-        if (lane == 0) {
-            int idx = 0;
-#pragma unroll
-            for (int i2 = 0; i2 < NV; ++i2)
-#pragma unroll
-                for (int j2 = i2; j2 < NV; ++j2) {
-                    W[L.FD + i2 * NV + j2] = fd[idx];
-                    W[L.FD + j2 * NV + i2] = fd[idx];
-                    ++idx;
-                }
-        }
-        wave_sync();
-        // per-lane columns ib, jb of Abar and the (uniform) Bbar, constant over the stages
-        double Ai[NS], Aj[NS], Bl[NS][NU];
-#pragma unroll
-        for (int a_ = 0; a_ < NS; ++a_) {
-            Ai[a_] = Abar(a_, ib);
-            Aj[a_] = Abar(a_, jb);
-#pragma unroll
-            for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
-        }
-        // Htilde entry (i, j) of stage k
-        // (branch-free: every operand is loaded unconditionally and selected, so the loads of a
-        // stage issue back to back and are waited for once)
-        auto ht = [&](int k, int i, int j) __attribute__((always_inline)) -> double {
-            const double h = Hs[k * hstride + i * NV + j];
-            const double d = W[L.Dx + k * NV + i];
-            const double f = W[L.FD + i * NV + j];
-            return (h + (i == j ? d : 0.0)) + (k == kp ? f : 0.0);
-        };
-        // stage-k entries each lane needs, prefetched one stage ahead of the recursion as RAW
-        // operands (cost entry, box diagonal): they are combined only when the stage is
-        // processed, so the prefetch loads are not waited for inside the stage that issues them.
-        // The polytope term F'DF enters at stage kp only (a uniform branch).
+        // stage-k entries each lane needs, prefetched one stage ahead as RAW operands (cost
+        // entry, box diagonal) and combined only when the stage is processed; the polytope term
+        // F'DF enters at stage kp only (a uniform branch).  Operation order (H + D) + FD.
         struct StageH { double hij, dij, hui[NU], huj[NU], huu[NU][NU], duu[NU]; };
         auto load_h = [&](int k, StageH& sh) __attribute__((always_inline)) {
             const double* Hk = Hs + k * hstride;
@@ -573,7 +433,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 for (int y = 0; y < NU; ++y) sh.huu[x][y] = Hk[(NS + x) * NV + NS + y];
             }
         };
-        // Htilde entries of the stage (same operation order as ht())
         auto combine_h = [&](int k, const StageH& sh, StageH& o) __attribute__((always_inline)) {
             o.hij = sh.hij + (ib == jb ? sh.dij : 0.0);
 #pragma unroll
@@ -594,9 +453,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 }
             }
         };
-        // P_k broadcast: the owning lanes store the packed upper triangle, every lane reads the
-        // stage slot back (ds_read_b128, same address in all lanes)
-        constexpr int PST = pk_stride(NS);
         double pu[PST];
         auto bcast_p = [&](int k) __attribute__((always_inline)) {
             wave_sync();
@@ -609,9 +465,13 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             }
         };
         auto Pm = [&](int a_, int b_) __attribute__((always_inline)) -> double { return pu[pk_idx(NS, a_, b_)]; };
-        if (blane) W[L.P + N * PST + pk_idx(NS, ib, jb)] = ht(N, ib, jb);
+        {
+            StageH rN, cN;
+            load_h(N, rN);
+            combine_h(N, rN, cN);
+            if (blane) W[L.P + N * PST + pk_idx(NS, ib, jb)] = cN.hij;
+        }
         bcast_p(N);
-        STAMP(2);
         bool ok = true;
         StageH raw, nxt, cur;
         load_h(N - 1, raw);
@@ -693,15 +553,10 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int a_ = 0; a_ < NS; ++a_) acc += Phi_i[a_] * Tj[a_];
             v += acc;
-            // tables for the solves
             if (blane) W[L.P + k * PST + pk_idx(NS, ib, jb)] = v;
             if (lane < NS) {        // lane (0, jb): column jb of K
 #pragma unroll
                 for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + jb] = Kj[x];
-            }
-            if (kPhi && blane && ib == jb) {   // diagonal lane (ib, ib): column ib of Phi
-#pragma unroll
-                for (int a_ = 0; a_ < NS; ++a_) W[L.Phi + k * NS * NS + a_ * NS + ib] = Phi_i[a_];
             }
             if (lane == 0) {
 #pragma unroll
@@ -710,7 +565,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             bcast_p(k);
             raw = nxt;
         }
-        STAMP(3);
         // factor of the theta block of P_0 (np = 1: its reciprocal)
         double Pt[NP][NP], L0[NP][NP];
 #pragma unroll
@@ -733,16 +587,20 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         return ok;
     };
 
-    // complementarity right-hand side of a row: predictor t*lam, corrector + dt_a*dlam_a - sigma*mu
-    auto rcv = [&](double t, double l, double pr, bool corr, double smu) __attribute__((always_inline)) -> double {
-        return corr ? t * l + pr - smu : t * l;
-    };
-
     // ======================= Newton solve ==================================================
-    auto solve = [&](bool corr, double smu) __attribute__((always_inline)) {
-        STAMP(15);
-        // q = r_v + C'((lam o ri - rc)/t)
+    // right-hand side q = r_v + C'((lam o ri - rc)/t): the row wave supplies the box terms
+    // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
+    const int li = lane < NS ? lane : NS - 1;
+    double Acol[NS], Arow[NS], Bli[NU];     // Abar(:, li), Abar(li, :), Bbar(li, :) for the sweeps
+#pragma unroll
+    for (int c = 0; c < NS; ++c) { Acol[c] = Abar(c, li); Arow[c] = Abar(li, c); }
+#pragma unroll
+    for (int x = 0; x < NU; ++x) Bli[x] = Bbar(li, x);
+    auto solve = [&](int ods, int odu) __attribute__((always_inline)) {
         double qs[SPL][NS], qu[SPL][NU];
+        double gpe[NV];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gpe[c] = W[L.gpe + c];
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -750,54 +608,28 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int i = 0; i < NS; ++i) qs[j][i] = W[L.rs + kk * NS + i];
 #pragma unroll
-            for (int i = 0; i < NU; ++i) qu[j][i] = W[L.ru + kk * NU + i];
-#pragma unroll
             for (int i = 0; i < NX; ++i) {
                 double e = 0.0;
-                if (xpres(j, i, 0)) e += (lx[j][i][0] * rix(j, i, 0) - rcv(tx[j][i][0], lx[j][i][0], prx[j][i][0], corr, smu)) * itx[j][i][0];
-                if (xpres(j, i, 1)) e -= (lx[j][i][1] * rix(j, i, 1) - rcv(tx[j][i][1], lx[j][i][1], prx[j][i][1], corr, smu)) * itx[j][i][1];
+                e += W[L.ebox + (kk * NB + i) * 2];
+                e -= W[L.ebox + (kk * NB + i) * 2 + 1];
                 qs[j][i] += e;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                double e = qu[j][i];
-                if (upres(j, i, 0)) e += (lu[j][i][0] * riu(j, i, 0) - rcv(tu[j][i][0], lu[j][i][0], pru[j][i][0], corr, smu)) * itu[j][i][0];
-                if (upres(j, i, 1)) e -= (lu[j][i][1] * riu(j, i, 1) - rcv(tu[j][i][1], lu[j][i][1], pru[j][i][1], corr, smu)) * itu[j][i][1];
+                double e = W[L.ru + kk * NU + i];
+                e += W[L.ebox + (kk * NB + NX + i) * 2];
+                e -= W[L.ebox + (kk * NB + NX + i) * 2 + 1];
                 qu[j][i] = e;
             }
-        }
-        {
-            double vp[NV];
-            load_vp(vp, L.xs, L.xu);
-            double gpp[NV];
+            if (k == kp) {
 #pragma unroll
-            for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
+                for (int i = 0; i < NS; ++i) qs[j][i] += gpe[i];
+                if (kp < N) {
 #pragma unroll
-            for (int q = 0; q < RPL; ++q) {
-                const int r = lane + WAVE * q;
-                if (r < mp) {
-                    const double ri = fdot(r, vp) + tp[q] - hpi[r];
-                    const double pr = corr ? W[L.prp + r] : 0.0;
-                    const double e = (lp[q] * ri - rcv(tp[q], lp[q], pr, corr, smu)) * itp[q];
-#pragma unroll
-                    for (int c = 0; c < NV; ++c) gpp[c] += Fs[c * mpad + r] * e;
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < NV; ++c) gpp[c] = wsum(gpp[c]);
-#pragma unroll
-            for (int j = 0; j < SPL; ++j) {
-                if (lane + WAVE * j == kp) {
-#pragma unroll
-                    for (int i = 0; i < NS; ++i) qs[j][i] += gpp[i];
-                    if (kp < N) {
-#pragma unroll
-                        for (int i = 0; i < NU; ++i) qu[j][i] += gpp[NS + i];
-                    }
+                    for (int i = 0; i < NU; ++i) qu[j][i] += gpe[NS + i];
                 }
             }
         }
-        STAMP(4);
         // pre-pass: wv_k = P_{k+1} re_k, qt_k = qs_k + K_k' qu_k, qh_k = qt_k + Phi_k' wv_k ;
         // p_N = qs_N.  qh carries everything of the backward recursion that does not depend on
         // p_{k+1}, so the sequential sweep is one NS x NS mat-vec per stage.
@@ -805,11 +637,15 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
-                const double* Pn = W + L.P + (k + 1) * pk_stride(NS);
+                const double* Pn = W + L.P + (k + 1) * PST;
                 const double* Kk = W + L.K + k * NU * NS;
-                double rek[NS], wk[NS], qtk[NS];
+                double rek[NS], wk[NS], qtk[NS], Kl[NU][NS];
 #pragma unroll
                 for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
+#pragma unroll
+                for (int x = 0; x < NU; ++x)
+#pragma unroll
+                    for (int c = 0; c < NS; ++c) Kl[x][c] = Kk[x * NS + c];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     double v = 0.0;
@@ -819,36 +655,21 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                     W[L.wv + k * NS + i] = v;
                     double qq = qs[j][i];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) qq += Kk[x * NS + i] * qu[j][x];
+                    for (int x = 0; x < NU; ++x) qq += Kl[x][i] * qu[j][x];
                     qtk[i] = qq;
                 }
-                if constexpr (kPhi) {
-                    const double* Ph = W + L.Phi + k * NS * NS;
+                // Phi_k = Abar + Bbar K_k, column i formed as in the factorisation
 #pragma unroll
-                    for (int i = 0; i < NS; ++i) {
-                        double v = qtk[i];
+                for (int i = 0; i < NS; ++i) {
+                    double v = qtk[i];
 #pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Ph[c * NS + i] * wk[c];
-                        W[L.qt_xpi + k * NS + i] = v;
+                    for (int c = 0; c < NS; ++c) {
+                        double ph = Abar(c, i);
+#pragma unroll
+                        for (int x = 0; x < NU; ++x) ph += Bbar(c, x) * Kl[x][i];
+                        v += ph * wk[c];
                     }
-                } else {
-                    double bw[NU];
-#pragma unroll
-                    for (int x = 0; x < NU; ++x) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Bbar(c, x) * wk[c];
-                        bw[x] = v;
-                    }
-#pragma unroll
-                    for (int i = 0; i < NS; ++i) {
-                        double v = qtk[i];
-#pragma unroll
-                        for (int c = 0; c < NS; ++c) v += Abar(c, i) * wk[c];
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) v += Kk[x * NS + i] * bw[x];
-                        W[L.qt_xpi + k * NS + i] = v;
-                    }
+                    W[L.qt_xpi + k * NS + i] = v;
                 }
 #pragma unroll
                 for (int x = 0; x < NU; ++x) W[L.qu + k * NU + x] = qu[j][x];
@@ -858,51 +679,44 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             }
         }
         wave_sync();
-        STAMP(5);
         // backward sweep: lane i < NS computes entry i of p_k = Phi_k' p_{k+1} + qh_k; the new
-        // vector is broadcast with readlane (scalar registers), stage data prefetched a stage ahead
+        // vector is broadcast with readlane (scalar registers); two register sets used
+        // alternately (stages k, k-1), each refilled two stages ahead
         {
-            const int li = lane < NS ? lane : NS - 1;
             double p[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) p[i] = W[L.pv + N * NS + i];
-            auto load_b = [&](int k, double (&col)[NS], double& q) __attribute__((always_inline)) {
+            // Phi_k column li = Abar(:, li) + Bbar K_k(:, li)
+            auto load_b = [&](int k, double (&kc)[NU], double& q) __attribute__((always_inline)) {
                 q = W[L.qt_xpi + k * NS + li];
-                if constexpr (kPhi) {
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) col[c] = W[L.Phi + k * NS * NS + c * NS + li];
-                } else {
-#pragma unroll
-                    for (int c = 0; c < NS; ++c) {
-                        double v = Abar(c, li);
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) v += Bbar(c, x) * W[L.K + k * NU * NS + x * NS + li];
-                        col[c] = v;
-                    }
-                }
+                for (int x = 0; x < NU; ++x) kc[x] = W[L.K + k * NU * NS + x * NS + li];
             };
-            // two register sets used alternately (stages k, k-1), each refilled two stages ahead
-            double c0[NS], q0, c1[NS], q1;
-            load_b(N - 1, c0, q0);
-            if (N >= 2) load_b(N - 2, c1, q1);
-            auto step_b = [&](int k, const double (&col)[NS], double q) __attribute__((always_inline)) {
+            double k0[NU], q0, k1[NU], q1;
+            load_b(N - 1, k0, q0);
+            if (N >= 2) load_b(N - 2, k1, q1);
+            auto step_b = [&](int k, const double (&kc)[NU], double q) __attribute__((always_inline)) {
                 double acc = q;
 #pragma unroll
-                for (int c = 0; c < NS; ++c) acc += col[c] * p[c];
+                for (int c = 0; c < NS; ++c) {
+                    double ph = Acol[c];
+#pragma unroll
+                    for (int x = 0; x < NU; ++x) ph += Bl[c][x] * kc[x];
+                    acc += ph * p[c];
+                }
                 if (lane < NS) W[L.pv + k * NS + lane] = acc;
 #pragma unroll
                 for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
             };
             for (int k = N - 1; k >= 0; k -= 2) {
-                step_b(k, c0, q0);
-                if (k >= 2) load_b(k - 2, c0, q0);
+                step_b(k, k0, q0);
+                if (k >= 2) load_b(k - 2, k0, q0);
                 if (k == 0) break;
-                step_b(k - 1, c1, q1);
-                if (k >= 3) load_b(k - 3, c1, q1);
+                step_b(k - 1, k1, q1);
+                if (k >= 3) load_b(k - 3, k1, q1);
             }
         }
         wave_sync();
-        STAMP(6);
         // post-backward: kff_k = -Rhat^{-1}(qu_k + Bbar'(p_{k+1} + w_k)); f_k = Bbar kff_k + re_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -931,7 +745,6 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             }
         }
         wave_sync();
-        STAMP(7);
         // theta_0 step + forward sweep: lane i < NS computes entry i of ds_{k+1} = Phi_k ds_k + f_k
         {
             double d[NS];
@@ -945,45 +758,41 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int x = 0; x < NP; ++x) d[NX + x] = r0[x];
             if (lane == 0) {
 #pragma unroll
-                for (int i = 0; i < NS; ++i) W[L.dsv + i] = d[i];
+                for (int i = 0; i < NS; ++i) W[ods + i] = d[i];
             }
-            const int li = lane < NS ? lane : NS - 1;
-            auto load_f = [&](int k, double (&row)[NS], double& f) __attribute__((always_inline)) {
+            // Phi_k row li = Abar(li, :) + Bbar(li, :) K_k
+            auto load_f = [&](int k, double (&kr)[NU][NS], double& f) __attribute__((always_inline)) {
                 f = W[L.fv + k * NS + li];
-                if constexpr (kPhi) {
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) row[c] = W[L.Phi + k * NS * NS + li * NS + c];
-                } else {
+                for (int x = 0; x < NU; ++x)
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) {
-                        double v = Abar(li, c);
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) v += Bbar(li, x) * W[L.K + k * NU * NS + x * NS + c];
-                        row[c] = v;
-                    }
-                }
+                    for (int c = 0; c < NS; ++c) kr[x][c] = W[L.K + k * NU * NS + x * NS + c];
             };
-            double r0_[NS], f0, r1_[NS], f1;
-            load_f(0, r0_, f0);
-            if (N >= 2) load_f(1, r1_, f1);
-            auto step_f = [&](int k, const double (&row)[NS], double f) __attribute__((always_inline)) {
+            double k0[NU][NS], f0, k1[NU][NS], f1;
+            load_f(0, k0, f0);
+            if (N >= 2) load_f(1, k1, f1);
+            auto step_f = [&](int k, const double (&kr)[NU][NS], double f) __attribute__((always_inline)) {
                 double acc = f;
 #pragma unroll
-                for (int c = 0; c < NS; ++c) acc += row[c] * d[c];
-                if (lane < NS) W[L.dsv + (k + 1) * NS + lane] = acc;
+                for (int c = 0; c < NS; ++c) {
+                    double ph = Arow[c];
+#pragma unroll
+                    for (int x = 0; x < NU; ++x) ph += Bli[x] * kr[x][c];
+                    acc += ph * d[c];
+                }
+                if (lane < NS) W[ods + (k + 1) * NS + lane] = acc;
 #pragma unroll
                 for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
             };
             for (int k = 0; k < N; k += 2) {
-                step_f(k, r0_, f0);
-                if (k + 2 < N) load_f(k + 2, r0_, f0);
+                step_f(k, k0, f0);
+                if (k + 2 < N) load_f(k + 2, k0, f0);
                 if (k + 1 >= N) break;
-                step_f(k + 1, r1_, f1);
-                if (k + 3 < N) load_f(k + 3, r1_, f1);
+                step_f(k + 1, k1, f1);
+                if (k + 3 < N) load_f(k + 3, k1, f1);
             }
         }
         wave_sync();
-        STAMP(8);
         // post-forward: du_k = K_k ds_k + kff_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -994,112 +803,28 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
                 for (int x = 0; x < NU; ++x) {
                     double v = kff[j][x];
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * W[L.dsv + k * NS + c];
-                    W[L.duv + k * NU + x] = v;
+                    for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * W[ods + k * NS + c];
+                    W[odu + k * NU + x] = v;
                 }
             } else if (k == N) {
 #pragma unroll
-                for (int x = 0; x < NU; ++x) W[L.duv + N * NU + x] = 0.0;
+                for (int x = 0; x < NU; ++x) W[odu + N * NU + x] = 0.0;
             }
         }
         wave_sync();
     };
 
-    // ======================= row passes over the step (dt, dlam recomputed) ================
-    // mode 0: max ratio (returns max of -dt/t, -dlam/lam); mode 1: comp sum after alpha and
-    // store predictor products; mode 2: apply the step alpha to t, lam.
-    auto row_pass = [&](int mode, bool corr, double smu, double al) __attribute__((always_inline)) -> double {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k > N) continue;
-            double dsk[NS], duk[NU];
-#pragma unroll
-            for (int i = 0; i < NS; ++i) dsk[i] = W[L.dsv + k * NS + i];
-#pragma unroll
-            for (int i = 0; i < NU; ++i) duk[i] = W[L.duv + k * NU + i];
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (!xpres(j, i, h)) continue;
-                    const double rc = rcv(tx[j][i][h], lx[j][i][h], prx[j][i][h], corr, smu);
-                    const double dt = -rix(j, i, h) - (h == 0 ? dsk[i] : -dsk[i]);
-                    const double dl = (-rc - lx[j][i][h] * dt) * itx[j][i][h];
-                    if (mode == 0) {
-                        acc = fmax(acc, -dt * itx[j][i][h]);
-                        acc = fmax(acc, -dl / lx[j][i][h]);
-                    } else if (mode == 1) {
-                        acc += (tx[j][i][h] + al * dt) * (lx[j][i][h] + al * dl);
-                        prx[j][i][h] = dt * dl;
-                    } else {
-                        tx[j][i][h] += al * dt;
-                        lx[j][i][h] += al * dl;
-                    }
-                }
-#pragma unroll
-            for (int i = 0; i < NU; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (!upres(j, i, h)) continue;
-                    const double rc = rcv(tu[j][i][h], lu[j][i][h], pru[j][i][h], corr, smu);
-                    const double dt = -riu(j, i, h) - (h == 0 ? duk[i] : -duk[i]);
-                    const double dl = (-rc - lu[j][i][h] * dt) * itu[j][i][h];
-                    if (mode == 0) {
-                        acc = fmax(acc, -dt * itu[j][i][h]);
-                        acc = fmax(acc, -dl / lu[j][i][h]);
-                    } else if (mode == 1) {
-                        acc += (tu[j][i][h] + al * dt) * (lu[j][i][h] + al * dl);
-                        pru[j][i][h] = dt * dl;
-                    } else {
-                        tu[j][i][h] += al * dt;
-                        lu[j][i][h] += al * dl;
-                    }
-                }
-        }
-        double vp[NV], dvp[NV];
-        load_vp(vp, L.xs, L.xu);
-        load_vp(dvp, L.dsv, L.duv);
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const int r = lane + WAVE * q;
-            if (r >= mp) continue;
-            const double ri = fdot(r, vp) + tp[q] - hpi[r];
-            const double pr = corr ? W[L.prp + r] : 0.0;
-            const double rc = rcv(tp[q], lp[q], pr, corr, smu);
-            const double dt = -ri - fdot(r, dvp);
-            const double dl = (-rc - lp[q] * dt) * itp[q];
-            if (mode == 0) {
-                acc = fmax(acc, -dt * itp[q]);
-                acc = fmax(acc, -dl / lp[q]);
-            } else if (mode == 1) {
-                acc += (tp[q] + al * dt) * (lp[q] + al * dl);
-                W[L.prp + r] = dt * dl;
-            } else {
-                tp[q] += al * dt;
-                lp[q] += al * dl;
-            }
-        }
-        if (mode == 0) return wmax(acc);
-        if (mode == 1) return wsum(acc);
-        return 0.0;
-    };
-    auto step_len = [&](bool corr, double smu) __attribute__((always_inline)) -> double {
-        const double rm = row_pass(0, corr, smu, 0.0);
-        return rm > 1.0 ? 1.0 / rm : 1.0;
-    };
-    // primal/dual stage update by alpha (dpi_k = P_k ds_k + p_k)
-    auto update_stage = [&](double al) __attribute__((always_inline)) {
+    // primal/dual stage update by alpha along (ids, idu); dpi_k = P_k ds_k + p_k
+    auto update_stage = [&](double al, int ids, int idu) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k > N) continue;
             double dsk[NS];
 #pragma unroll
-            for (int i = 0; i < NS; ++i) dsk[i] = W[L.dsv + k * NS + i];
+            for (int i = 0; i < NS; ++i) dsk[i] = W[ids + k * NS + i];
             if (k >= 1) {
-                const double* Pk = W + L.P + k * pk_stride(NS);
+                const double* Pk = W + L.P + k * PST;
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     double v = W[L.pv + k * NS + i];
@@ -1112,121 +837,77 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
             for (int i = 0; i < NS; ++i) s[j][i] += al * dsk[i];
             if (k < N) {
 #pragma unroll
-                for (int i = 0; i < NU; ++i) u[j][i] += al * W[L.duv + k * NU + i];
+                for (int i = 0; i < NU; ++i) u[j][i] += al * W[idu + k * NU + i];
             }
         }
     };
 
     // ======================= initial point ==================================================
-#pragma unroll
-    for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-        for (int i = 0; i < NX; ++i)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) { tx[j][i][h] = 1.0; lx[j][i][h] = 1.0; prx[j][i][h] = 0.0; }
-#pragma unroll
-        for (int i = 0; i < NU; ++i)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) { tu[j][i][h] = 1.0; lu[j][i][h] = 1.0; pru[j][i][h] = 0.0; }
-    }
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; }
-    double stat = 0, feas = 0, csum = 0, gscale = 0;
-    residuals(stat, feas, csum, gscale);
+    double feasA = 0, gsA = 0;
+    write_state();
+    stage_partials(feasA, gsA);
+    BARRIER();                                            // I0: row-side tables of t = lam = 1
+    const double minv = 1.0 / fmax(X[X_CNT], 1.0);
+    const double bscale = fmax(x0max, X[X_BSR]);
+    combine();
     int flag = 0;
     if (!factor()) flag = -8;
-    solve(false, 0.0);
-    {
-        // tt = t + dt (t = 1) at the unit-scaled least-squares point; lam~ = -tt; shift
-        double tmin = INFINITY, tmax = -INFINITY;
-        row_pass(2, false, 0.0, 1.0);      // t <- 1 + dt (lam is reset below)
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (xpres(j, i, h)) { tmin = fmin(tmin, tx[j][i][h]); tmax = fmax(tmax, tx[j][i][h]); }
-#pragma unroll
-            for (int i = 0; i < NU; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (upres(j, i, h)) { tmin = fmin(tmin, tu[j][i][h]); tmax = fmax(tmax, tu[j][i][h]); }
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q)
-            if (prow(q)) { tmin = fmin(tmin, tp[q]); tmax = fmax(tmax, tp[q]); }
-        update_stage(1.0);
-        tmin = wmin(tmin);
-        tmax = wmax(tmax);
-        const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
-        const double shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
-#pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const double t = tx[j][i][h];
-                    const bool pr = xpres(j, i, h);
-                    tx[j][i][h] = pr ? t + shp : 1.0;
-                    lx[j][i][h] = pr ? -t + shd : 0.0;
-                }
-#pragma unroll
-            for (int i = 0; i < NU; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const double t = tu[j][i][h];
-                    const bool pr = upres(j, i, h);
-                    tu[j][i][h] = pr ? t + shp : 1.0;
-                    lu[j][i][h] = pr ? -t + shd : 0.0;
-                }
-        }
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const double t = tp[q];
-            const bool pr = prow(q);
-            tp[q] = pr ? t + shp : 1.0;
-            lp[q] = pr ? -t + shd : 0.0;
-        }
-    }
+    BARRIER();                                            // I1: predictor rhs of the start
+    solve(L.dsv, L.duv);
+    update_stage(1.0, L.dsv, L.duv);
+    BARRIER();                                            // I2: row wave takes dt (old iterate), shifts
+    BARRIER();                                            // I3: row wave done with the old iterate
+    write_state();
+    stage_partials(feasA, gsA);
 
     // ======================= main loop ======================================================
     int it = 0;
-    double mu = 0.0, mu_min = INFINITY;
+    double mu = 0.0, mu_min = INFINITY, stat = 0.0, feas = 0.0;
     const int max_iter = a.max_iter;
-    if (flag == 0) {
-        for (it = 0; it <= max_iter; ++it) {
-            STAMP(14);
-            residuals(stat, feas, csum, gscale);
-            STAMP(0);
-            mu = csum * minv;
-            if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
-                mu <= a.tol_comp) { flag = 1; break; }
-            if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
-            if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) { flag = -2; break; }
+    for (it = 0;; ++it) {
+        BARRIER();                                        // B0: row multipliers / D / F'DF ready
+        STAMP(0);
+        stat = combine();
+        STAMP(1);
+        BARRIER();                                        // B1: row residual norm, comp sum
+        STAMP(2);
+        feas = fmax(feasA, X[X_FEASB]);
+        mu = X[X_CS] * minv;
+        bool stop = false;
+        if (flag != 0) {
+            stop = true;
+        } else if (stat <= a.tol_stat * (1.0 + gsA) && feas <= a.tol_feas * (1.0 + bscale) &&
+                   mu <= a.tol_comp) {
+            flag = 1; stop = true;
+        } else if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) {
+            flag = -8; stop = true;
+        } else if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) {
+            flag = -2; stop = true;
+        } else {
             mu_min = fmin(mu_min, mu);
-            if (it == max_iter) break;
-            if (!factor()) { flag = -8; break; }
-            solve(false, 0.0);                                  // predictor
-            STAMP(9);
-            const double al_aff = step_len(false, 0.0);
-            STAMP(10);
-            const double mua = row_pass(1, false, 0.0, al_aff) * minv;
-            STAMP(11);
-            double sg = mua / mu;
-            sg = sg * sg * sg;
-            const double smu = sg * mu;
-            solve(true, smu);                                   // corrector
-            STAMP(9);
-            double al = step_len(true, smu) * a.tau;
-            STAMP(10);
-            if (al > 1.0) al = 1.0;
-            row_pass(2, true, smu, al);
-            STAMP(12);
-            update_stage(al);
-            STAMP(13);
+            if (it == max_iter) stop = true;
         }
+        if (!stop && !factor()) { flag = -8; stop = true; }
+        STAMP(3);
+        if (lane == 0) X[X_STOP] = stop ? 1.0 : 0.0;
+        BARRIER();                                        // B2: predictor rhs ready; stop flag
+        STAMP(4);
+        if (stop) break;
+        solve(L.dsv, L.duv);                              // predictor
+        STAMP(5);
+        BARRIER();                                        // B3: predictor direction out
+        BARRIER();                                        // B4: corrector rhs ready
+        STAMP(6);
+        solve(L.dsc, L.duc);                              // corrector
+        STAMP(7);
+        BARRIER();                                        // B5: corrector direction out
+        BARRIER();                                        // B6: step length ready
+        STAMP(8);
+        const double al = X[X_ALPHA];
+        update_stage(al, L.dsc, L.duc);
+        write_state();
+        stage_partials(feasA, gsA);
+        STAMP(9);
     }
 
     // ======================= outputs =======================================================
@@ -1265,37 +946,9 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) po[i] = pi[j][i];
         }
-        if (a.lamx_out) {
-            double* lo = a.lamx_out + ((int64_t)inst * (N + 1) + k) * NX * 2;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                lo[i] = xpres(j, i, 1) ? lx[j][i][1] : 0.0;        // lower
-                lo[NX + i] = xpres(j, i, 0) ? lx[j][i][0] : 0.0;   // upper
-            }
-        }
-        if (a.lamu_out && k < N) {
-            double* lo = a.lamu_out + ((int64_t)inst * N + k) * NU * 2;
-#pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                lo[i] = upres(j, i, 1) ? lu[j][i][1] : 0.0;
-                lo[NU + i] = upres(j, i, 0) ? lu[j][i][0] : 0.0;
-            }
-        }
-    }
-    if (a.lamp_out) {
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const int r = lane + WAVE * q;
-            if (r < mp) a.lamp_out[(int64_t)inst * mp + r] = lp[q];
-        }
     }
     fv = wsum(fv);
-#ifdef BQP_STAMPS
-    if (lane == 0 && a.stamps) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) a.stamps[(int64_t)inst * 16 + i] = (double)st_acc[i];
-    }
-#endif
+    STAMP_STORE(0);
     if (lane == 0) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
@@ -1306,11 +959,468 @@ __global__ void __launch_bounds__(256) ocp_ipm_kernel(OcpKernelArgs a) {
     }
 }
 
+// ==========================================================================================
+// row wave
+// ==========================================================================================
+template <int NX, int NU, int NP, int SPL, int RPL>
+__device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, const QpLds& L,
+                                         const double* Fs, int lane, int inst) {
+    constexpr int NS = NX + NP;
+    constexpr int NV = NS + NU;
+    constexpr int NB = NX + NU;          // box slots per stage: x then u, each [upper, lower]
+    const int N = a.N, mp = a.mp, kp = a.kp;
+    constexpr int mpad = RPL * WAVE;     // polytope table stride (host sets a.mpad to the same)
+    double* X = W + L.xch;
+    STAMP_DECL;
+
+    // ---------------- box rows of stage k = lane + 64 j: bounds to LDS, presence mask -------
+    unsigned msk[SPL];
+    double bsl = 0.0, mcount = 0.0;
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+        const int k = lane + WAVE * j;
+        const bool act = k <= N;
+        msk[j] = 0;
+#pragma unroll
+        for (int sl = 0; sl < NB; ++sl) {
+            double ub = INFINITY, lb = -INFINITY;
+            if (sl < NX) {
+                if (act && k > 0) {
+                    if (a.xub) ub = a.xub[(int64_t)inst * a.sxb + (int64_t)k * NX + sl];
+                    if (a.xlb) lb = a.xlb[(int64_t)inst * a.sxb + (int64_t)k * NX + sl];
+                }
+            } else {
+                if (act && k < N) {
+                    if (a.uub) ub = a.uub[(int64_t)inst * a.sub + (int64_t)k * NU + (sl - NX)];
+                    if (a.ulb) lb = a.ulb[(int64_t)inst * a.sub + (int64_t)k * NU + (sl - NX)];
+                }
+            }
+            if (isfinite(ub)) { msk[j] |= 1u << (2 * sl); bsl = fmax(bsl, fabs(ub)); }
+            if (isfinite(lb)) { msk[j] |= 2u << (2 * sl); bsl = fmax(bsl, fabs(lb)); }
+            if (act) {
+                W[L.bnd + (k * NB + sl) * 2] = ub;
+                W[L.bnd + (k * NB + sl) * 2 + 1] = lb;
+            }
+        }
+        mcount += __builtin_popcount(msk[j]);
+    }
+    auto pres = [&](int j, int sl, int h) __attribute__((always_inline)) -> bool { return (msk[j] >> (2 * sl + h)) & 1u; };
+    // polytope rows l, l+64, ...
+    double* hpi = W + L.hp;
+    {
+        const double* hg = a.hp + (int64_t)inst * a.shp;
+        for (int r = lane; r < mp; r += WAVE) hpi[r] = hg[r];
+    }
+    wave_sync();
+    auto prow = [&](int q) __attribute__((always_inline)) -> bool { return lane + WAVE * q < mp; };
+#pragma unroll
+    for (int q = 0; q < RPL; ++q)
+        if (prow(q)) { mcount += 1.0; bsl = fmax(bsl, fabs(hpi[lane + WAVE * q])); }
+    mcount = wsum(mcount);
+    bsl = wmax(bsl);
+    if (lane == 0) { X[X_CNT] = mcount; X[X_BSR] = bsl; }
+    const double minv = 1.0 / fmax(mcount, 1.0);
+    auto fdot = [&](int r, const double (&v)[NV]) __attribute__((always_inline)) -> double {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) acc += Fs[c * mpad + r] * v[c];
+        return acc;
+    };
+    auto load_v = [&](double (&v)[NV], int bs, int bu) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < NS; ++c) v[c] = W[bs + kp * NS + c];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) v[NS + c] = (kp < N) ? W[bu + kp * NU + c] : 0.0;
+    };
+
+    // row state: slack t, multiplier lam, 1/t; polytope rows also their residual ri (box-row
+    // residuals are re-formed from the LDS stage vector and bounds when needed)
+    double tx[SPL][NB][2], lx[SPL][NB][2], itx[SPL][NB][2];
+    double tp[RPL], lp[RPL], itp[RPL], rp[RPL];
+#pragma unroll
+    for (int j = 0; j < SPL; ++j)
+#pragma unroll
+        for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) { tx[j][sl][h] = 1.0; lx[j][sl][h] = 1.0; }
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; rp[q] = 0.0; }
+
+    // ---- multiplier-side tables (depend on t, lam only): box multipliers, Fp'lam, 1/t,
+    //      D = lam/t per stage, F'DF, sum t.lam ----
+    auto lam_side = [&]() __attribute__((always_inline)) {
+        double cs = 0.0;
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) itx[j][sl][h] = 1.0 / tx[j][sl][h];
+            if (k <= N) {
+#pragma unroll
+                for (int sl = 0; sl < NB; ++sl) {
+                    W[L.blam + (k * NB + sl) * 2] = pres(j, sl, 0) ? lx[j][sl][0] : 0.0;
+                    W[L.blam + (k * NB + sl) * 2 + 1] = pres(j, sl, 1) ? lx[j][sl][1] : 0.0;
+                    double d = 0;
+                    if (pres(j, sl, 0)) d += lx[j][sl][0] * itx[j][sl][0];
+                    if (pres(j, sl, 1)) d += lx[j][sl][1] * itx[j][sl][1];
+                    W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
+                    if (pres(j, sl, 0)) cs += tx[j][sl][0] * lx[j][sl][0];
+                    if (pres(j, sl, 1)) cs += tx[j][sl][1] * lx[j][sl][1];
+                }
+#pragma unroll
+                for (int i = NX; i < NS; ++i) W[L.Dx + k * NV + i] = 0.0;
+            }
+        }
+        double gpp[NV];
+        double fd[NV * (NV + 1) / 2];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV * (NV + 1) / 2; ++c) fd[c] = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            ROW_FENCE(q);
+            itp[q] = 1.0 / tp[q];
+            const int r = lane + WAVE * q;
+            if (r < mp) {
+                double f[NV];
+#pragma unroll
+                for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
+#pragma unroll
+                for (int c = 0; c < NV; ++c) gpp[c] += f[c] * lp[q];
+                cs += tp[q] * lp[q];
+                const double d = lp[q] * itp[q];
+                int idx = 0;
+#pragma unroll
+                for (int i2 = 0; i2 < NV; ++i2) {
+                    const double di = d * f[i2];
+#pragma unroll
+                    for (int j2 = i2; j2 < NV; ++j2) fd[idx++] += di * f[j2];
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gpp[c] = wsum(gpp[c]);
+#pragma unroll
+        for (int c = 0; c < NV * (NV + 1) / 2; ++c) fd[c] = wsum(fd[c]);
+        cs = wsum(cs);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NV; ++c) W[L.gpp + c] = gpp[c];
+            int idx = 0;
+#pragma unroll
+            for (int i2 = 0; i2 < NV; ++i2)
+#pragma unroll
+                for (int j2 = i2; j2 < NV; ++j2) {
+                    W[L.FD + i2 * NV + j2] = fd[idx];
+                    W[L.FD + j2 * NV + i2] = fd[idx];
+                    ++idx;
+                }
+            X[X_CS] = cs;
+        }
+    };
+
+    // box-row residual of the current iterate: v + t - ub (upper), -v + t + lb (lower); the
+    // stage vector in LDS is the iterate's until the stage wave writes the next one (after B6)
+    auto box_res = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> double {
+        const double v = sl < NX ? W[L.xs + k * NS + sl] : W[L.xu + k * NU + (sl - NX)];
+        const double b = W[L.bnd + (k * NB + sl) * 2 + h];
+        return h == 0 ? v + tx[j][sl][0] - b : -v + tx[j][sl][1] + b;
+    };
+    // ---- row residuals of the current iterate (box: +-v + t -+ b; polytope: Fp v + t - hp) ----
+    auto row_residuals = [&]() __attribute__((always_inline)) {
+        double fe = 0.0;
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (pres(j, sl, h)) fe = fmax(fe, fabs(box_res(j, k, sl, h)));
+        }
+        double vp[NV];
+        load_v(vp, L.xs, L.xu);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            ROW_FENCE(q);
+            const int r = lane + WAVE * q;
+            if (r < mp) {
+                const double ri = fdot(r, vp) + tp[q] - hpi[r];
+                rp[q] = ri;
+                fe = fmax(fe, fabs(ri));
+            }
+        }
+        fe = wmax(fe);
+        if (lane == 0) X[X_FEASB] = fe;
+    };
+
+    // complementarity right-hand side of a row: predictor t*lam, corrector + dt_a*dlam_a - sigma*mu
+    auto rcv = [&](double t, double l, double pr, bool corr, double smu) __attribute__((always_inline)) -> double {
+        return corr ? t * l + pr - smu : t * l;
+    };
+    // box-row step dt = -ri - (+-dv) along the direction (ids, idu)
+    auto box_dir = [&](int j, int k, int sl, int h, int ids, int idu) __attribute__((always_inline)) -> double {
+        const double dv = sl < NX ? W[ids + k * NS + sl] : W[idu + k * NU + (sl - NX)];
+        return -box_res(j, k, sl, h) - (h == 0 ? dv : -dv);
+    };
+    // box-row predictor product dt_a * dlam_a (recomputed from the predictor direction)
+    auto box_pred_prod = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> double {
+        const double dt = box_dir(j, k, sl, h, L.dsv, L.duv);
+        const double dl = (-(tx[j][sl][h] * lx[j][sl][h]) - lx[j][sl][h] * dt) * itx[j][sl][h];
+        return dt * dl;
+    };
+
+    // ---- right-hand-side terms (lam o ri - rc)/t: box [upper, lower] per stage, Fp'e ----
+    auto rhs_terms = [&](bool corr, double smu) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    double e = 0.0;
+                    if (pres(j, sl, h)) {
+                        const double pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
+                        e = (lx[j][sl][h] * box_res(j, k, sl, h) - rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu)) * itx[j][sl][h];
+                    }
+                    W[L.ebox + (k * NB + sl) * 2 + h] = e;
+                }
+        }
+        double gpe[NV];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gpe[c] = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            ROW_FENCE(q);
+            const int r = lane + WAVE * q;
+            if (r < mp) {
+                const double pr = corr ? W[L.prp + r] : 0.0;
+                const double e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * itp[q];
+#pragma unroll
+                for (int c = 0; c < NV; ++c) gpe[c] += Fs[c * mpad + r] * e;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gpe[c] = wsum(gpe[c]);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NV; ++c) W[L.gpe + c] = gpe[c];
+        }
+    };
+
+    // ---- row passes along the direction (ids, idu): dt = -ri - C dv, dlam = (-rc - lam dt)/t.
+    //      mode 0: ratio max(-dt/t, -dlam/lam); 1: sum (t+al dt)(lam+al dlam) and store the
+    //      polytope predictor products; 2: apply t += al dt, lam += al dlam ----
+    auto row_pass = [&](int mode, bool corr, double smu, double al, int ids, int idu) __attribute__((always_inline)) -> double {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (!pres(j, sl, h)) continue;
+                    const double pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
+                    const double rc = rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu);
+                    const double dt = box_dir(j, k, sl, h, ids, idu);
+                    const double dl = (-rc - lx[j][sl][h] * dt) * itx[j][sl][h];
+                    if (mode == 0) {
+                        acc = fmax(acc, -dt * itx[j][sl][h]);
+                        acc = fmax(acc, -dl / lx[j][sl][h]);
+                    } else if (mode == 1) {
+                        acc += (tx[j][sl][h] + al * dt) * (lx[j][sl][h] + al * dl);
+                    } else {
+                        tx[j][sl][h] += al * dt;
+                        lx[j][sl][h] += al * dl;
+                    }
+                }
+        }
+        double dvp[NV];
+        load_v(dvp, ids, idu);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            ROW_FENCE(q);
+            const int r = lane + WAVE * q;
+            if (r >= mp) continue;
+            const double pr = corr ? W[L.prp + r] : 0.0;
+            const double rc = rcv(tp[q], lp[q], pr, corr, smu);
+            const double dt = -rp[q] - fdot(r, dvp);
+            const double dl = (-rc - lp[q] * dt) * itp[q];
+            if (mode == 0) {
+                acc = fmax(acc, -dt * itp[q]);
+                acc = fmax(acc, -dl / lp[q]);
+            } else if (mode == 1) {
+                acc += (tp[q] + al * dt) * (lp[q] + al * dl);
+                W[L.prp + r] = dt * dl;
+            } else {
+                tp[q] += al * dt;
+                lp[q] += al * dl;
+            }
+        }
+        if (mode == 0) return wmax(acc);
+        if (mode == 1) return wsum(acc);
+        return 0.0;
+    };
+
+    // ======================= initial point ==================================================
+    lam_side();
+    BARRIER();                                            // I0
+    row_residuals();
+    rhs_terms(false, 0.0);
+    BARRIER();                                            // I1
+    BARRIER();                                            // I2: start direction in (dsv, duv)
+    {
+        // t~ = t + dt (t = 1) at the unit-scaled least-squares point; lam~ = -t~; shift
+        row_pass(2, false, 0.0, 1.0, L.dsv, L.duv);
+        double tmin = INFINITY, tmax = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < SPL; ++j)
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (pres(j, sl, h)) { tmin = fmin(tmin, tx[j][sl][h]); tmax = fmax(tmax, tx[j][sl][h]); }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if (prow(q)) { tmin = fmin(tmin, tp[q]); tmax = fmax(tmax, tp[q]); }
+        tmin = wmin(tmin);
+        tmax = wmax(tmax);
+        const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
+        const double shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
+#pragma unroll
+        for (int j = 0; j < SPL; ++j)
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const double t = tx[j][sl][h];
+                    const bool pr = pres(j, sl, h);
+                    tx[j][sl][h] = pr ? t + shp : 1.0;
+                    lx[j][sl][h] = pr ? -t + shd : 0.0;
+                }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const double t = tp[q];
+            const bool pr = prow(q);
+            tp[q] = pr ? t + shp : 1.0;
+            lp[q] = pr ? -t + shd : 0.0;
+        }
+    }
+    lam_side();
+    BARRIER();                                            // I3
+
+    // ======================= main loop ======================================================
+    for (;;) {
+        BARRIER();                                        // B0
+        STAMP(0);
+        row_residuals();
+        STAMP(1);
+        BARRIER();                                        // B1
+        rhs_terms(false, 0.0);
+        STAMP(2);
+        BARRIER();                                        // B2
+        STAMP(3);
+        if (X[X_STOP] != 0.0) break;
+        BARRIER();                                        // B3: predictor direction in (dsv, duv)
+        STAMP(4);
+        const double mu = X[X_CS] * minv;
+        const double rm_a = row_pass(0, false, 0.0, 0.0, L.dsv, L.duv);
+        const double al_aff = rm_a > 1.0 ? 1.0 / rm_a : 1.0;
+        const double mua = row_pass(1, false, 0.0, al_aff, L.dsv, L.duv) * minv;
+        double sg = mua / mu;
+        sg = sg * sg * sg;
+        const double smu = sg * mu;
+        rhs_terms(true, smu);
+        STAMP(5);
+        BARRIER();                                        // B4
+        BARRIER();                                        // B5: corrector direction in (dsc, duc)
+        STAMP(6);
+        const double rm = row_pass(0, true, smu, 0.0, L.dsc, L.duc);
+        double al = (rm > 1.0 ? 1.0 / rm : 1.0) * a.tau;
+        if (al > 1.0) al = 1.0;
+        if (lane == 0) X[X_ALPHA] = al;
+        row_pass(2, true, smu, al, L.dsc, L.duc);
+        STAMP(7);
+        BARRIER();                                        // B6
+        lam_side();
+        STAMP(8);
+    }
+
+    // ======================= outputs (multipliers) ==========================================
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+        const int k = lane + WAVE * j;
+        if (k > N) continue;
+        if (a.lamx_out) {
+            double* lo = a.lamx_out + ((int64_t)inst * (N + 1) + k) * NX * 2;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                lo[i] = pres(j, i, 1) ? lx[j][i][1] : 0.0;        // lower
+                lo[NX + i] = pres(j, i, 0) ? lx[j][i][0] : 0.0;   // upper
+            }
+        }
+        if (a.lamu_out && k < N) {
+            double* lo = a.lamu_out + ((int64_t)inst * N + k) * NU * 2;
+#pragma unroll
+            for (int i = 0; i < NU; ++i) {
+                lo[i] = pres(j, NX + i, 1) ? lx[j][NX + i][1] : 0.0;
+                lo[NU + i] = pres(j, NX + i, 0) ? lx[j][NX + i][0] : 0.0;
+            }
+        }
+    }
+    if (a.lamp_out) {
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            if (r < mp) a.lamp_out[(int64_t)inst * mp + r] = lp[q];
+        }
+    }
+    STAMP_STORE(16);
+}
+
+// ==========================================================================================
+// kernel: QPB instances per workgroup, waves [0, QPB) stage waves, [QPB, 2 QPB) row waves
+// ==========================================================================================
+template <int NX, int NU, int NP, int SPL, int RPL>
+__global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
+    constexpr int NS = NX + NP;
+    constexpr int NV = NS + NU;
+    extern __shared__ double lds[];
+    const int N = a.N;
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int qpb = a.wpb;
+    // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
+    double* Hs = lds;
+    double* Fs = lds + (N + 1) * a.hstride;
+    for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
+    for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
+    __syncthreads();
+    const bool rowwave = wid >= qpb;
+    const int slot = rowwave ? wid - qpb : wid;
+    const int inst = blockIdx.x * qpb + slot;
+    if (inst >= a.batch) return;       // both waves of an empty slot leave together
+    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad);
+    double* W = lds + a.shared_doubles + slot * L.total;
+    if (!rowwave)
+        stage_wave<NX, NU, NP, SPL>(a, W, L, Hs, lane, inst);
+    else
+        row_wave<NX, NU, NP, SPL, RPL>(a, W, L, Fs, lane, inst);
+}
+
 // ------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------------
 int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad) {
-    return WaveLds::make(N, nx, nu, np, mpad, N + 1 <= 64).total;
+    return QpLds::make(N, nx, nu, np, mpad).total;
 }
 
 template <int NX, int NU, int NP, int SPL, int RPL>
@@ -1320,7 +1430,7 @@ static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipSt
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * a.wpb), lds, st, a);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(128 * a.wpb), lds, st, a);
     return hipGetLastError();
 }
 
@@ -1367,8 +1477,8 @@ hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_
 #else
     if (nx == 4 && nu == 1 && np == 1) return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);
     if (nx == 2 && nu == 2 && np == 2) return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st);
-#endif
     return hipErrorInvalidValue;
+#endif
 }
 
 }  // namespace bqp

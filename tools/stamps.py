@@ -21,14 +21,20 @@ X = g['dx'][np.arange(B) % 1000]
 h = bqp.Handle(0)
 r = bqp.solve_ocp(lm.prob, X, handle=h)
 r = bqp.solve_ocp(lm.prob, X, handle=h)
-ms, _ = h.kernel_ms()
-st = np.zeros((B, 16))
+st = np.zeros((B, 32))
 _lib.check(lib.bqp_debug_stamps(h.value, 20, 6, 616, _lib.ptr(st)), 'stamps')
-names = ['residuals', 'factor:recip+Dx', 'factor:F\'DF', 'factor:riccati', 'solve:q+F\'e',
-         'solve:prepass', 'solve:backward', 'solve:post-bwd', 'solve:forward', 'solve:post-fwd',
-         'step_len', 'comp_after', 'row update', 'stage update', 'loop top', 'factor tail']
-tot = st.sum(axis=1).mean()
-print('batch %d kernel %.3f ms, mean iterations %.2f, cycles/instance (stamped) %.0f' % (B, ms, r.iterations.mean(), tot))
-for i, n in enumerate(names):
-    if st[:, i].mean() > 0:
-        print('%-18s %10.0f cyc  %5.1f %%  per-iter %8.0f' % (n, st[:, i].mean(), 100 * st[:, i].mean() / tot, st[:, i].mean() / r.iterations.mean()))
+# STAMP(id) closes phase id; the phase names follow the barrier schedule of bqp_ocp.hip
+stage = ['wait B0 + residual combine', 'combine', 'wait B1', 'decide + factor', 'wait B2',
+         'solve pred', 'wait B3,B4', 'solve corr', 'wait B5,B6', 'update + partials']
+row = ['wait B0', 'row residuals', 'rhs pred', 'wait B1,B2', 'wait B3',
+       'ratio/comp/sigma/rhs corr', 'wait B4,B5', 'ratio corr + apply', 'wait B6 + lam side']
+ms, _ = h.kernel_ms()
+it = r.iterations.mean()
+print('batch %d kernel %.3f ms, mean iterations %.2f' % (B, ms, it))
+for role, names, base in (('stage wave', stage, 0), ('row wave', row, 16)):
+    tot = st[:, base:base + 16].sum(axis=1).mean()
+    print('%s: cycles/instance (stamped loop) %.0f' % (role, tot))
+    for i, n in enumerate(names):
+        v = st[:, base + i].mean()
+        if v > 0:
+            print('  %-28s %10.0f cyc  %5.1f %%  per-iter %8.0f' % (n, v, 100 * v / tot, v / it))

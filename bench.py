@@ -1,19 +1,28 @@
-"""Benchmark: batched Moore-Greitzer N=20 MPC QP solves on MI355X (BASELINE.json configs[1]).
+"""Benchmark: batched MPC QP solves on MI355X (BASELINE.json configs).
 
-One "step" = one batched solve of the config-C2 workload: 1024 independent F1 LMPC QPs
-(costLMPC.m / constraintsLMPC.m; 21 decision variables, 806 inequality rows incl. the 616-row
-terminal set) at the 1000 stored closed-loop states of LMPC_N20_sys_full.mat cycled to 1024,
-fp64, inputs resident in HBM, through bqp_solve_ocp_batched_device (one kernel launch).
+Default (the driver's bench line) = config C2, BASELINE.json configs[1]: one "step" = one
+batched solve of 1024 independent F1 LMPC QPs per GPU (costLMPC.m / constraintsLMPC.m; 21
+decision variables, 806 inequality rows incl. the 616-row terminal set) at the 1000 stored
+closed-loop states of LMPC_N20_sys_full.mat cycled to 1024, fp64, inputs resident in HBM,
+through bqp_solve_ocp_batched_device (one solve-kernel launch).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C3|C4|C5] [--batch B]
 
-N > 1: launched by torch.distributed.run, one rank per GPU; each rank solves its own batch
-(weak scaling, no collective in the timed region); results are gathered once after timing
-(RCCL all-gather) and checked on rank 0.
+Other configs - measured the same way, reported in DESIGN.md:
+  C3  trackingMPC double integrator (F5), N=30, 22-row terminal set, 4096 per GPU (1024 x0 x 4
+      references), per-instance linear terms;
+  C4  learned-model Monte-Carlo: 65 536 perturbed (A, B) MG models in total, N=20, sharded
+      contiguously over the ranks (strong scaling), per-instance models;
+  C5  long-horizon MG DMS tracking LMPC (F2), N=100, 8192 per GPU, fp64 (no fp32 path yet).
 
-Prints ONE JSON line (rank 0) with value = QP-steps/s over all ranks, the roofline of the solve
-kernel (algorithmic FP64 flops / kernel time, hipEvents on the launch stream) and the CPU
-baseline (oracle/cpu_ipm.c, the same algorithm in C, OpenMP over host cores, bounded sample).
+N > 1: launched by torch.distributed.run, one rank per GPU; each rank solves its own shard
+(no collective in the timed region); the first moves and exit flags are all-gathered once
+after timing (RCCL over xGMI) - bqp.dist.
+
+Prints ONE JSON line (rank 0): value = QP-steps/s over all ranks; roofline of the solve kernel
+(algorithmic FP64 flops / kernel time from hipEvents on the launch stream; HBM traffic from the
+committed rocprofv3 PMC summary profiles/pmc_latest.json); the CPU baseline (oracle/cpu_ipm.c,
+the same algorithm in C, OpenMP over host cores, bounded sample).
 """
 import argparse
 import ctypes as C
@@ -29,7 +38,8 @@ sys.path.insert(0, os.path.join(ROOT, 'learning-based-mpc_amd'))
 import numpy as np  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) dense peak, spec
-HBM_PEAK_GBS = 8000.0
+METRIC = 'QP-steps/s (whole node) at N=20 Moore-Greitzer; KKT-residual vs MATLAB ref'
+GOLD = os.path.join(ROOT, 'tests', 'golden')
 
 
 def flops_per_iter(N, ns, nu, nx, m_T):
@@ -39,38 +49,118 @@ def flops_per_iter(N, ns, nu, nx, m_T):
                 + 8 * m_s) + m_T * (ns ** 2 + 9 * ns + 12)
 
 
-def build_problem():
-    """MG LMPC design data exactly as MATLAB held it (tests/golden/mg_design.npz, from the
-    R2019a workspace dump) + the 616-row terminal set (term_set.mat)."""
+# ------------------------------------------------------------------------------------------
+# workloads: (problem, per-instance inputs of this rank, K_ref source)
+# ------------------------------------------------------------------------------------------
+def _mg_design():
+    d = np.load(os.path.join(GOLD, 'mg_design.npz'))
+    ts = np.load(os.path.join(GOLD, 'term_set.npz'))
+    return d, ts
+
+
+def workload(cfg, batch, rank, world):
+    """Returns dict(prob, X (b, nx), A, B, w (per-instance or None), uniq (index of each
+    instance into the K_ref sample), sample (x0/A/B/w of the unique instances), total,
+    scaling, text)."""
     import bqp
-    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'mg_design.npz'))
-    ts = np.load(os.path.join(ROOT, 'tests', 'golden', 'term_set.npz'))
-    lm = bqp.LMPC(d['A'], d['B'], d['K'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
-                  d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], ts['F_w_N'], ts['h_w_N'], N=20)
-    return lm
+    from bqp import dist as bd
+    if cfg in ('C2', 'C4'):
+        d, ts = _mg_design()
+        lm = bqp.LMPC(d['A'], d['B'], d['K'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                      d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], ts['F_w_N'], ts['h_w_N'], N=20)
+        dx = np.load(os.path.join(GOLD, 'lmpc_N20.npz'))['dx']
+        if cfg == 'C2':
+            B = batch or 1024
+            gi = (np.arange(B) + rank * B) % 1000
+            return dict(prob=lm.prob, X=dx[gi], A=None, B=None, w=None, uniq=gi,
+                        sample=dict(X=dx[:1000]), total=B * world, scaling='weak', gidx=gi,
+                        text='C2: MG LMPC (F1) N=20, 616-row terminal set, batch %d per GPU, fp64' % B,
+                        data='synthetic: the 1000 stored closed-loop states of LMPC_N20_sys_full.mat cycled')
+        total = batch or 65536
+        a, b = bd.shard(total, rank, world)
+        rng = np.random.default_rng(4)                 # SURVEY 8(d) C4 generator, seed 4
+        E = rng.standard_normal((total, 4, 4))
+        e = rng.standard_normal((total, 4, 1))
+        A = d['A'] + 0.01 * E[a:b] * np.abs(d['A'])
+        Bm = d['B'].reshape(4, 1) + 0.01 * e[a:b] * np.abs(d['B'].reshape(4, 1))
+        gi = np.arange(a, b)
+        ns = b - a                                     # K_ref of every instance of the shard
+        return dict(prob=lm.prob, X=dx[gi % 1000], A=A, B=Bm, w=None, uniq=np.arange(b - a) % ns,
+                    sample=dict(X=dx[gi[:ns] % 1000], A=A[:ns], B=Bm[:ns]), total=total,
+                    scaling='strong', gidx=gi,
+                    text='C4: MG LMPC (F1) N=20, %d perturbed (A,B) models in total, sharded over %d GPU(s), fp64'
+                         % (total, world),
+                    data='synthetic: A_i = A + 0.01 E_i|A|, B_i = B + 0.01 e_i|B| (seed 4), x0 cycled from C2')
+    if cfg == 'C3':
+        g = np.load(os.path.join(GOLD, 'di_design.npz'))
+        N = int(g['N'])
+        tm = bqp.TrackingMPC(g['A'], g['B'], g['Q'], g['R'], g['P'], g['T'], g['LAMBDA'], g['PSI'],
+                             g['F_x'], g['h_x'], g['F_u'], g['h_u'], g['F_T'], g['h_T'], N=N)
+        B = batch or 4096
+        nu_ = len(g['x0']) * len(g['xs'])
+        gi = (np.arange(B) + rank * B) % nu_
+        X = g['x0'][gi // len(g['xs'])]
+        XS = g['xs'][gi % len(g['xs'])]
+        w, _ = tm.linear_terms(XS)
+        allx = g['x0'][np.arange(nu_) // len(g['xs'])]
+        allw, _ = tm.linear_terms(g['xs'][np.arange(nu_) % len(g['xs'])])
+        return dict(prob=tm.prob, X=X, A=None, B=None, w=w, uniq=gi, sample=dict(X=allx, w=allw),
+                    total=B * world, scaling='weak', gidx=gi,
+                    text='C3: trackingMPC DI (F5) N=%d, %d-row terminal set, batch %d per GPU, fp64'
+                         % (N, len(g['h_T']), B),
+                    data='synthetic: 1024 feasible x0 ~ U([-5,5]^2) (seed 30) x 4 references '
+                         '(RunExample.m:213-223), tests/golden/di_design.npz')
+    if cfg == 'C5':
+        d, ts = _mg_design()
+        g = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
+        N = int(g['N'])
+        tl = bqp.TrackingLMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                              d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], ts['F_w_N'],
+                              ts['h_w_N'], d['x_wp'], d['u_wp'], N=N)
+        B = batch or 8192
+        nx_ = len(g['x'])
+        gi = (np.arange(B) + rank * B) % nx_
+        X = g['x'] - tl.x_eq
+        return dict(prob=tl.prob, X=X[gi], A=None, B=None, w=None, uniq=gi, sample=dict(X=X),
+                    total=B * world, scaling='weak', gidx=gi,
+                    text='C5: MG DMS tracking LMPC (F2) N=%d, 616-row terminal set, batch %d per GPU, fp64'
+                         % (N, B),
+                    data='synthetic: the 499 stored closed-loop states of DSS_tLMPC.mat cycled')
+    raise ValueError(cfg)
 
 
-def cpu_baseline(prob, X_unique, threads):
-    """CPU leg: the C restatement of the same IPM (oracle/cpu_ipm.c), fp64, timed on the host
-    cores (single-core and all-core samples); also returns its per-instance iteration counts,
-    the K_ref of the algorithmic-flop count."""
+def ocp_dict(prob):
+    return dict(nx=prob.nx, nu=prob.nu, np=prob.np, N=prob.N, A=prob.A, B=prob.B, c=prob.c,
+                W=prob.W, w=prob.w, xlb=prob.xlb, xub=prob.xub, ulb=prob.ulb, uub=prob.uub,
+                Fp=prob.Fp, hp=prob.hp, kp=prob.poly_stage)
+
+
+def cpu_reference(prob, sample, threads, timed):
+    """CPU leg: the C restatement of the same IPM (oracle/cpu_ipm.c), fp64.  Returns the
+    per-instance iteration counts of the sample (K_ref of the algorithmic flop count, SURVEY.md
+    8(d)) and, if timed, single-core and all-core throughput on a bounded sample."""
     from oracle import cpu_ref
-    ocp = dict(nx=prob.nx, nu=prob.nu, np=prob.np, N=prob.N, A=prob.A, B=prob.B, c=prob.c,
-               W=prob.W, w=prob.w, xlb=prob.xlb, xub=prob.xub, ulb=prob.ulb, uub=prob.uub,
-               Fp=prob.Fp, hp=prob.hp, kp=prob.poly_stage)
+    ocp = ocp_dict(prob)
     cpu_ref.lib()
-    s1 = X_unique[:256]
-    t0 = time.perf_counter(); cpu_ref.solve(ocp, s1, threads=1); t1 = time.perf_counter()
-    single = len(s1) / (t1 - t0)
-    reps = max(1, int(np.ceil(single * threads * 1.0 / len(X_unique))))
-    sa = np.tile(X_unique, (reps, 1))
-    t0 = time.perf_counter(); ra = cpu_ref.solve(ocp, sa, threads=threads); t1 = time.perf_counter()
-    allc = len(sa) / (t1 - t0)
-    kref = ra['iterations'][:len(X_unique)]
+    X = sample['X']
+    kw = {k: sample[k] for k in ('A', 'B', 'w') if k in sample}
+    r = cpu_ref.solve(ocp, X, threads=threads, **kw)
+    kref = r['iterations'].astype(float)
+    if not timed:
+        return None, kref
+    n1 = min(256, len(X))
+    kw1 = {k: v[:n1] for k, v in kw.items()}
+    t0 = time.perf_counter(); cpu_ref.solve(ocp, X[:n1], threads=1, **kw1); t1 = time.perf_counter()
+    single = n1 / (t1 - t0)
+    reps = max(1, int(np.ceil(single * threads * 1.0 / len(X))))
+    kwa = {k: np.concatenate([v] * reps) for k, v in kw.items()}
+    Xa = np.concatenate([X] * reps)
+    t0 = time.perf_counter(); cpu_ref.solve(ocp, Xa, threads=threads, **kwa); t1 = time.perf_counter()
+    allc = len(Xa) / (t1 - t0)
     return dict(value=round(allc, 1), unit='QP-steps/s', cores=threads, kind='port',
                 single_core=round(single, 1),
-                sample='%d C2 QPs all-core + %d single-core; oracle/cpu_ipm.c (same IPM, fp64, '
-                       '-O3 -march=native, OpenMP)' % (len(sa), len(s1))), kref
+                sample='%d QPs all-core + %d single-core of the same workload; oracle/cpu_ipm.c '
+                       '(same IPM, fp64, -O3 -march=native, OpenMP)' % (len(Xa), n1)), kref
 
 
 def main():
@@ -78,14 +168,16 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--batch', type=int, default=1024)
+    ap.add_argument('--config', default='C2', choices=['C2', 'C3', 'C4', 'C5'])
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     import bqp
-    from bqp import _lib
+    from bqp import _lib, dist as bd
+    from bqp.ocp import _cm
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -95,29 +187,29 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
-    lm = build_problem()
-    prob = lm.prob
-    g = np.load(os.path.join(ROOT, 'tests', 'golden', 'lmpc_N20.npz'))
-    B = args.batch
-    X = g['dx'][(np.arange(B) + rank * B) % 1000]
+    wl = workload(args.config, args.batch, rank, world)
+    prob, X = wl['prob'], wl['X']
+    B = X.shape[0]
+    N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
+    nv = nx + nu + npar
 
     # ---- resident device inputs / outputs (torch is only the allocator) ------------------
-    from bqp.ocp import pack
-    dims, hdata, batch, keep = pack(prob, X)
-    N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
-
     def dt(a):
-        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
 
-    from bqp.ocp import _cm
-    dA, dB = dt(_cm(prob.A)), dt(_cm(prob.B))
-    dW, dw, dc = dt(_cm(prob.W)), dt(prob.w), dt(prob.c)
+    dA = dt(_cm(prob.A) if wl['A'] is None else _cm(wl['A']))
+    dB = dt(_cm(prob.B) if wl['B'] is None else _cm(wl['B']))
+    dw = dt(prob.w if wl['w'] is None else wl['w'])
+    dW, dc = dt(_cm(prob.W)), dt(prob.c)
     dxlb, dxub, dulb, duub = dt(prob.xlb), dt(prob.xub), dt(prob.ulb), dt(prob.uub)
     dF, dh, dx0 = dt(_cm(prob.Fp)), dt(prob.hp), dt(X)
     P = _lib.dptr
     data = _lib.OcpData(A=P(dA), B=P(dB), c=P(dc), W=P(dW), w=P(dw), xlb=P(dxlb), xub=P(dxub),
                         ulb=P(dulb), uub=P(duub), Fp=P(dF), hp=P(dh), x0=P(dx0),
-                        sA=0, sB=0, sc=0, sW=0, sw=0, sxb=0, sub=0, sFp=0, shp=0, sx0=nx)
+                        sA=0 if wl['A'] is None else nx * nx, sB=0 if wl['B'] is None else nx * nu,
+                        sc=0, sW=0, sw=0 if wl['w'] is None else (N + 1) * nv, sxb=0, sub=0,
+                        sFp=0, shp=0, sx0=nx)
+    dims = _lib.OcpDims(nx, nu, npar, N, mp, prob.poly_stage)
     ox = torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev)
     ou = torch.empty((B, N, nu), dtype=torch.float64, device=dev)
     ot = torch.empty((B, npar), dtype=torch.float64, device=dev)
@@ -141,7 +233,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -149,70 +240,72 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = bd.max_over_ranks(t1 - t0, dev, world)
     # kernel-only timing: hipEvents on the launch stream, separate pass (one event pair / step)
+    kms = []
     for _ in range(min(args.steps, 20)):
         step()
         ms, _ = h.kernel_ms()
         kms.append(ms)
     kernel_ms = float(np.mean(kms))
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # one RCCL all-gather of the first moves + status after timing (result collection)
-        u0 = ou[:, 0, :].contiguous()
-        gath = [torch.empty_like(u0) for _ in range(world)]
-        dist.all_gather(gath, u0)
-        fl = [torch.empty_like(oe) for _ in range(world)]
-        dist.all_gather(fl, oe)
+    # one all-gather of the first moves + status after timing (result collection, bqp.dist)
+    total_rows = wl['total'] if wl['scaling'] == 'strong' else B * world
+    u0_all = bd.gather_rows(ou[:, 0, :].contiguous(), total_rows, world)
+    fl_all = bd.gather_rows(oe, total_rows, world).cpu().numpy()
     flags = oe.cpu().numpy()
     u0 = ou[:, 0, 0].cpu().numpy()
-    # correctness on the bench batch vs fixture optima (instances present in the fixture)
-    sel = g['idx']
-    pos = {int(i): j for j, i in enumerate(sel)}
-    err = max([abs(u0[b] - g['du_star'][pos[int(((b + rank * B) % 1000))]])
-               for b in range(B) if int((b + rank * B) % 1000) in pos] or [0.0])
+
+    # correctness on the bench batch (C2: vs the fixture's exact optima)
+    check = {'converged_frac': float((flags == 1).mean()),
+             'infeasible_count_all_ranks': int((fl_all == -2).sum()),
+             'gathered_rows': int(u0_all.shape[0])}
+    if args.config == 'C2':
+        g = np.load(os.path.join(GOLD, 'lmpc_N20.npz'))
+        pos = {int(i): j for j, i in enumerate(g['idx'])}
+        err = max([abs(u0[b] - g['du_star'][pos[int(wl['gidx'][b])]])
+                   for b in range(B) if int(wl['gidx'][b]) in pos] or [0.0])
+        check['max_abs_du0_vs_exact'] = float(err)
 
     if rank == 0:
-        total = world * B * args.steps
-        value = total / elapsed
+        value = wl['total'] / (elapsed / args.steps) if wl['scaling'] == 'strong' \
+            else world * B * args.steps / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
         threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
-        cpu, kref_u = cpu_baseline(prob, g['dx'][:1000], threads)
-        # algorithmic flops per launch: sum over the batch of K_ref x F_iter
-        kref = kref_u[(np.arange(B) + rank * B) % 1000].astype(float)
-        F_it = flops_per_iter(20, 5, 1, 4, 616)
+        timed = not args.no_cpu
+        cpu, kref_u = cpu_reference(prob, wl['sample'], threads, timed)
+        # algorithmic flops per launch: sum over the batch of K_ref x F_iter;
+        # instances the reference solver does not converge on (infeasible) count with their
+        # own iteration count
+        kref = kref_u[wl['uniq']]
+        F_it = flops_per_iter(N, nx + npar, nu, nx, mp)
         flops_launch = float((kref * F_it).sum())
         achieved = flops_launch / (kernel_ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
-        if os.path.exists(pmc):
+        if args.config == 'C2' and os.path.exists(pmc):
             try:
                 traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
             except Exception:
                 traffic = None
-        if args.no_cpu:
-            cpu = None
+        check['mean_iterations_ref'] = float(kref.mean())
         line = {
-            'metric': 'QP-steps/s (whole node) at N=20 Moore-Greitzer; KKT-residual vs MATLAB ref',
+            'metric': METRIC,
             'value': round(value, 1), 'unit': 'QP-steps/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
-            'data': 'synthetic: the 1000 stored closed-loop states of LMPC_N20_sys_full.mat cycled',
-            'config': {'workload': 'C2: MG LMPC (F1) N=20, 616-row terminal set, batch %d per GPU, fp64' % B,
-                       'batch_per_gpu': B, 'horizon': 20, 'parallelism': 'dp%d' % world},
+            'higher_is_better': True, 'scaling': wl['scaling'], 'vs_baseline': None, 'dtype': 'f64',
+            'data': wl['data'],
+            'config': {'workload': wl['text'], 'batch_per_gpu': B, 'horizon': N,
+                       'parallelism': 'dp%d' % world},
             'roofline': {'bound': 'mfma', 'achieved': round(achieved, 4),
                          'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
                          'kernel_ms': round(kernel_ms, 4),
                          'flops_per_launch': flops_launch,
                          'note': 'FP64 vector ALU roof (MI355X FP64 matrix peak is the same 78.6 TF/s); '
-                                 'algorithmic flops = K_ref x F_iter (SURVEY.md 8(d))'},
+                                 'algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); traffic = HBM '
+                                 'bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE (profiles/)'},
             'cpu_baseline': cpu,
-            'check': {'converged_frac': float((flags == 1).mean()),
-                      'max_abs_du0_vs_exact': float(err),
-                      'mean_iterations_ref': float(kref.mean())},
+            'check': check,
         }
         print(json.dumps(line))
     if world > 1:

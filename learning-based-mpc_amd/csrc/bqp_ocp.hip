@@ -90,6 +90,17 @@ __device__ __forceinline__ double rl(double v, int src) {
 }
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
+// 1/t for the row slacks and multipliers (t > 0 inside the IPM): hardware reciprocal estimate
+// refined by two Newton steps (|error| ~ 1 ulp); recomputed at every use instead of kept in
+// registers (the row wave's register budget at two waves per SIMD)
+__device__ __forceinline__ double frcp(double t) {
+    double r = __builtin_amdgcn_rcp(t);
+    double e = __builtin_fma(-t, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-t, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
 template <int N>
 __device__ __forceinline__ bool chol_small(const double (&M)[N][N], double (&L)[N][N]) {
     bool ok = true;
@@ -1035,8 +1046,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 
     // row state: slack t, multiplier lam, 1/t; polytope rows also their residual ri (box-row
     // residuals are re-formed from the LDS stage vector and bounds when needed)
-    double tx[SPL][NB][2], lx[SPL][NB][2], itx[SPL][NB][2];
-    double tp[RPL], lp[RPL], itp[RPL], rp[RPL];
+    double tx[SPL][NB][2], lx[SPL][NB][2];
+    double tp[RPL], lp[RPL], rp[RPL];
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
 #pragma unroll
@@ -1053,18 +1064,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) itx[j][sl][h] = 1.0 / tx[j][sl][h];
             if (k <= N) {
 #pragma unroll
                 for (int sl = 0; sl < NB; ++sl) {
                     W[L.blam + (k * NB + sl) * 2] = pres(j, sl, 0) ? lx[j][sl][0] : 0.0;
                     W[L.blam + (k * NB + sl) * 2 + 1] = pres(j, sl, 1) ? lx[j][sl][1] : 0.0;
                     double d = 0;
-                    if (pres(j, sl, 0)) d += lx[j][sl][0] * itx[j][sl][0];
-                    if (pres(j, sl, 1)) d += lx[j][sl][1] * itx[j][sl][1];
+                    if (pres(j, sl, 0)) d += lx[j][sl][0] * frcp(tx[j][sl][0]);
+                    if (pres(j, sl, 1)) d += lx[j][sl][1] * frcp(tx[j][sl][1]);
                     W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
                     if (pres(j, sl, 0)) cs += tx[j][sl][0] * lx[j][sl][0];
                     if (pres(j, sl, 1)) cs += tx[j][sl][1] * lx[j][sl][1];
@@ -1082,7 +1089,6 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             ROW_FENCE(q);
-            itp[q] = 1.0 / tp[q];
             const int r = lane + WAVE * q;
             if (r < mp) {
                 double f[NV];
@@ -1091,7 +1097,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpp[c] += f[c] * lp[q];
                 cs += tp[q] * lp[q];
-                const double d = lp[q] * itp[q];
+                const double d = lp[q] * frcp(tp[q]);
                 int idx = 0;
 #pragma unroll
                 for (int i2 = 0; i2 < NV; ++i2) {
@@ -1170,7 +1176,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     // box-row predictor product dt_a * dlam_a (recomputed from the predictor direction)
     auto box_pred_prod = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> double {
         const double dt = box_dir(j, k, sl, h, L.dsv, L.duv);
-        const double dl = (-(tx[j][sl][h] * lx[j][sl][h]) - lx[j][sl][h] * dt) * itx[j][sl][h];
+        const double dl = (-(tx[j][sl][h] * lx[j][sl][h]) - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
         return dt * dl;
     };
 
@@ -1187,7 +1193,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                     double e = 0.0;
                     if (pres(j, sl, h)) {
                         const double pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
-                        e = (lx[j][sl][h] * box_res(j, k, sl, h) - rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu)) * itx[j][sl][h];
+                        e = (lx[j][sl][h] * box_res(j, k, sl, h) - rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu)) * frcp(tx[j][sl][h]);
                     }
                     W[L.ebox + (k * NB + sl) * 2 + h] = e;
                 }
@@ -1201,7 +1207,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             const int r = lane + WAVE * q;
             if (r < mp) {
                 const double pr = corr ? W[L.prp + r] : 0.0;
-                const double e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * itp[q];
+                const double e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * frcp(tp[q]);
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpe[c] += Fs[c * mpad + r] * e;
             }
@@ -1231,10 +1237,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                     const double pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
                     const double rc = rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu);
                     const double dt = box_dir(j, k, sl, h, ids, idu);
-                    const double dl = (-rc - lx[j][sl][h] * dt) * itx[j][sl][h];
+                    const double dl = (-rc - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
                     if (mode == 0) {
-                        acc = fmax(acc, -dt * itx[j][sl][h]);
-                        acc = fmax(acc, -dl / lx[j][sl][h]);
+                        acc = fmax(acc, -dt * frcp(tx[j][sl][h]));
+                        acc = fmax(acc, -dl * frcp(lx[j][sl][h]));
                     } else if (mode == 1) {
                         acc += (tx[j][sl][h] + al * dt) * (lx[j][sl][h] + al * dl);
                     } else {
@@ -1253,10 +1259,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             const double pr = corr ? W[L.prp + r] : 0.0;
             const double rc = rcv(tp[q], lp[q], pr, corr, smu);
             const double dt = -rp[q] - fdot(r, dvp);
-            const double dl = (-rc - lp[q] * dt) * itp[q];
+            const double dl = (-rc - lp[q] * dt) * frcp(tp[q]);
             if (mode == 0) {
-                acc = fmax(acc, -dt * itp[q]);
-                acc = fmax(acc, -dl / lp[q]);
+                acc = fmax(acc, -dt * frcp(tp[q]));
+                acc = fmax(acc, -dl * frcp(lp[q]));
             } else if (mode == 1) {
                 acc += (tp[q] + al * dt) * (lp[q] + al * dl);
                 W[L.prp + r] = dt * dl;

@@ -14,13 +14,13 @@ _lib.LIB_PATH = os.path.join(ROOT, 'learning-based-mpc_amd', 'build', 'stamps', 
 lib = _lib.load()
 lib.bqp_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _lib._PD]
 import bench
-lm = bench.build_problem()
 g = np.load(os.path.join(ROOT, 'tests', 'golden', 'lmpc_N20.npz'))
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+lm = bench.workload('C2', B, 0, 1)['prob']
 X = g['dx'][np.arange(B) % 1000]
 h = bqp.Handle(0)
-r = bqp.solve_ocp(lm.prob, X, handle=h)
-r = bqp.solve_ocp(lm.prob, X, handle=h)
+r = bqp.solve_ocp(lm, X, handle=h)
+r = bqp.solve_ocp(lm, X, handle=h)
 st = np.zeros((B, 32))
 _lib.check(lib.bqp_debug_stamps(h.value, 20, 6, 616, _lib.ptr(st)), 'stamps')
 # STAMP(id) closes phase id; the phase names follow the barrier schedule of bqp_ocp.hip

@@ -417,16 +417,21 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     // itself, broadcast through the packed LDS table.
     const int ib = (lane < NS * NS) ? lane / NS : 0, jb = (lane < NS * NS) ? lane % NS : 0;
     const bool blane = lane < NS * NS && ib <= jb;
-    double Ai[NS], Aj[NS], Bl[NS][NU];
-#pragma unroll
-    for (int a_ = 0; a_ < NS; ++a_) {
-        Ai[a_] = Abar(a_, ib);
-        Aj[a_] = Abar(a_, jb);
-#pragma unroll
-        for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
-    }
     constexpr int PST = pk_stride(NS);
+    // the model operands of the factor and of the sweeps are re-read from LDS at the start of
+    // each phase (not kept live across the iteration: register budget at two waves per SIMD)
+    auto load_ab = [&](double (&Ai)[NS], double (&Aj)[NS], double (&Bl)[NS][NU]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int a_ = 0; a_ < NS; ++a_) {
+            Ai[a_] = Abar(a_, ib);
+            Aj[a_] = Abar(a_, jb);
+#pragma unroll
+            for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
+        }
+    };
     auto factor = [&]() __attribute__((always_inline)) -> bool {
+        double Ai[NS], Aj[NS], Bl[NS][NU];
+        load_ab(Ai, Aj, Bl);
         // stage-k entries each lane needs, prefetched one stage ahead as RAW operands (cost
         // entry, box diagonal) and combined only when the stage is processed; the polytope term
         // F'DF enters at stage kp only (a uniform branch).  Operation order (H + D) + FD.
@@ -602,12 +607,17 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     // right-hand side q = r_v + C'((lam o ri - rc)/t): the row wave supplies the box terms
     // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
     const int li = lane < NS ? lane : NS - 1;
-    double Acol[NS], Arow[NS], Bli[NU];     // Abar(:, li), Abar(li, :), Bbar(li, :) for the sweeps
-#pragma unroll
-    for (int c = 0; c < NS; ++c) { Acol[c] = Abar(c, li); Arow[c] = Abar(li, c); }
-#pragma unroll
-    for (int x = 0; x < NU; ++x) Bli[x] = Bbar(li, x);
     auto solve = [&](int ods, int odu) __attribute__((always_inline)) {
+        double Acol[NS], Arow[NS], Bli[NU], Bl[NS][NU];  // Abar(:, li), Abar(li, :), Bbar(li, :), Bbar
+#pragma unroll
+        for (int c = 0; c < NS; ++c) {
+            Acol[c] = Abar(c, li);
+            Arow[c] = Abar(li, c);
+#pragma unroll
+            for (int x = 0; x < NU; ++x) Bl[c][x] = Bbar(c, x);
+        }
+#pragma unroll
+        for (int x = 0; x < NU; ++x) Bli[x] = Bbar(li, x);
         double qs[SPL][NS], qu[SPL][NU];
         double gpe[NV];
 #pragma unroll

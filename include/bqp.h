@@ -162,6 +162,65 @@ int bqp_quadprog_batched_device(bqp_handle h, const bqp_dims* d, int batch,
                                 double* lam_ineqlin, double* lam_eqlin, double* lam_lower,
                                 double* lam_upper, bqp_output* out, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Learning-based MPC (forms F3/F4): the learned prediction model
+ *   x+ = A x + B u + g(x, u),  g = Nadaraya-Watson oracle over a data window (oracleL2NW.m)
+ * makes the per-step problem an NLP; it is solved by a Gauss-Newton SQP whose QP sub-problems
+ * run in the dense kernel.  Replaces
+ *   fmincon(costLBMPC, constraintsLBMPC)   matlab/LBMPC/functions/ocpLBMPC.m:27-31   (F3)
+ *   solver(..., 'p', data)                 matlab/LBMPC/examples/hybrid_LBMPC_casadi.m:173-178 (F4)
+ *   oracleL2NW(x, u, data)                 matlab/LBMPC/functions/oracleL2NW.m:1-36
+ *
+ * Decision z = [v_0..v_{N-1}; theta] (n = N*nu + np) with the rollout input u_k = K x_k + v_k
+ * (F3: v = c, K = Kstabil; F4: v = u - u_eq, K = 0), deviation coordinates.  Cost:
+ *   sum_{k < n_run} |Lq (x^L_k - LAMBDA th)|^2 + |Lr (u^L_k - PSI th)|^2
+ *     + |Lp (x^T_N - LAMBDA th)|^2 + |Lt (LAMBDA th - xs)|^2
+ * on the LEARNED rollout x^L (terminal x^T = learned or nominal x_N), subject to the condensed
+ * NOMINAL-model constraints Ain z <= bin (the host shim builds them from constraintsLBMPC.m /
+ * hybrid_LBMPC_casadi.m:283-310).  The NW window is 7 x q column-major per instance: rows 1-3
+ * X = [dx1; dx2; du], rows 4-7 Y (hybrid_LBMPC_casadi.m:128 layout; no validity mask).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    int nx, nu, np, N;
+    int n_run;          /* running-cost stages k = 0..n_run-1 (F3: N-2, costLBMPC.m:30; F4: N) */
+    int term_learned;   /* terminal P cost on the learned (1, F3) or nominal (0, F4) x_N */
+    int q;              /* points in the NW window (<= 512) */
+    int m;              /* rows of Ain */
+} bqp_lbmpc_dims;
+
+typedef struct {
+    const double *A, *B, *K;          /* nx*nx, nx*nu, nu*nx (column-major), shared */
+    const double *Lq, *Lr, *Lp, *Lt;  /* upper-triangular ROW-major weight factors:
+                                         Lq'Lq = w Q, Lr'Lr = w R (w = running weight), Lp'Lp = P, Lt'Lt = T */
+    const double *LAMBDA, *PSI, *xs;  /* nx*np, nu*np (column-major), nx */
+    const double* data; int64_t sdata;  /* NW window 7*q per instance (stride; 0 = shared) */
+    const double* x0;   int64_t sx0;    /* nx per instance */
+    const double* Ain;                  /* m*n column-major, shared */
+    const double* bin;  int64_t sbin;   /* m per instance */
+    double bandwidth, lambda;           /* NW kernel; <= 0 selects the reference's 0.5, 1e-3 */
+} bqp_lbmpc_data;
+
+/* Batched NW oracle: g (batch*4) and optionally dg/dxi (batch*4*3, row-major per instance) at
+ * the query points xi (batch*3). */
+int bqp_nw_oracle(bqp_handle h, int batch, int q, const double* data, int64_t sdata,
+                  const double* xi, double* g, double* dg, double bandwidth, double lambda);
+int bqp_nw_oracle_device(bqp_handle h, int batch, int q, const double* data, int64_t sdata,
+                         const double* xi, double* g, double* dg, double bandwidth,
+                         double lambda, void* stream);
+
+/* SQP solve.  z (batch*n): in = start (fmincon's opt_var warm start), out = solution; lam
+ * (batch*m, may be NULL): multipliers of Ain z <= bin; cost (batch, may be NULL); exitflag:
+ * 1 converged, 0 iteration limit (opt->max_iter SQP iterations), -2 QP sub-problem infeasible,
+ * -8 numerical failure.  The _device variant synchronises its stream every 4 SQP iterations
+ * (early exit when the whole batch has converged). */
+int bqp_lbmpc_solve_batched(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                            const bqp_lbmpc_data* data, const bqp_options* opt, double* z,
+                            double* lam, double* cost, int* exitflag, int* iterations);
+int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                                   const bqp_lbmpc_data* data, const bqp_options* opt, double* z,
+                                   double* lam, double* cost, int* exitflag, int* iterations,
+                                   void* stream);
+
 /* Timing of the most recent solve on this handle: kernel time measured with hipEvents on the
  * launch stream (ms), and the number of kernel launches it covered. */
 int bqp_last_kernel_ms(bqp_handle h, double* ms, int* launches);

@@ -51,9 +51,21 @@ class Strides(C.Structure):
     _fields_ = [(n, C.c_int64) for n in ('sH', 'sf', 'sA', 'sb', 'sAeq', 'sbeq', 'slb', 'sub')]
 
 
+class LbmpcDims(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ('nx', 'nu', 'np', 'N', 'n_run', 'term_learned', 'q', 'm')]
+
+
+class LbmpcData(C.Structure):
+    _fields_ = [(n, _PD) for n in ('A', 'B', 'K', 'Lq', 'Lr', 'Lp', 'Lt', 'LAMBDA', 'PSI', 'xs')] + \
+               [('data', _PD), ('sdata', C.c_int64), ('x0', _PD), ('sx0', C.c_int64),
+                ('Ain', _PD), ('bin', _PD), ('sbin', C.c_int64),
+                ('bandwidth', C.c_double), ('lambda_', C.c_double)]
+
+
 EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version',
            'bqp_solve_ocp_batched', 'bqp_solve_ocp_batched_device', 'bqp_quadprog_batched',
-           'bqp_quadprog_batched_device', 'bqp_last_kernel_ms']
+           'bqp_quadprog_batched_device', 'bqp_last_kernel_ms', 'bqp_nw_oracle',
+           'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device']
 
 _lib = None
 
@@ -88,6 +100,16 @@ def load():
     lib.bqp_quadprog_batched_device.argtypes = [C.c_void_p, C.POINTER(Dims), C.c_int, C.POINTER(Strides)] + \
         [_PD] * 8 + [C.POINTER(Options), _PD, _PD, _PI, _PD, _PD, _PD, _PD, C.c_void_p, C.c_void_p]
     lib.bqp_last_kernel_ms.argtypes = [C.c_void_p, _PD, _PI]
+    lib.bqp_nw_oracle.argtypes = [C.c_void_p, C.c_int, C.c_int, _PD, C.c_int64, _PD, _PD, _PD,
+                                  C.c_double, C.c_double]
+    lib.bqp_nw_oracle_device.argtypes = [C.c_void_p, C.c_int, C.c_int, _PD, C.c_int64, _PD, _PD,
+                                         _PD, C.c_double, C.c_double, C.c_void_p]
+    lib.bqp_lbmpc_solve_batched.argtypes = [C.c_void_p, C.POINTER(LbmpcDims), C.c_int,
+                                            C.POINTER(LbmpcData), C.POINTER(Options), _PD, _PD,
+                                            _PD, _PI, _PI]
+    lib.bqp_lbmpc_solve_batched_device.argtypes = [C.c_void_p, C.POINTER(LbmpcDims), C.c_int,
+                                                   C.POINTER(LbmpcData), C.POINTER(Options), _PD,
+                                                   _PD, _PD, _PI, _PI, C.c_void_p]
     _lib = lib
     return lib
 

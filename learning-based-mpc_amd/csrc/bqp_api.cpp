@@ -42,6 +42,7 @@ struct bqp_handle_s {
     DevBuf work;   // tables + stats (device entry points)
     DevBuf stage;  // staging of host-pointer calls
     DevBuf dwork;  // dense per-instance scratch
+    DevBuf lwork;  // learning-based MPC (SQP) buffers
     int last_batch = 0;
 };
 
@@ -136,6 +137,7 @@ int bqp_destroy(bqp_handle h) {
         h->work.release();
         h->stage.release();
         h->dwork.release();
+        h->lwork.release();
         if (h->ev0) hipEventDestroy(h->ev0);
         if (h->ev1) hipEventDestroy(h->ev1);
         if (h->stream) hipStreamDestroy(h->stream);
@@ -429,6 +431,200 @@ int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_s
     if (lam_lower) HIP_TRY(hipMemcpyAsync(lam_lower, lld, sizeof(double) * nxo, hipMemcpyDeviceToHost, h->stream));
     if (lam_upper) HIP_TRY(hipMemcpyAsync(lam_upper, lud, sizeof(double) * nxo, hipMemcpyDeviceToHost, h->stream));
     if (out) HIP_TRY(hipMemcpyAsync(out, od, outbytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return BQP_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// learning-based MPC: Nadaraya-Watson oracle and the Gauss-Newton SQP (bqp_lbmpc.hip)
+// ------------------------------------------------------------------------------------------
+#define LB_NTRIAL 8
+
+int bqp_nw_oracle_device(bqp_handle h, int batch, int q, const double* data, int64_t sdata,
+                         const double* xi, double* g, double* dg, double bandwidth,
+                         double lambda, void* stream) {
+    if (!h || batch <= 0 || q <= 0 || !data || !xi || !g) return BQP_E_ARG;
+    if (q > 512) return BQP_E_UNSUPPORTED;
+    DevScope ds(h->device);
+    const double bw = bandwidth > 0 ? bandwidth : 0.5, lam = lambda > 0 ? lambda : 1e-3;
+    HIP_TRY(bqp::launch_nw_oracle(batch, q, data, sdata, xi, g, dg, bw, lam, (hipStream_t)stream));
+    return BQP_OK;
+}
+
+int bqp_nw_oracle(bqp_handle h, int batch, int q, const double* data, int64_t sdata,
+                  const double* xi, double* g, double* dg, double bandwidth, double lambda) {
+    if (!h || batch <= 0 || q <= 0 || !data || !xi || !g) return BQP_E_ARG;
+    if (q > 512) return BQP_E_UNSUPPORTED;
+    DevScope ds(h->device);
+    const size_t nd = span(batch, sdata, (size_t)7 * q);
+    const size_t tot = nd + (3 + 4 + 12) * (size_t)batch;
+    HIP_TRY(h->stage.reserve(sizeof(double) * tot));
+    double* dd = (double*)h->stage.p;
+    double* dx = dd + nd;
+    double* dgv = dx + 3 * (size_t)batch;
+    double* ddg = dgv + 4 * (size_t)batch;
+    HIP_TRY(hipMemcpyAsync(dd, data, sizeof(double) * nd, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(dx, xi, sizeof(double) * 3 * batch, hipMemcpyHostToDevice, h->stream));
+    int rc = bqp_nw_oracle_device(h, batch, q, dd, sdata, dx, dgv, ddg, bandwidth, lambda, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(g, dgv, sizeof(double) * 4 * batch, hipMemcpyDeviceToHost, h->stream));
+    if (dg) HIP_TRY(hipMemcpyAsync(dg, ddg, sizeof(double) * 12 * batch, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return BQP_OK;
+}
+
+static int lbmpc_check(const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_data* D) {
+    if (!d || !D || batch <= 0) return BQP_E_ARG;
+    if (d->N <= 0 || d->n_run < 0 || d->n_run > d->N || d->q <= 0 || d->m < 0) return BQP_E_ARG;
+    if (!D->A || !D->B || !D->K || !D->Lq || !D->Lr || !D->Lp || !D->Lt || !D->LAMBDA ||
+        !D->PSI || !D->xs || !D->data || !D->x0 || (d->m > 0 && (!D->Ain || !D->bin)))
+        return BQP_E_ARG;
+    const int n = d->N * d->nu + d->np;
+    if (!bqp::lbmpc_supported(d->nx, d->nu, d->np, n, d->q) || d->m > 8192) return BQP_E_UNSUPPORTED;
+    return BQP_OK;
+}
+
+int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                                   const bqp_lbmpc_data* D, const bqp_options* opt, double* z,
+                                   double* lam, double* cost, int* exitflag, int* iterations,
+                                   void* stream) {
+    if (!h) return BQP_E_ARG;
+    int rc = lbmpc_check(d, batch, D);
+    if (rc) return rc;
+    if (!z || !exitflag || !iterations) return BQP_E_ARG;
+    DevScope ds(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    bqp_options o;
+    resolve(opt, &o);
+    const int N = d->N, n = N * d->nu + d->np, m = d->m;
+    const int nr = d->n_run * (d->nx + d->nu) + 2 * d->nx;
+    const size_t B = batch;
+    const size_t nd = B * nr * n + B * nr + B * n * n + B * n + 2 * B * m + B * n + B +
+                      B * LB_NTRIAL + 2 * B;
+    const size_t ni = 2 * B + 4;
+    HIP_TRY(h->lwork.reserve(sizeof(double) * nd + sizeof(int) * ni));
+    double* p = (double*)h->lwork.p;
+    bqp::LbmpcArgs a;
+    memset(&a, 0, sizeof(a));
+    a.Jr = p; p += B * nr * n;
+    a.er = p; p += B * nr;
+    a.H = p; p += B * n * n;
+    a.f = p; p += B * n;
+    a.bsh = p; p += B * m;
+    double* lam_int = p; p += B * m;
+    a.d = p; p += B * n;
+    a.cost0 = p; p += B;
+    a.costT = p; p += B * LB_NTRIAL;
+    a.stat = p; p += B;
+    a.cprev = p; p += B;
+    int* ip = (int*)p;
+    a.qpflag = ip; ip += B;
+    a.done = ip; ip += B;
+    a.ndone = ip;
+    a.lam = lam ? lam : lam_int;
+    a.z = z; a.flag = exitflag; a.iters = iterations;
+    a.N = N; a.n = n; a.nr = nr; a.m = m; a.q = d->q; a.n_run = d->n_run;
+    a.term_learned = d->term_learned; a.batch = batch; a.ntrial = LB_NTRIAL;
+    a.max_iter = o.max_iter;
+    const double bw = D->bandwidth > 0 ? D->bandwidth : 0.5;
+    a.hinv2 = 1.0 / (bw * bw);
+    a.lam_nw = D->lambda > 0 ? D->lambda : 1e-3;
+    a.tol_step = o.tol_stat;            // |d| <= tol_stat (1 + |z|)
+    a.tol_stat = 10.0 * o.tol_stat;     // |grad J + Ain' lam| <= 10 tol_stat (1 + |grad J|)
+    a.A = D->A; a.B = D->B; a.K = D->K; a.Lq = D->Lq; a.Lr = D->Lr; a.Lp = D->Lp; a.Lt = D->Lt;
+    a.LAM = D->LAMBDA; a.PSI = D->PSI; a.xs = D->xs;
+    a.data = D->data; a.sdata = D->sdata; a.x0 = D->x0; a.sx0 = D->sx0;
+    a.Ain = D->Ain; a.bin = D->bin; a.sbin = D->sbin;
+    HIP_TRY(hipMemsetAsync(a.done, 0, sizeof(int) * (B + 1), st));   // done[] and ndone
+    HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * B, st));
+    HIP_TRY(hipMemsetAsync(a.flag, 0, sizeof(int) * B, st));
+    // QP sub-problem (dense kernel): min 0.5 d'Hd + f'd  s.t.  Ain d <= bin - Ain z
+    const int64_t wst = bqp::dense_work_doubles(n, m, 0);
+    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * B + B * 4 + 8)));
+    bqp::DenseKernelArgs q;
+    memset(&q, 0, sizeof(q));
+    q.n = n; q.m = m; q.me = 0; q.batch = batch; q.max_iter = 100;
+    q.tol_stat = 1e-8; q.tol_feas = 1e-10; q.tol_comp = 1e-14; q.tau = 0.995;   // bqp_default_options
+    q.H = a.H; q.f = a.f; q.A = D->Ain; q.b = a.bsh;
+    q.sH = (int64_t)n * n; q.sf = n; q.sA = 0; q.sb = m;
+    q.x = a.d; q.lam_ineqlin = a.lam; q.exitflag = a.qpflag;
+    q.work = (double*)h->dwork.p; q.work_stride = wst;
+    q.stats = (double*)h->dwork.p + (size_t)wst * B;
+    HIP_TRY(hipEventRecord(h->ev0, st));
+    int launches = 0;
+    for (int it = 0; it < o.max_iter; ++it) {
+        HIP_TRY(bqp::launch_lbmpc_rollout(a, 1, st));
+        HIP_TRY(bqp::launch_lbmpc_normal(a, st));
+        HIP_TRY(bqp::launch_dense(q, st));
+        HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
+        HIP_TRY(bqp::launch_lbmpc_update(a, st));
+        launches += 5;
+        if ((it & 3) == 3 || it + 1 == o.max_iter) {
+            int nd_h = 0;
+            HIP_TRY(hipMemcpyAsync(&nd_h, a.ndone, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (nd_h >= batch) break;
+        }
+    }
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    h->timed = true;
+    h->launches = launches;
+    if (cost) HIP_TRY(hipMemcpyAsync(cost, a.cost0, sizeof(double) * B, hipMemcpyDeviceToDevice, st));
+    return BQP_OK;
+}
+
+int bqp_lbmpc_solve_batched(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                            const bqp_lbmpc_data* D, const bqp_options* opt, double* z,
+                            double* lam, double* cost, int* exitflag, int* iterations) {
+    if (!h) return BQP_E_ARG;
+    int rc = lbmpc_check(d, batch, D);
+    if (rc) return rc;
+    if (!z || !exitflag || !iterations) return BQP_E_ARG;
+    DevScope ds(h->device);
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N, m = d->m;
+    const int n = N * nu + np;
+    struct In { const double* src; size_t n; double* dst; };
+    In in[] = {
+        {D->A, (size_t)nx * nx, nullptr}, {D->B, (size_t)nx * nu, nullptr},
+        {D->K, (size_t)nu * nx, nullptr}, {D->Lq, (size_t)nx * nx, nullptr},
+        {D->Lr, (size_t)nu * nu, nullptr}, {D->Lp, (size_t)nx * nx, nullptr},
+        {D->Lt, (size_t)nx * nx, nullptr}, {D->LAMBDA, (size_t)nx * np, nullptr},
+        {D->PSI, (size_t)nu * np, nullptr}, {D->xs, (size_t)nx, nullptr},
+        {D->data, span(batch, D->sdata, (size_t)7 * d->q), nullptr},
+        {D->x0, span(batch, D->sx0, nx), nullptr},
+        {D->Ain, (size_t)m * n, nullptr}, {D->bin, span(batch, D->sbin, m), nullptr},
+        {z, (size_t)batch * n, nullptr},
+    };
+    const int nin = sizeof(in) / sizeof(in[0]);
+    size_t tot = 0;
+    for (int i = 0; i < nin; ++i) tot += (in[i].src ? in[i].n : 0);
+    const size_t nlam = (size_t)batch * m;
+    tot += nlam + batch;
+    HIP_TRY(h->stage.reserve(sizeof(double) * tot + sizeof(int) * 2 * (size_t)batch));
+    double* cur = (double*)h->stage.p;
+    for (int i = 0; i < nin; ++i) {
+        if (!in[i].src || in[i].n == 0) continue;
+        in[i].dst = cur;
+        HIP_TRY(hipMemcpyAsync(cur, in[i].src, sizeof(double) * in[i].n, hipMemcpyHostToDevice, h->stream));
+        cur += in[i].n;
+    }
+    double* zd = in[nin - 1].dst;
+    double* ld = cur; cur += nlam;
+    double* cd = cur; cur += batch;
+    int* ed = (int*)cur;
+    int* itd = ed + batch;
+    bqp_lbmpc_data Dd = *D;
+    Dd.A = in[0].dst; Dd.B = in[1].dst; Dd.K = in[2].dst; Dd.Lq = in[3].dst; Dd.Lr = in[4].dst;
+    Dd.Lp = in[5].dst; Dd.Lt = in[6].dst; Dd.LAMBDA = in[7].dst; Dd.PSI = in[8].dst;
+    Dd.xs = in[9].dst; Dd.data = in[10].dst; Dd.x0 = in[11].dst; Dd.Ain = in[12].dst;
+    Dd.bin = in[13].dst;
+    rc = bqp_lbmpc_solve_batched_device(h, d, batch, &Dd, opt, zd, ld, cd, ed, itd, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(z, zd, sizeof(double) * batch * n, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(exitflag, ed, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(iterations, itd, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    if (lam && m) HIP_TRY(hipMemcpyAsync(lam, ld, sizeof(double) * nlam, hipMemcpyDeviceToHost, h->stream));
+    if (cost) HIP_TRY(hipMemcpyAsync(cost, cd, sizeof(double) * batch, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return BQP_OK;
 }

@@ -49,4 +49,31 @@ struct DenseKernelArgs {
 int dense_work_doubles(int n, int m, int me);
 hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st);
 
+// Learning-based MPC (Gauss-Newton SQP on the NW-learned model), bqp_lbmpc.hip.  Small
+// matrices column-major (A nx*nx, B nx*nu, K nu*nx, LAMBDA nx*np, PSI nu*np); weight factors
+// upper-triangular row-major (Lq nx*nx, Lr nu*nu, Lp, Lt nx*nx); NW window 7 x q column-major.
+struct LbmpcArgs {
+    int N, n, nr, m, q, n_run, term_learned, batch, ntrial, max_iter;
+    double hinv2, lam_nw, tol_step, tol_stat;
+    const double *A, *B, *K, *Lq, *Lr, *Lp, *Lt, *LAM, *PSI, *xs;
+    const double* data; int64_t sdata;
+    const double* x0; int64_t sx0;
+    const double* Ain;                  // m x n column-major, shared
+    const double* bin; int64_t sbin;    // m per instance
+    double* z;                          // batch x n iterate (in: start, out: solution)
+    double* d;                          // batch x n QP step
+    double* lam;                        // batch x m QP multipliers
+    double *Jr, *er;                    // batch x nr x n (row-major), batch x nr
+    double *H, *f, *bsh;                // batch x n x n (column-major), batch x n, batch x m
+    double *cost0, *costT, *stat, *cprev;  // batch, batch x ntrial, batch, batch
+    int *qpflag, *flag, *done, *iters, *ndone;
+};
+
+hipError_t launch_nw_oracle(int batch, int q, const double* data, int64_t sdata, const double* xi,
+                            double* g, double* dg, double bw, double lam, hipStream_t st);
+bool lbmpc_supported(int nx, int nu, int np, int n, int q);
+hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st);
+hipError_t launch_lbmpc_normal(const LbmpcArgs& a, hipStream_t st);
+hipError_t launch_lbmpc_update(const LbmpcArgs& a, hipStream_t st);
+
 }  // namespace bqp

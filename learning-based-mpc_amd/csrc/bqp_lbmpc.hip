@@ -1,0 +1,425 @@
+// bqp_lbmpc.hip — learning-based MPC on gfx950: the batched Nadaraya-Watson oracle and the
+// device side of the Gauss-Newton SQP that solves the reference's LBMPC problems (forms F3/F4).
+//
+// Reference: functions/oracleL2NW.m:26-36 / examples/hybrid_LBMPC_casadi.m:331-358 (the NW
+// oracle), models/learnedModel.m:25 (x+ = A x + B u + g), functions/costLBMPC.m:20-45 and
+// constraintsLBMPC.m:18-45 (F3), examples/hybrid_LBMPC_casadi.m:250-311 (F4).  The algorithm
+// is stated in oracle/lbmpc.py; the host loop is bqp_lbmpc_solve_batched_device (bqp_lbmpc_api.cpp).
+//
+// Kernels (one SQP iteration = rollout(GN) -> normal -> dense QP -> rollout(trials) -> update):
+//   nw_oracle_kernel      one wave per query point: g(xi), dg/dxi; lanes over the data window
+//   lbmpc_rollout_kernel  one wave per (instance, trial): the learned rollout u = K x + v,
+//                         x+ = A x + B u + g(x, u) (NW sums over the window held in LDS, lanes
+//                         over data points, DPP wave reductions), the nominal rollout, the
+//                         weighted residuals of the quadratic cost and - GN mode - the forward
+//                         sensitivities dx/dz (lanes over the columns of z) written as the rows
+//                         of the residual Jacobian Jr (row-major, coalesced along z)
+//   lbmpc_normal_kernel   one workgroup per instance: H = 2 Jr'Jr, f = 2 Jr'er through LDS row
+//                         tiles, and the QP right-hand side b_in - A_in z
+//   lbmpc_update_kernel   one wave per instance: convergence test (step, NLP stationarity
+//                         |f + A_in' lam|), Armijo choice among the trial step lengths, z += a d
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "bqp_internal.h"
+#include "bqp_wave.h"
+
+namespace bqp {
+
+#define LB_WAVE 64
+#define LB_MAXQ 512      // NW window capacity (data points) held in LDS
+#define LB_CPL 4         // z columns per lane in the sensitivity recursion (n <= 256)
+
+// NW sums at xi over the window in LDS (7 x q, column-major: point i at D[7 i .. 7 i + 6]).
+// Returns g (4) and, if JAC, dg (4 x 3, row-major); every lane ends with the uniform values.
+template <bool JAC>
+__device__ __forceinline__ void nw_eval(const double* D, int q, double hinv2, double lam,
+                                        const double (&xi)[3], double (&g)[4], double (&dg)[4][3],
+                                        int lane) {
+    double s = 0.0, sy[4] = {0, 0, 0, 0}, ds[3] = {0, 0, 0}, dsy[4][3] = {};
+    for (int i = lane; i < q; i += LB_WAVE) {
+        const double* p = D + 7 * i;
+        const double d0 = p[0] - xi[0], d1 = p[1] - xi[1], d2 = p[2] - xi[2];
+        const double k = exp(-(d0 * d0 + d1 * d1 + d2 * d2) * hinv2);
+        s += k;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sy[r] += p[3 + r] * k;
+        if (JAC) {
+            const double c = 2.0 * hinv2 * k;
+            const double dk[3] = {c * d0, c * d1, c * d2};
+#pragma unroll
+            for (int c3 = 0; c3 < 3; ++c3) {
+                ds[c3] += dk[c3];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dsy[r][c3] += p[3 + r] * dk[c3];
+            }
+        }
+    }
+    s = wsum(s);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sy[r] = wsum(sy[r]);
+    const double den = lam + s;
+    const double iden = 1.0 / den;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[r] = sy[r] * iden;
+    if (JAC) {
+#pragma unroll
+        for (int c3 = 0; c3 < 3; ++c3) {
+            ds[c3] = wsum(ds[c3]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dsy[r][c3] = wsum(dsy[r][c3]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c3 = 0; c3 < 3; ++c3) dg[r][c3] = (dsy[r][c3] - g[r] * ds[c3]) * iden;
+    }
+}
+
+__device__ __forceinline__ void load_window(double* D, const double* src, int q, int lane) {
+    for (int i = lane; i < 7 * q; i += LB_WAVE) D[i] = src[i];
+    wave_sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// standalone oracle: g, dg at a batch of query points (oracleL2NW.m)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) nw_oracle_kernel(int batch, int q, const double* data,
+                                                       int64_t sdata, const double* xi_in,
+                                                       double* g_out, double* dg_out,
+                                                       double hinv2, double lam) {
+    __shared__ double D[7 * LB_MAXQ];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (b >= batch) return;
+    load_window(D, data + (int64_t)b * sdata, q, lane);
+    double xi[3] = {xi_in[3 * b], xi_in[3 * b + 1], xi_in[3 * b + 2]};
+    double g[4], dg[4][3];
+    nw_eval<true>(D, q, hinv2, lam, xi, g, dg, lane);
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            g_out[4 * b + r] = g[r];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                if (dg_out) dg_out[12 * b + 3 * r + c] = dg[r][c];   // row-major 4 x 3
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// rollout: cost (all modes), residual Jacobian (GN mode)
+// ------------------------------------------------------------------------------------------
+template <int NX, int NU, int NP>
+__global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) {
+    static_assert(NX >= 2 && NU == 1, "NW input xi = [x_1; x_2; u] needs nx >= 2, nu = 1");
+    __shared__ double D[7 * LB_MAXQ];
+    const int lane = threadIdx.x;
+    const int nt = gn ? 1 : a.ntrial;
+    const int b = blockIdx.x / nt, t = blockIdx.x % nt;
+    if (b >= a.batch || a.done[b]) return;
+    const int N = a.N, n = a.n, nr = a.nr;
+    load_window(D, a.data + (int64_t)b * a.sdata, a.q, lane);
+    const double alpha = gn ? 0.0 : ldexp(1.0, -t);
+    const double* z = a.z + (int64_t)b * n;
+    const double* dz = a.d + (int64_t)b * n;
+    auto zv = [&](int j) __attribute__((always_inline)) -> double {
+        return gn ? z[j] : z[j] + alpha * dz[j];
+    };
+    // column-major small matrices
+    auto Am = [&](int i, int j) __attribute__((always_inline)) { return a.A[j * NX + i]; };
+    auto Bm = [&](int i, int j) __attribute__((always_inline)) { return a.B[j * NX + i]; };
+    auto Km = [&](int i, int j) __attribute__((always_inline)) { return a.K[j * NU + i]; };
+    auto LAM = [&](int i, int j) __attribute__((always_inline)) { return a.LAM[j * NX + i]; };
+    auto PSI = [&](int i, int j) __attribute__((always_inline)) { return a.PSI[j * NU + i]; };
+    double th[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) th[p] = zv(N * NU + p);
+    double x[NX], xn[NX];
+    const double* x0 = a.x0 + (int64_t)b * a.sx0;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) { x[i] = x0[i]; xn[i] = x0[i]; }
+    // sensitivities of the learned (SL) and nominal (SN) states w.r.t. z, columns j = lane + 64 c
+    double SL[LB_CPL][NX], SN[LB_CPL][NX];
+#pragma unroll
+    for (int c = 0; c < LB_CPL; ++c)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) { SL[c][i] = 0.0; SN[c][i] = 0.0; }
+    double* Jr = gn ? a.Jr + (int64_t)b * nr * n : nullptr;
+    double* er = gn ? a.er + (int64_t)b * nr : nullptr;
+    double J = 0.0;
+    int row = 0;
+    // weighted residual block L (e) with L upper-triangular (row-major), e = v - M theta;
+    // GN: its Jacobian rows for the lane's columns from sensitivities S (d v / d z)
+    auto residual = [&](const double* Lw, int dim, const double* v, auto&& Mth, auto&& Scol) __attribute__((always_inline)) {
+        for (int r = 0; r < dim; ++r) {
+            double e = 0.0;
+            for (int c2 = r; c2 < dim; ++c2) {
+                double ec = v[c2];
+#pragma unroll
+                for (int p = 0; p < NP; ++p) ec -= Mth(c2, p) * th[p];
+                e += Lw[r * dim + c2] * ec;
+            }
+            J += e * e;
+            if (gn) {
+                if (lane == 0) er[row + r] = e;
+#pragma unroll
+                for (int c = 0; c < LB_CPL; ++c) {
+                    const int j = lane + LB_WAVE * c;
+                    if (j < n) {
+                        double acc = 0.0;
+                        for (int c2 = r; c2 < dim; ++c2) {
+                            double s = Scol(c, c2);
+                            if (j >= N * NU) s -= Mth(c2, j - N * NU);
+                            acc += Lw[r * dim + c2] * s;
+                        }
+                        Jr[(int64_t)(row + r) * n + j] = acc;
+                    }
+                }
+            }
+        }
+        row += dim;
+    };
+    for (int k = 0; k < N; ++k) {
+        const double vk = zv(k);
+        double u = vk, un = vk;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) { u += Km(0, i) * x[i]; un += Km(0, i) * xn[i]; }
+        // input sensitivities U = K S + e_k
+        double UL[LB_CPL], UN[LB_CPL];
+        if (gn) {
+#pragma unroll
+            for (int c = 0; c < LB_CPL; ++c) {
+                const int j = lane + LB_WAVE * c;
+                double ul = (j == k) ? 1.0 : 0.0, unn = ul;
+#pragma unroll
+                for (int i = 0; i < NX; ++i) { ul += Km(0, i) * SL[c][i]; unn += Km(0, i) * SN[c][i]; }
+                UL[c] = ul; UN[c] = unn;
+            }
+        }
+        if (k < a.n_run) {
+            residual(a.Lq, NX, x, LAM, [&](int c, int i) { return SL[c][i]; });
+            residual(a.Lr, NU, &u, PSI, [&](int c, int i) { return UL[c]; });
+        }
+        // learned step
+        const double xi[3] = {x[0], x[1], u};
+        double g[4], dg[4][3];
+        if (gn) nw_eval<true>(D, a.q, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        else nw_eval<false>(D, a.q, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        double x1[NX], xn1[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double v = Bm(i, 0) * u + (i < 4 ? g[i] : 0.0);
+            double w = Bm(i, 0) * un;
+#pragma unroll
+            for (int c2 = 0; c2 < NX; ++c2) { v += Am(i, c2) * x[c2]; w += Am(i, c2) * xn[c2]; }
+            x1[i] = v; xn1[i] = w;
+        }
+        if (gn) {
+#pragma unroll
+            for (int c = 0; c < LB_CPL; ++c) {
+                double sl[NX], sn[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) {
+                    double gx0 = i < 4 ? dg[i][0] : 0.0, gx1 = i < 4 ? dg[i][1] : 0.0, gu = i < 4 ? dg[i][2] : 0.0;
+                    double v = (Bm(i, 0) + gu) * UL[c] + gx0 * SL[c][0] + gx1 * SL[c][1];
+                    double w = Bm(i, 0) * UN[c];
+#pragma unroll
+                    for (int c2 = 0; c2 < NX; ++c2) { v += Am(i, c2) * SL[c][c2]; w += Am(i, c2) * SN[c][c2]; }
+                    sl[i] = v; sn[i] = w;
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) { SL[c][i] = sl[i]; SN[c][i] = sn[i]; }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) { x[i] = x1[i]; xn[i] = xn1[i]; }
+    }
+    // terminal P on x_N (learned or nominal), T on (LAMBDA theta - xs)
+    if (a.term_learned)
+        residual(a.Lp, NX, x, LAM, [&](int c, int i) { return SL[c][i]; });
+    else
+        residual(a.Lp, NX, xn, LAM, [&](int c, int i) { return SN[c][i]; });
+    {
+        // rows Lt (LAMBDA theta - xs): written as L (v - M theta) with v = -xs, M = -LAMBDA
+        double mxs[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) mxs[i] = -a.xs[i];
+        auto mLAM = [&](int i, int p) { return -LAM(i, p); };
+        residual(a.Lt, NX, mxs, mLAM, [&](int c, int i) { return 0.0; });
+    }
+    if (lane == 0) {
+        if (gn) a.cost0[b] = J;
+        else a.costT[(int64_t)b * nt + t] = J;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// normal equations H = 2 Jr'Jr, f = 2 Jr'er (column-major H), QP rhs b_in - A_in z
+// ------------------------------------------------------------------------------------------
+#define LB_RC 16         // Jr rows per LDS tile
+#define LB_MAXN 128      // n <= 128 for the normal kernel (8 x 8 accumulators per thread)
+__global__ void __launch_bounds__(256) lbmpc_normal_kernel(LbmpcArgs a) {
+    __shared__ double T[LB_RC * LB_MAXN];
+    __shared__ double E[LB_RC];
+    const int b = blockIdx.x;
+    if (b >= a.batch || a.done[b]) return;
+    const int n = a.n, nr = a.nr, tid = threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+    const double* Jr = a.Jr + (int64_t)b * nr * n;
+    const double* er = a.er + (int64_t)b * nr;
+    double acc[8][8], fa = 0.0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] = 0.0;
+    for (int r0 = 0; r0 < nr; r0 += LB_RC) {
+        const int rc = min(LB_RC, nr - r0);
+        __syncthreads();
+        for (int i = tid; i < rc * n; i += 256) T[(i / n) * LB_MAXN + (i % n)] = Jr[(int64_t)r0 * n + i];
+        if (tid < rc) E[tid] = er[r0 + tid];
+        __syncthreads();
+        for (int r = 0; r < rc; ++r) {
+            const double* Tr = T + r * LB_MAXN;
+            double cj[8];
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2) cj[q2] = (tx + 16 * q2 < n) ? Tr[tx + 16 * q2] : 0.0;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int i = ty + 16 * p;
+                const double ci = (i < n) ? Tr[i] : 0.0;
+#pragma unroll
+                for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] += ci * cj[q2];
+            }
+            if (tid < n) fa += Tr[tid] * E[r];
+        }
+    }
+    double* H = a.H + (int64_t)b * n * n;
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int q2 = 0; q2 < 8; ++q2) {
+            const int i = ty + 16 * p, j = tx + 16 * q2;
+            if (i < n && j < n) H[(int64_t)j * n + i] = 2.0 * acc[p][q2];
+        }
+    if (tid < n) a.f[(int64_t)b * n + tid] = 2.0 * fa;
+    // b_in - A_in z (A_in column-major m x n, shared)
+    const double* z = a.z + (int64_t)b * n;
+    const double* bin = a.bin + (int64_t)b * a.sbin;
+    for (int r = tid; r < a.m; r += 256) {
+        double v = bin[r];
+        for (int j = 0; j < n; ++j) v -= a.Ain[(int64_t)j * a.m + r] * z[j];
+        a.bsh[(int64_t)b * a.m + r] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// convergence test + Armijo line search + step (one wave per instance)
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) lbmpc_update_kernel(LbmpcArgs a) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (b >= a.batch || a.done[b]) return;
+    const int n = a.n, m = a.m;
+    double* z = a.z + (int64_t)b * n;
+    const double* d = a.d + (int64_t)b * n;
+    const double* f = a.f + (int64_t)b * n;
+    const double* lam = a.lam + (int64_t)b * m;
+    const double* bsh = a.bsh + (int64_t)b * m;
+    const int qflag = a.qpflag[b];
+    // NLP stationarity |f + A_in' lam|, norms, slope f'd, start feasibility
+    double st = 0.0, fn = 0.0, dn = 0.0, zn = 0.0, sl = 0.0, viol = 0.0;
+    for (int j = lane; j < n; j += LB_WAVE) {
+        double g = f[j];
+        for (int r = 0; r < m; ++r) g += a.Ain[(int64_t)j * m + r] * lam[r];
+        st = fmax(st, fabs(g));
+        fn = fmax(fn, fabs(f[j]));
+        dn = fmax(dn, fabs(d[j]));
+        zn = fmax(zn, fabs(z[j]));
+        sl += f[j] * d[j];
+    }
+    for (int r = lane; r < m; r += LB_WAVE) viol = fmax(viol, -bsh[r]);
+    st = wmax(st); fn = wmax(fn); dn = wmax(dn); zn = wmax(zn); sl = wsum(sl); viol = wmax(viol);
+    const bool feas0 = viol <= 1e-9;
+    int it = a.iters[b];
+    int flag = 0;
+    bool fin = false;
+    // a QP that stopped on its iteration limit or numerically (-8) still returns its last
+    // interior iterate; near the SQP solution (d -> 0, multipliers of the active rows large,
+    // slacks -> 0) that is the usual way the sub-problem ends, and the step is used as is
+    const bool qp_ok = qflag == 1 || ((qflag == 0 || qflag == -8) && isfinite(dn) && isfinite(st));
+    if (qflag == -2 || !qp_ok) {
+        flag = (qflag == -2) ? -2 : -8;   // QP sub-problem infeasible / failed
+        fin = true;
+    } else if (feas0 && ((qflag == 1 && dn <= a.tol_step * (1.0 + zn) && st <= a.tol_stat * (1.0 + fn)) ||
+                         (it > 0 && dn <= 1e-6 * (1.0 + zn) &&
+                          (qflag != 1 ||
+                           fabs(a.cprev[b] - a.cost0[b]) <= 1e-12 * (1.0 + fabs(a.cost0[b])))))) {
+        // converged: KKT test, or the step has reached the accuracy of the interior-point QP
+        // solve (|d| <= 1e-6) and the cost no longer changes (stagnation at round-off) or the
+        // QP cannot resolve a smaller step
+        flag = 1;
+        fin = true;
+    }
+    if (!fin) {
+        const double J0 = a.cost0[b];
+        int tsel = a.ntrial - 1;
+        if (feas0) {
+            for (int t = 0; t < a.ntrial; ++t) {
+                const double al = ldexp(1.0, -t);
+                if (a.costT[(int64_t)b * a.ntrial + t] <= J0 + 1e-4 * al * sl) { tsel = t; break; }
+            }
+        } else {
+            tsel = 0;                     // infeasible start: full step to the linearised-feasible point
+        }
+        const double al = ldexp(1.0, -tsel);
+        for (int j = lane; j < n; j += LB_WAVE) z[j] += al * d[j];
+        if (lane == 0) a.cprev[b] = J0;
+        ++it;
+        if (it >= a.max_iter) { flag = 0; fin = true; }
+    }
+    if (lane == 0) {
+        a.iters[b] = it;
+        a.stat[b] = st;
+        if (fin) {
+            a.flag[b] = flag;
+            a.done[b] = 1;
+            atomicAdd(a.ndone, 1);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// launch helpers
+// ------------------------------------------------------------------------------------------
+hipError_t launch_nw_oracle(int batch, int q, const double* data, int64_t sdata, const double* xi,
+                            double* g, double* dg, double bw, double lam, hipStream_t st) {
+    if (q < 1 || q > LB_MAXQ) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nw_oracle_kernel, dim3(batch), dim3(64), 0, st, batch, q, data, sdata, xi,
+                       g, dg, 1.0 / (bw * bw), lam);
+    return hipGetLastError();
+}
+
+bool lbmpc_supported(int nx, int nu, int np, int n, int q) {
+    return nx == 4 && nu == 1 && np == 1 && n <= LB_MAXN && n <= LB_WAVE * LB_CPL && q >= 1 &&
+           q <= LB_MAXQ;
+}
+
+hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st) {
+    const int grid = a.batch * (gn ? 1 : a.ntrial);
+    hipLaunchKernelGGL((lbmpc_rollout_kernel<4, 1, 1>), dim3(grid), dim3(64), 0, st, a, gn);
+    return hipGetLastError();
+}
+
+hipError_t launch_lbmpc_normal(const LbmpcArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(lbmpc_normal_kernel, dim3(a.batch), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_lbmpc_update(const LbmpcArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(lbmpc_update_kernel, dim3(a.batch), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace bqp

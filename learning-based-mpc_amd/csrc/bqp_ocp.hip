@@ -28,66 +28,13 @@
 #include <stdint.h>
 
 #include "bqp_internal.h"
+#include "bqp_wave.h"
 
 namespace bqp {
 
 #define WAVE 64
 #define PIV_FLOOR 1e-14
 #define MU_BLOWUP 1e6
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Wave-wide reductions on DPP lane moves (quad_perm xor1/xor2, row_half_mirror, row_mirror
-// inside each 16-lane row, then row_bcast15/31 across rows) + a readlane of lane 63: no LDS
-// traffic, result uniform in every lane.  EXEC must be full (all call sites are wave-uniform).
-template <int CTRL, int ROWM>
-__device__ __forceinline__ double dpp_mov(double old, double v) {
-    const int2 o = __builtin_bit_cast(int2, old);
-    const int2 x = __builtin_bit_cast(int2, v);
-    int2 r;
-    r.x = __builtin_amdgcn_update_dpp(o.x, x.x, CTRL, ROWM, 0xf, false);
-    r.y = __builtin_amdgcn_update_dpp(o.y, x.y, CTRL, ROWM, 0xf, false);
-    return __builtin_bit_cast(double, r);
-}
-__device__ __forceinline__ double lane63(double v) {
-    const int2 x = __builtin_bit_cast(int2, v);
-    int2 r;
-    r.x = __builtin_amdgcn_readlane(x.x, 63);
-    r.y = __builtin_amdgcn_readlane(x.y, 63);
-    return __builtin_bit_cast(double, r);
-}
-__device__ __forceinline__ double wsum(double v) {
-    v += dpp_mov<0xB1, 0xf>(0.0, v);
-    v += dpp_mov<0x4E, 0xf>(0.0, v);
-    v += dpp_mov<0x141, 0xf>(0.0, v);
-    v += dpp_mov<0x140, 0xf>(0.0, v);
-    v += dpp_mov<0x142, 0xa>(0.0, v);
-    v += dpp_mov<0x143, 0xc>(0.0, v);
-    return lane63(v);
-}
-__device__ __forceinline__ double wmax(double v) {
-    v = fmax(v, dpp_mov<0xB1, 0xf>(-INFINITY, v));
-    v = fmax(v, dpp_mov<0x4E, 0xf>(-INFINITY, v));
-    v = fmax(v, dpp_mov<0x141, 0xf>(-INFINITY, v));
-    v = fmax(v, dpp_mov<0x140, 0xf>(-INFINITY, v));
-    v = fmax(v, dpp_mov<0x142, 0xa>(-INFINITY, v));
-    v = fmax(v, dpp_mov<0x143, 0xc>(-INFINITY, v));
-    return lane63(v);
-}
-__device__ __forceinline__ double wmin(double v) { return -wmax(-v); }
-// value of lane `src` broadcast to the wave (scalar register pair): the sequential Riccati
-// sweeps pass their NS-vector from stage to stage this way instead of through LDS
-__device__ __forceinline__ double rl(double v, int src) {
-    const int2 x = __builtin_bit_cast(int2, v);
-    int2 r;
-    r.x = __builtin_amdgcn_readlane(x.x, src);
-    r.y = __builtin_amdgcn_readlane(x.y, src);
-    return __builtin_bit_cast(double, r);
-}
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
 // 1/t for the row slacks and multipliers (t > 0 inside the IPM): hardware reciprocal estimate

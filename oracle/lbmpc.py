@@ -1,0 +1,233 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Restatement of the learning-based MPC problems (forms F3/F4) and of the
+algorithm the GPU path uses for them: a Gauss-Newton SQP whose QP sub-problems go through the
+batched dense solver.  numpy, one instance at a time - the checker for the HIP path.
+
+Reference anchors
+-----------------
+* Nadaraya-Watson oracle: ``functions/oracleL2NW.m:26-36`` (struct data X 3xn, Y 4xn) and
+  ``examples/hybrid_LBMPC_casadi.m:331-358`` (7xq matrix data, no validity mask: zero columns
+  enter the normaliser).  g(xi) = sum_i Y_i k_i / (lambda + sum_j k_j),
+  k_i = exp(-|X_i - xi|^2 / h^2), h = 0.5, lambda = 1e-3, xi = [x_1; x_2; u].
+* learned model ``models/learnedModel.m:25``: x+ = A x + B u + g(x, u).
+* F3 (fmincon LBMPC): ``functions/costLBMPC.m:20-45`` (rollout u = K x + c on the LEARNED
+  model; running cost for k < N-1 on (x_{k-1}, u_{k-1}); terminal P, T on x_N),
+  ``functions/constraintsLBMPC.m:18-45`` (NOMINAL model; at k = 1 F_x_d x_1 <= h_x_d and
+  F_w_N [x_1; theta] <= h_w_N; F_x x_k <= h_x, F_u u_{k-1} <= h_u for k = 1..N-1).
+* F4 (hybrid LBMPC, CasADi/IPOPT): ``examples/hybrid_LBMPC_casadi.m:250-311`` (running cost
+  delta * (...) on the learned rollout from x_0 for k = 0..N-1, terminal cost on the NOMINAL
+  decision x_N, nominal dynamics as equalities, the same stage-1 sets, boxes for k = 1..N).
+  Golden instance: ``examples/DSS_NMPC.m`` (IPOPT optimum y_OL, :1147; tests/golden/
+  lbmpc_instance.npz).
+
+Algorithm (shared with the HIP path, bqp/lbmpc.py + csrc/bqp_lbmpc.hip)
+----------------------------------------------------------------------
+Decision z = [v_0..v_{N-1}; theta] (v = c for F3, v = u - u_eq for F4), deviation coordinates.
+Nominal states/inputs are affine in z (exact condensing, constraints A_in z <= b_in).  At the
+iterate z: learned rollout + forward sensitivities S_k = dx^L_k/dz, U_k = du^L_k/dz;
+GN model H = 2 sum J'WJ, f = 2 sum J'W e of the quadratic cost in the residuals e; QP
+min 0.5 d'Hd + f'd s.t. A_in (z + d) <= b_in; Armijo backtracking on the true cost over the
+trial steps alpha = 2^-j (j = 0..7), sufficient-decrease 1e-4; stop when |d|_inf <= tol_step
+(1 + |z|_inf) and the NLP stationarity |grad J + A_in' lam|_inf <= tol_stat (1 + |grad J|_inf).
+"""
+import numpy as np
+
+from . import dense_qp
+
+H_BW = 0.5
+LAM_NW = 1e-3
+
+
+def nw(xi, data):
+    """g (4,), dg/dxi (4, 3) of the NW oracle at xi (3,); data 7 x q."""
+    X, Y = data[:3], data[3:]
+    d = X - xi[:, None]                                  # (3, q)
+    k = np.exp(-(d * d).sum(0) / H_BW ** 2)              # (q,)
+    s = k.sum()
+    den = LAM_NW + s
+    sy = Y @ k                                           # (4,)
+    g = sy / den
+    # dk_i/dxi = k_i * 2 (X_i - xi) / h^2
+    dk = (k[None, :] * d) * (2.0 / H_BW ** 2)            # (3, q)
+    dsy = Y @ dk.T                                       # (4, 3)
+    ds = dk.sum(1)                                       # (3,)
+    dg = dsy / den - np.outer(sy, ds) / den ** 2
+    return g, dg
+
+
+def rollout(p, x0, z, learned=True, jac=False):
+    """x (N+1, nx), u (N, nu) of the (learned or nominal) closed rollout u_k = K x_k + v_k, and
+    optionally the sensitivities S (N+1, nx, n), U (N, nu, n) w.r.t. z."""
+    N, nx, nu = p['N'], p['nx'], p['nu']
+    n = N * nu + p['np']
+    A, B, K = p['A'], p['B'], p['K']
+    v = z[:N * nu].reshape(N, nu)
+    x = np.zeros((N + 1, nx)); u = np.zeros((N, nu))
+    x[0] = x0
+    S = np.zeros((N + 1, nx, n)); U = np.zeros((N, nu, n))
+    for k in range(N):
+        u[k] = K @ x[k] + v[k]
+        Ak, Bk = A, B
+        xn = A @ x[k] + B @ u[k]
+        if learned:
+            g, dg = nw(np.concatenate([x[k][:2], u[k]]), p['data'])
+            xn = xn + g
+            Gx = np.zeros((nx, nx)); Gx[:, :2] = dg[:, :2]
+            Ak, Bk = A + Gx, B + dg[:, 2:2 + nu]
+        x[k + 1] = xn
+        if jac:
+            U[k] = K @ S[k]
+            U[k][:, k * nu:(k + 1) * nu] += np.eye(nu)
+            S[k + 1] = Ak @ S[k] + Bk @ U[k]
+    return (x, u, S, U) if jac else (x, u)
+
+
+def _theta(p, z):
+    return z[p['N'] * p['nu']:]
+
+
+def cost(p, x0, z):
+    xL, uL = rollout(p, x0, z, learned=True)
+    th = _theta(p, z)
+    LAM, PSI, Q, R = p['LAMBDA'], p['PSI'], p['Q'], p['R']
+    J = 0.0
+    for k in range(p['n_run']):
+        ex = xL[k] - LAM @ th
+        eu = uL[k] - PSI @ th
+        J += p['w_run'] * (ex @ Q @ ex + eu @ R @ eu)
+    xT = xL[p['N']] if p['term_learned'] else rollout(p, x0, z, learned=False)[0][p['N']]
+    eT = xT - LAM @ th
+    es = LAM @ th - p['xs']
+    return J + eT @ p['P'] @ eT + es @ p['T'] @ es
+
+
+def gn_model(p, x0, z):
+    """GN Hessian H, exact gradient f of the cost at z."""
+    N, nu, npar = p['N'], p['nu'], p['np']
+    n = N * nu + npar
+    LAM, PSI, Q, R = p['LAMBDA'], p['PSI'], p['Q'], p['R']
+    xL, uL, S, U = rollout(p, x0, z, learned=True, jac=True)
+    th = _theta(p, z)
+    Et = np.zeros((npar, n)); Et[:, N * nu:] = np.eye(npar)
+    H = np.zeros((n, n)); f = np.zeros(n)
+    w = p['w_run']
+    for k in range(p['n_run']):
+        Jx = S[k] - LAM @ Et
+        Ju = U[k] - PSI @ Et
+        ex = xL[k] - LAM @ th
+        eu = uL[k] - PSI @ th
+        H += 2 * w * (Jx.T @ Q @ Jx + Ju.T @ R @ Ju)
+        f += 2 * w * (Jx.T @ Q @ ex + Ju.T @ R @ eu)
+    if p['term_learned']:
+        xT, ST = xL[N], S[N]
+    else:
+        xn, _, Sn, _ = rollout(p, x0, z, learned=False, jac=True)
+        xT, ST = xn[N], Sn[N]
+    JT = ST - LAM @ Et
+    eT = xT - LAM @ th
+    H += 2 * (JT.T @ p['P'] @ JT)
+    f += 2 * (JT.T @ p['P'] @ eT)
+    Js = LAM @ Et
+    es = LAM @ th - p['xs']
+    H += 2 * (Js.T @ p['T'] @ Js)
+    f += 2 * (Js.T @ p['T'] @ es)
+    return H, f
+
+
+def constraints(p, x0):
+    """A_in z <= b_in from the nominal rollout (exact: affine in z)."""
+    N, nu, npar = p['N'], p['nu'], p['np']
+    n = N * nu + npar
+    z0 = np.zeros(n)
+    x, u, S, U = rollout(p, x0, z0, learned=False, jac=True)
+    Et = np.zeros((npar, n)); Et[:, N * nu:] = np.eye(npar)
+    rows, rhs = [], []
+    # stage 1 sets (constraintsLBMPC.m:26-30, hybrid_LBMPC_casadi.m:296-300)
+    rows.append(p['F_x_d'] @ S[1]); rhs.append(p['h_x_d'] - p['F_x_d'] @ x[1])
+    FT = p['F_T']
+    nxT = p['nx']
+    rows.append(FT[:, :nxT] @ S[1] + FT[:, nxT:] @ Et)
+    rhs.append(p['h_T'] - FT[:, :nxT] @ x[1])
+    for k in range(1, p['n_box'] + 1):
+        rows.append(p['F_x'] @ S[k]); rhs.append(p['h_x'] - p['F_x'] @ x[k])
+        rows.append(p['F_u'] @ U[k - 1]); rhs.append(p['h_u'] - p['F_u'] @ u[k - 1])
+    return np.vstack(rows), np.concatenate(rhs)
+
+
+def sqp(p, x0, z0=None, max_iter=100, tol_step=1e-10, tol_stat=1e-9, trace=None):
+    """Gauss-Newton SQP with parallel-trial Armijo line search (see module doc).
+    Returns z, lam_in, info."""
+    N, nu, npar = p['N'], p['nu'], p['np']
+    n = N * nu + npar
+    Ain, bin_ = constraints(p, x0)
+    z = np.zeros(n) if z0 is None else np.array(z0, float)
+    if np.any(Ain @ z > bin_ + 1e-12):
+        # feasible start: the QP's own solution with the model at z (first iterate)
+        pass
+    lam = np.zeros(Ain.shape[0])
+    J = cost(p, x0, z)
+    it = 0
+    stat = np.inf
+    for it in range(1, max_iter + 1):
+        H, f = gn_model(p, x0, z)
+        qp = dict(H=H, f=f, A=Ain, b=bin_ - Ain @ z, Aeq=np.zeros((0, n)), beq=np.zeros(0),
+                  lb=np.full(n, -np.inf), ub=np.full(n, np.inf))
+        d, _, lamq, info = dense_qp.solve(qp)
+        lam = lamq['ineqlin']
+        stat = np.abs(f + Ain.T @ lam).max()
+        feas_start = np.all(Ain @ z <= bin_ + 1e-9)
+        if trace is not None:
+            trace.append(dict(it=it, J=J, step=np.abs(d).max(), stat=stat))
+        if feas_start and np.abs(d).max() <= tol_step * (1 + np.abs(z).max()) and \
+                stat <= tol_stat * (1 + np.abs(f).max()):
+            break
+        slope = f @ d
+        acc = False
+        for j in range(8):
+            a = 0.5 ** j
+            Jt = cost(p, x0, z + a * d)
+            if not feas_start or Jt <= J + 1e-4 * a * slope:
+                z = z + a * d
+                J = Jt
+                acc = True
+                break
+        if not acc:
+            z = z + 0.5 ** 7 * d
+            J = cost(p, x0, z)
+    return z, lam, dict(iterations=it, cost=J, stat=stat)
+
+
+# ----------------------------------------------------------------------------------------
+# problem builders
+# ----------------------------------------------------------------------------------------
+def _common(mg, N, data, F_T, h_T, F_x_d, h_x_d):
+    return dict(nx=4, nu=1, np=1, N=N, A=mg['A'], B=mg['B'].reshape(4, 1),
+                Q=mg['Q'], R=np.atleast_2d(mg['R']), P=mg['P'],
+                T=float(mg['Tscalar']) * np.eye(4), LAMBDA=mg['LAMBDA'].reshape(4, 1),
+                PSI=np.atleast_2d(mg['PSI']).reshape(1, 1), xs=np.zeros(4),
+                F_x=mg['F_x'], h_x=mg['h_x'], F_u=mg['F_u'], h_u=mg['h_u'],
+                F_T=np.asarray(F_T, float), h_T=np.asarray(h_T, float).ravel(),
+                F_x_d=np.asarray(F_x_d, float), h_x_d=np.asarray(h_x_d, float).ravel(),
+                data=np.asarray(data, float))
+
+
+def f3_problem(mg, N, data, F_T, h_T, F_x_d, h_x_d):
+    """fmincon LBMPC (costLBMPC.m / constraintsLBMPC.m), decision [c; theta]."""
+    p = _common(mg, N, data, F_T, h_T, F_x_d, h_x_d)
+    p.update(K=np.asarray(mg['K'], float).reshape(1, 4), w_run=1.0, n_run=max(N - 2, 0),
+             term_learned=True, n_box=N - 1)
+    return p
+
+
+def f4_problem(mg, N, data, F_T, h_T, F_x_d, h_x_d, delta=0.01):
+    """hybrid LBMPC (hybrid_LBMPC_casadi.m:250-311), decision [u - u_eq; theta]."""
+    p = _common(mg, N, data, F_T, h_T, F_x_d, h_x_d)
+    p.update(K=np.zeros((1, 4)), w_run=delta, n_run=N, term_learned=False, n_box=N)
+    return p
+
+
+def f4_to_y(p, x0, z, x_eq, u_eq):
+    """y_OL layout of hybrid_LBMPC_casadi.m (absolute [x_0..x_N; u; theta])."""
+    x, u = rollout(p, x0, z, learned=False)
+    return np.concatenate([(x + x_eq).ravel(), (u + u_eq).ravel(), _theta(p, z)])

@@ -221,6 +221,34 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
                                    double* lam, double* cost, int* exitflag, int* iterations,
                                    void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Closed-loop simulation: per time step, the batched structured solve at
+ * the measured states, then one step of the true plant with the first input - the loop of
+ * DMS_tracking_LMPC_casadi.m:153-189 / DSS_tracking_LMPC_casadi.m (solver(...), then
+ * xmeasure = dynamic(delta, xmeasure, u_OL(1:m))) for a whole batch of initial states.
+ * The OCP is posed in deviation coordinates around (x_eq, u_eq); data->x0 is ignored (the
+ * measured states are fed back).  x_init (batch*nx), X (batch*(steps+1)*nx) and
+ * U (batch*steps*nu) are absolute; exitflag (batch*steps, may be NULL) per solve.
+ * Plant BQP_PLANT_MG_RK4: Moore-Greitzer `system` (:215-221) under one RK4 step of length
+ * delta (`dynamic`, :297-304); nx = 4, nu = 1.
+ * ---------------------------------------------------------------------------------------- */
+#define BQP_PLANT_MG_RK4 1
+typedef struct {
+    int plant;           /* BQP_PLANT_MG_RK4 */
+    int steps;           /* closed-loop steps (mpciterations) */
+    double delta;        /* plant step (s) */
+    const double* x_eq;  /* nx working point (device memory in the _device variant) */
+    const double* u_eq;  /* nu */
+} bqp_closed_loop;
+
+int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* data,
+                        const bqp_options* opt, const bqp_closed_loop* cl, const double* x_init,
+                        double* X, double* U, int* exitflag);
+int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
+                               const bqp_ocp_data* data, const bqp_options* opt,
+                               const bqp_closed_loop* cl, const double* x_init, double* X,
+                               double* U, int* exitflag, void* stream);
+
 /* Timing of the most recent solve on this handle: kernel time measured with hipEvents on the
  * launch stream (ms), and the number of kernel launches it covered. */
 int bqp_last_kernel_ms(bqp_handle h, double* ms, int* launches);

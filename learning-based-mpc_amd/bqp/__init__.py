@@ -9,5 +9,6 @@ from .ocp import OcpProblem, solve_ocp  # noqa: F401
 from .mpc import LMPC, TrackingLMPC, TrackingMPC  # noqa: F401
 from .quadprog import quadprog  # noqa: F401
 from .lbmpc import LBMPC, HybridLBMPC, nw_oracle  # noqa: F401
+from .loop import closed_loop  # noqa: F401
 
 __version__ = '0.1.0'

@@ -65,7 +65,8 @@ class LbmpcData(C.Structure):
 EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version',
            'bqp_solve_ocp_batched', 'bqp_solve_ocp_batched_device', 'bqp_quadprog_batched',
            'bqp_quadprog_batched_device', 'bqp_last_kernel_ms', 'bqp_nw_oracle',
-           'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device']
+           'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device',
+           'bqp_closed_loop_ocp', 'bqp_closed_loop_ocp_device']
 
 _lib = None
 
@@ -110,6 +111,11 @@ def load():
     lib.bqp_lbmpc_solve_batched_device.argtypes = [C.c_void_p, C.POINTER(LbmpcDims), C.c_int,
                                                    C.POINTER(LbmpcData), C.POINTER(Options), _PD,
                                                    _PD, _PD, _PI, _PI, C.c_void_p]
+    lib.bqp_closed_loop_ocp.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int, C.POINTER(OcpData),
+                                        C.POINTER(Options), C.c_void_p, _PD, _PD, _PD, _PI]
+    lib.bqp_closed_loop_ocp_device.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int,
+                                               C.POINTER(OcpData), C.POINTER(Options), C.c_void_p,
+                                               _PD, _PD, _PD, _PI, C.c_void_p]
     _lib = lib
     return lib
 

@@ -1,0 +1,43 @@
+"""Closed-loop simulation on the GPU (bqp_closed_loop_ocp): the MPC loop of the reference's
+tracking-LMPC examples - solve at the measured state, apply the first move to the true plant,
+repeat - for a whole batch of initial states at once.
+
+Reference: ``examples/DMS_tracking_LMPC_casadi.m:153-189`` / ``DSS_tracking_LMPC_casadi.m``
+(``solver(...)`` then ``xmeasure = dynamic(delta, xmeasure, u_OL(1:m))``), with the
+Moore-Greitzer plant ``system`` (:215-221) integrated by one RK4 step (``dynamic``, :297-304).
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .ocp import OcpResult, _default_handle, pack
+
+BQP_PLANT_MG_RK4 = 1
+
+
+class ClosedLoop(C.Structure):
+    _fields_ = [('plant', C.c_int), ('steps', C.c_int), ('delta', C.c_double),
+                ('x_eq', _lib._PD), ('u_eq', _lib._PD)]
+
+
+def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, **opts):
+    """mpc: a TrackingLMPC (deviation coordinates around mpc.x_eq, mpc.u_eq); x_init (batch, n)
+    absolute initial states.  Returns X (batch, steps+1, n), U (batch, steps, m) absolute, and
+    the per-step exit flags (batch, steps)."""
+    lib = _lib.load()
+    h = handle or _default_handle()
+    x_init = np.ascontiguousarray(np.atleast_2d(x_init), dtype=np.float64)
+    b = x_init.shape[0]
+    prob = mpc.prob
+    dims, data, batch, keep = pack(prob, x_init - mpc.x_eq)
+    xeq = np.ascontiguousarray(mpc.x_eq, dtype=np.float64)
+    ueq = np.ascontiguousarray(mpc.u_eq, dtype=np.float64)
+    cl = ClosedLoop(BQP_PLANT_MG_RK4, int(steps), float(delta), _lib.ptr(xeq), _lib.ptr(ueq))
+    X = np.zeros((b, steps + 1, prob.nx)); U = np.zeros((b, steps, prob.nu))
+    flags = np.zeros((b, steps), np.int32)
+    o = _lib.options(**opts)
+    rc = lib.bqp_closed_loop_ocp(h.value, C.byref(dims), b, C.byref(data), C.byref(o), C.byref(cl),
+                                 _lib.ptr(x_init), _lib.ptr(X), _lib.ptr(U), _lib.iptr(flags))
+    _lib.check(rc, 'bqp_closed_loop_ocp')
+    return OcpResult(X=X, U=U, exitflag=flags)

@@ -43,6 +43,7 @@ struct bqp_handle_s {
     DevBuf stage;  // staging of host-pointer calls
     DevBuf dwork;  // dense per-instance scratch
     DevBuf lwork;  // learning-based MPC (SQP) buffers
+    DevBuf cwork;  // closed-loop simulation buffers
     int last_batch = 0;
 };
 
@@ -138,6 +139,7 @@ int bqp_destroy(bqp_handle h) {
         h->stage.release();
         h->dwork.release();
         h->lwork.release();
+        h->cwork.release();
         if (h->ev0) hipEventDestroy(h->ev0);
         if (h->ev1) hipEventDestroy(h->ev1);
         if (h->stream) hipStreamDestroy(h->stream);
@@ -625,6 +627,112 @@ int bqp_lbmpc_solve_batched(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     HIP_TRY(hipMemcpyAsync(iterations, itd, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
     if (lam && m) HIP_TRY(hipMemcpyAsync(lam, ld, sizeof(double) * nlam, hipMemcpyDeviceToHost, h->stream));
     if (cost) HIP_TRY(hipMemcpyAsync(cost, cd, sizeof(double) * batch, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return BQP_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// closed-loop simulation: batched structured solve + true-plant step, per time step
+// ------------------------------------------------------------------------------------------
+int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
+                               const bqp_ocp_data* D, const bqp_options* opt,
+                               const bqp_closed_loop* cl, const double* x_init, double* X,
+                               double* U, int* exitflag, void* stream) {
+    if (!h || !cl || !x_init || !X || !U) return BQP_E_ARG;
+    int rc = ocp_check(d, batch, D);
+    if (rc) return rc;
+    if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
+        return BQP_E_ARG;
+    if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;   // the MG plant
+    DevScope ds(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
+    const size_t B = batch;
+    const size_t nd = B * nx + B * (N + 1) * nx + B * N * nu + B * np;
+    HIP_TRY(h->cwork.reserve(sizeof(double) * nd + sizeof(int) * B));
+    double* s = (double*)h->cwork.p;
+    double* xo = s + B * nx;
+    double* uo = xo + B * (N + 1) * nx;
+    double* th = uo + B * N * nu;
+    int* fl = (int*)(th + B * np);
+    HIP_TRY(bqp::launch_closed_loop_init(batch, nx, cl->steps, x_init, cl->x_eq, s, X, st));
+    bqp_ocp_data Dm = *D;
+    Dm.x0 = s;
+    Dm.sx0 = nx;
+    hipEvent_t e0 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventRecord(e0, st));
+    for (int t = 0; t < cl->steps; ++t) {
+        rc = bqp_solve_ocp_batched_device(h, d, batch, &Dm, opt, xo, uo, th, nullptr, fl, nullptr,
+                                          nullptr, stream);
+        if (rc) { hipEventDestroy(e0); return rc; }
+        HIP_TRY(bqp::launch_mg_plant(batch, N, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
+                                     s, X, U, exitflag, st));
+    }
+    // timing of the whole loop (solves + plant steps) on this stream
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    HIP_TRY(hipEventSynchronize(h->ev1));
+    std::swap(h->ev0, e0);
+    hipEventDestroy(e0);
+    h->timed = true;
+    h->launches = 3 * cl->steps;
+    return BQP_OK;
+}
+
+int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
+                        const bqp_options* opt, const bqp_closed_loop* cl, const double* x_init,
+                        double* X, double* U, int* exitflag) {
+    if (!h || !cl || !x_init || !X || !U) return BQP_E_ARG;
+    int rc = ocp_check(d, batch, D);
+    if (rc) return rc;
+    DevScope ds(h->device);
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N, mp = d->n_poly;
+    const int nv = nx + nu + np;
+    struct In { const double* src; size_t n; double* dst; };
+    In in[] = {
+        {D->A, span(batch, D->sA, (size_t)nx * nx), nullptr},
+        {D->B, span(batch, D->sB, (size_t)nx * nu), nullptr},
+        {D->c, D->c ? span(batch, D->sc, nx) : 0, nullptr},
+        {D->W, (size_t)(N + 1) * nv * nv, nullptr},
+        {D->w, D->w ? span(batch, D->sw, (size_t)(N + 1) * nv) : 0, nullptr},
+        {D->xlb, D->xlb ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},
+        {D->xub, D->xub ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},
+        {D->ulb, D->ulb ? span(batch, D->sub, (size_t)N * nu) : 0, nullptr},
+        {D->uub, D->uub ? span(batch, D->sub, (size_t)N * nu) : 0, nullptr},
+        {D->Fp, mp > 0 ? (size_t)mp * nv : 0, nullptr},
+        {D->hp, mp > 0 ? span(batch, D->shp, mp) : 0, nullptr},
+        {x_init, (size_t)batch * nx, nullptr},
+        {cl->x_eq, (size_t)nx, nullptr},
+        {cl->u_eq, (size_t)nu, nullptr},
+    };
+    const int nin = sizeof(in) / sizeof(in[0]);
+    const size_t nX = (size_t)batch * (cl->steps + 1) * nx, nU = (size_t)batch * cl->steps * nu;
+    size_t tot = nX + nU;
+    for (int i = 0; i < nin; ++i) tot += (in[i].src ? in[i].n : 0);
+    HIP_TRY(h->stage.reserve(sizeof(double) * tot + sizeof(int) * (size_t)batch * cl->steps));
+    double* cur = (double*)h->stage.p;
+    for (int i = 0; i < nin; ++i) {
+        if (!in[i].src || in[i].n == 0) continue;
+        in[i].dst = cur;
+        HIP_TRY(hipMemcpyAsync(cur, in[i].src, sizeof(double) * in[i].n, hipMemcpyHostToDevice, h->stream));
+        cur += in[i].n;
+    }
+    double* Xd = cur; cur += nX;
+    double* Ud = cur; cur += nU;
+    int* Fd = (int*)cur;
+    bqp_ocp_data Dd = *D;
+    Dd.A = in[0].dst; Dd.B = in[1].dst; Dd.c = in[2].dst; Dd.W = in[3].dst; Dd.w = in[4].dst;
+    Dd.xlb = in[5].dst; Dd.xub = in[6].dst; Dd.ulb = in[7].dst; Dd.uub = in[8].dst;
+    Dd.Fp = in[9].dst; Dd.hp = in[10].dst;
+    Dd.x0 = in[11].dst;   // placeholder (the loop feeds the measured states)
+    bqp_closed_loop cd = *cl;
+    cd.x_eq = in[12].dst; cd.u_eq = in[13].dst;
+    rc = bqp_closed_loop_ocp_device(h, d, batch, &Dd, opt, &cd, in[11].dst, Xd, Ud,
+                                    exitflag ? Fd : nullptr, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(X, Xd, sizeof(double) * nX, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(U, Ud, sizeof(double) * nU, hipMemcpyDeviceToHost, h->stream));
+    if (exitflag) HIP_TRY(hipMemcpyAsync(exitflag, Fd, sizeof(int) * (size_t)batch * cl->steps, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return BQP_OK;
 }

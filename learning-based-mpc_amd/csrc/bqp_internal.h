@@ -76,4 +76,11 @@ hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st);
 hipError_t launch_lbmpc_normal(const LbmpcArgs& a, hipStream_t st);
 hipError_t launch_lbmpc_update(const LbmpcArgs& a, hipStream_t st);
 
+// closed-loop simulation (bqp_plant.hip): Moore-Greitzer RK4 plant between batched solves
+hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* xinit,
+                                   const double* xeq, double* s, double* X, hipStream_t st);
+hipError_t launch_mg_plant(int batch, int N, int steps, int t, double delta, const double* uo,
+                           const int* fl, const double* xeq, const double* ueq, double* s,
+                           double* X, double* U, int* flags, hipStream_t st);
+
 }  // namespace bqp

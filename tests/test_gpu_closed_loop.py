@@ -1,0 +1,52 @@
+"""GPU closed loop (bqp_closed_loop_ocp): the DSS tracking-LMPC run of the reference
+(DSS_tracking_LMPC_casadi.m, N=100, RK4 Moore-Greitzer plant, 500 steps from x_init) regenerated
+on the GPU and compared with the stored IPOPT closed loop (data/casadi/DSS_tLMPC.mat) and with
+the same loop driven by the C restatement of the solver.
+
+The throttle-rate state x4 (natural frequency sqrt(1000) rad/s at delta = 0.01 s) makes the loop
+extremely sensitive in the transient: perturbing the applied input by 1e-11 moves x4 by 4e-3
+around step 80 (measured with the C port).  Pointwise parity is therefore asserted on the slow
+states x1, x2 over the whole run, and on all states once the transient has settled (k >= 150)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dss_tracking_lmpc_closed_loop(mg, term_set, handle=None):
+    import bqp
+    from oracle import cpu_ref, qp_forms
+    from oracle.mg_model import mg_rk4
+    g = golden('dms_DSS_tLMPC.npz')
+    N = int(g['N'])
+    tl = bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                          mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                          term_set[0], term_set[1], mg['x_wp'], mg['u_wp'], N=N)
+    Xs = g['x']                                    # stored closed loop, 499 states
+    T = Xs.shape[0] - 1
+    # a batch: the reference's x_init plus 7 states of the stored run as further initial states
+    X0 = Xs[[0, 50, 100, 150, 200, 300, 400, 450]]
+    r = bqp.closed_loop(tl, X0, T, delta=0.01)
+    assert (r.exitflag == 1).all()
+    X = r.X[0]
+    e = np.abs(X - Xs)
+    assert e[:, :2].max() < 2e-4, e[:, :2].max()
+    assert e[150:].max() < 2e-4, e[150:].max()
+    # the same loop with the C restatement of the solver
+    ocp = qp_forms.dms_ocp(mg, N, *term_set)
+    x = Xs[0].copy(); Xc = [x]
+    for k in range(T):
+        c = cpu_ref.solve(ocp, (x - mg['x_wp'])[None])
+        u = c['u'][0, 0, 0] + mg['u_wp']
+        assert abs(u - r.U[0, k, 0]) < 1e-6 or k > 40
+        x = mg_rk4(0.01, x, u); Xc.append(x)
+    Xc = np.array(Xc)
+    assert np.abs(X - Xc)[:, :2].max() < 2e-4
+    assert np.abs(X - Xc)[150:].max() < 2e-4
+    # every instance of the batch: the first step equals a single solve + one RK4 step
+    for i in range(1, len(X0)):
+        s = tl.solve(X0[i:i + 1])
+        assert np.abs(r.U[i, 0, 0] - s.u0[0, 0]) < 1e-13
+        assert np.abs(r.X[i, 1] - mg_rk4(0.01, X0[i], s.u0[0, 0])).max() < 1e-13

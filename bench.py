@@ -168,10 +168,12 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--config', default='C2', choices=['C2', 'C3', 'C4', 'C5'])
+    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C3', 'C4', 'C5', 'CL'])
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
     args = ap.parse_args()
+    if args.config in ('C1', 'CL'):
+        return bench_aux(args)
 
     import torch
     import torch.distributed as dist
@@ -311,6 +313,99 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_aux(args):
+    """Single-GPU measurements of the SURVEY.md §8(f) paths (not the driver's bench line):
+    C1  LBMPC (fmincon form F3, costLBMPC.m / constraintsLBMPC.m), N=10, NW window
+        train_data(:, 1:100), Gauss-Newton SQP on the GPU (bqp_lbmpc_solve_batched); one step =
+        one batched SQP solve (default batch 1 = the reference's single-instance config);
+    CL  closed-loop DSS tracking LMPC (N=100, RK4 plant), one step = one batched closed-loop
+        step (solve + plant) over --batch initial states; timed over --steps steps of one loop.
+    The CPU leg is the numpy restatement (oracle/lbmpc.py, interpreted) for C1 and the C
+    restatement + numpy RK4 for CL, on a bounded sample."""
+    import time as _t
+    import torch
+    import bqp
+    dev = torch.device('cuda', 0)
+    torch.cuda.set_device(0)
+    d, ts = _mg_design()
+    h = bqp.Handle(0)
+    from oracle.mg_model import mg_problem   # test-side data only for the CPU leg below
+    if args.config == 'C1':
+        g = np.load(os.path.join(GOLD, 'lbmpc_instance.npz'))
+        td = np.load(os.path.join(GOLD, 'train_data.npz'))['data'][:, :100]
+        lb = bqp.LBMPC(d['A'], d['B'], d['K'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                       d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], g['F_w_N'], g['h_w_N'],
+                       g['F_x_d'], g['h_x_d'], N=10)
+        B = args.batch or 1
+        rng = np.random.default_rng(1)
+        X0 = np.column_stack([rng.uniform(-0.35, 0.0, B), rng.uniform(-0.4, 0.0, B),
+                              0.01 * rng.standard_normal(B), 0.1 * rng.standard_normal(B)])
+        X0[0] = [-0.35, -0.4, 0.0, 0.0]                      # LBMPC_RunExample.m:41-44
+        for _ in range(args.warmup):
+            r = lb.solve(X0, td, handle=h)
+        t0 = _t.perf_counter()
+        kms = []
+        for _ in range(args.steps):
+            r = lb.solve(X0, td, handle=h)
+            kms.append(h.kernel_ms()[0])
+        el = _t.perf_counter() - t0
+        # CPU leg: the oracle's numpy SQP (interpreted) on the first instances
+        from oracle import lbmpc as olb
+        p = olb.f3_problem(mg_problem(), 10, td, g['F_w_N'], g['h_w_N'], g['F_x_d'], g['h_x_d'])
+        ns = min(B, 8)
+        c0 = _t.perf_counter()
+        for i in range(ns):
+            olb.sqp(p, X0[i])
+        cpu = ns / (_t.perf_counter() - c0)
+        line = dict(metric='LBMPC SQP solves/s (F3, N=10)', value=round(B * args.steps / el, 2),
+                    unit='SQP-solves/s', n_gpus=1, steps=args.steps, warmup=args.warmup,
+                    ms_per_step=round(1e3 * el / args.steps, 4), higher_is_better=True,
+                    scaling='weak', vs_baseline=None, dtype='f64',
+                    data='x0 = LBMPC_RunExample.m dx_init (+ seeded random states), window train_data(:,1:100)',
+                    config={'workload': 'C1: MG LBMPC (F3) N=10, batch %d' % B, 'batch_per_gpu': B,
+                            'horizon': 10, 'parallelism': 'dp1'},
+                    roofline=None, kernel_ms=round(float(np.mean(kms)), 4),
+                    cpu_baseline=dict(value=round(cpu, 2), unit='SQP-solves/s', cores=1,
+                                      kind='port', sample='%d solves of oracle/lbmpc.py (numpy)' % ns),
+                    check=dict(converged_frac=float((r.exitflag == 1).mean()),
+                               mean_sqp_iterations=float(r.iterations.mean())))
+    else:
+        gl = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
+        tl = bqp.TrackingLMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                              d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], ts['F_w_N'],
+                              ts['h_w_N'], d['x_wp'], d['u_wp'], N=100)
+        B = args.batch or 1024
+        X0 = gl['x'][np.arange(B) % len(gl['x'])]
+        bqp.closed_loop(tl, X0, 2, handle=h)
+        t0 = _t.perf_counter()
+        r = bqp.closed_loop(tl, X0, args.steps, handle=h)
+        el = _t.perf_counter() - t0
+        kms = h.kernel_ms()[0]
+        from oracle import cpu_ref, qp_forms
+        from oracle.mg_model import mg_rk4
+        mgp = mg_problem()
+        ocp = qp_forms.dms_ocp(mgp, 100, ts['F_w_N'], ts['h_w_N'])
+        c0 = _t.perf_counter()
+        x = X0[:16].copy()
+        for k in range(10):
+            c = cpu_ref.solve(ocp, x - mgp['x_wp'], threads=1)
+            u = c['u'][:, 0, 0] + mgp['u_wp']
+            x = np.array([mg_rk4(0.01, x[i], u[i]) for i in range(len(x))])
+        cpu = 16 * 10 / (_t.perf_counter() - c0)
+        line = dict(metric='closed-loop MPC steps/s (DSS tracking LMPC N=100, RK4 plant)',
+                    value=round(B * args.steps / el, 1), unit='instance-steps/s', n_gpus=1,
+                    steps=args.steps, warmup=1, ms_per_step=round(1e3 * el / args.steps, 4),
+                    higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
+                    data='initial states = stored DSS_tLMPC.mat states cycled',
+                    config={'workload': 'CL: closed loop, batch %d, %d steps' % (B, args.steps),
+                            'batch_per_gpu': B, 'horizon': 100, 'parallelism': 'dp1'},
+                    roofline=None, kernel_ms=round(kms, 4),
+                    cpu_baseline=dict(value=round(cpu, 1), unit='instance-steps/s', cores=1,
+                                      kind='port', sample='16 instances x 10 steps, oracle/cpu_ipm.c + numpy RK4'),
+                    check=dict(converged_frac=float((r.exitflag == 1).mean())))
+    print(json.dumps(line))
 
 
 if __name__ == '__main__':

@@ -12,6 +12,7 @@
 #include <math.h>
 
 #include "bqp_internal.h"
+#include "bqp_wave.h"
 
 namespace bqp {
 
@@ -477,8 +478,296 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     }
 }
 
+// ==========================================================================================
+// small dense QPs (n <= 32, no equality rows): one WAVE per instance, every vector and the
+// factor in LDS, DPP wave reductions, readlane-broadcast triangular solves - no workgroup
+// barrier anywhere.  Same Mehrotra rules and start as dense_ipm_kernel; used for the LBMPC
+// SQP sub-problems (n = N*nu + np = 11 at config C1) and small quadprog calls, where the
+// workgroup kernel above is barrier-bound (~130 us per IPM iteration at n = 11).
+// ==========================================================================================
+#define SW_NMAX 32
+#define SW_LDS_MAX (64 * 1024 / 8)   // doubles of dynamic LDS per wave-instance
+
+#define SW_A_LDS_MAX 4096             // A (m x n) staged in LDS when it has at most this many entries
+
+__host__ __device__ inline int small_lds_doubles(int n, int m) {
+    return n * n + 4 * n + 12 * n + 7 * m + (m * n <= SW_A_LDS_MAX ? m * n : 0);
+}
+
+__global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
+    const int inst = blockIdx.x;
+    if (inst >= a.batch) return;
+    const int n = a.n, m = a.m, lane = threadIdx.x;
+    extern __shared__ double sm[];
+    double* K = sm;                       // n x n column-major; lower Cholesky factor in place
+    double* z = K + n * n;
+    double* q = z + n;
+    double* dz = q + n;
+    double* rd = dz + n;
+    double* tB = rd + n;                  // bound rows: [upper 0..n-1, lower n..2n-1]
+    double* lB = tB + 2 * n;
+    double* riB = lB + 2 * n;
+    double* rcB = riB + 2 * n;
+    double* dtB = rcB + 2 * n;
+    double* dlB = dtB + 2 * n;
+    double* tA = dlB + 2 * n;             // inequality rows
+    double* lA = tA + m;
+    double* riA = lA + m;
+    double* rcA = riA + m;
+    double* dtA = rcA + m;
+    double* dlA = dtA + m;
+    double* DA = dlA + m;
+    const double* H = a.H + (int64_t)inst * a.sH;
+    const double* f = a.f + (int64_t)inst * a.sf;
+    const double* A = a.A ? a.A + (int64_t)inst * a.sA : nullptr;
+    const double* b = a.b ? a.b + (int64_t)inst * a.sb : nullptr;
+    const double* lb = a.lb ? a.lb + (int64_t)inst * a.slb : nullptr;
+    const double* ub = a.ub ? a.ub + (int64_t)inst * a.sub : nullptr;
+    if (A && m * n <= SW_A_LDS_MAX) {             // the rows are re-read ~6x per IPM iteration
+        double* As = DA + m;
+        for (int i = lane; i < m * n; i += 64) As[i] = A[i];
+        wave_sync();
+        A = As;
+    }
+    auto up_present = [&](int j) -> bool { return ub && isfinite(ub[j]); };
+    auto lo_present = [&](int j) -> bool { return lb && isfinite(lb[j]); };
+    double cnt = 0.0;
+    for (int j = lane; j < n; j += 64) cnt += (up_present(j) ? 1.0 : 0.0) + (lo_present(j) ? 1.0 : 0.0);
+    const double minv = 1.0 / fmax(wsum(cnt) + (double)m, 1.0);
+
+    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) {
+        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0;
+        for (int r = lane; r < m; r += 64) {
+            double v = tA[r] - b[r];
+            for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
+            riA[r] = v;
+            fe = fmax(fe, fabs(v));
+            cs += tA[r] * lA[r];
+        }
+        for (int j = lane; j < n; j += 64) {
+            double v = f[j];
+            for (int i = 0; i < n; ++i) v += H[(int64_t)j * n + i] * z[i];
+            gs = fmax(gs, fabs(v));
+            for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * lA[r];
+            riB[j] = 0.0; riB[n + j] = 0.0;
+            if (up_present(j)) { v += lB[j]; riB[j] = z[j] + tB[j] - ub[j]; cs += tB[j] * lB[j]; }
+            if (lo_present(j)) { v -= lB[n + j]; riB[n + j] = -z[j] + tB[n + j] + lb[j]; cs += tB[n + j] * lB[n + j]; }
+            fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
+            rd[j] = v;
+            st = fmax(st, fabs(v));
+        }
+        stat = wmax(st); feas = wmax(fe); csum = wsum(cs); gscale = wmax(gs);
+        wave_sync();
+    };
+
+    // K = H + A'DA + bound diagonal; lower Cholesky in place (lane r owns row r)
+    auto factor = [&]() -> bool {
+        for (int r = lane; r < m; r += 64) DA[r] = lA[r] / tA[r];
+        wave_sync();
+        const int ne = n * (n + 1) / 2;
+        for (int e2 = lane; e2 < ne; e2 += 64) {
+            int j = (int)((sqrt(8.0 * e2 + 1.0) - 1.0) / 2.0);
+            while (j * (j + 1) / 2 > e2) --j;
+            while ((j + 1) * (j + 2) / 2 <= e2) ++j;
+            const int i = e2 - j * (j + 1) / 2;          // i <= j
+            double v = H[(int64_t)j * n + i];
+            for (int r = 0; r < m; ++r) v += A[(int64_t)i * m + r] * DA[r] * A[(int64_t)j * m + r];
+            if (i == j) {
+                if (up_present(j)) v += lB[j] / tB[j];
+                if (lo_present(j)) v += lB[n + j] / tB[n + j];
+            }
+            K[(int64_t)i * n + j] = v;                   // lower: row j, column i
+        }
+        wave_sync();
+        bool ok = true;
+        for (int j = 0; j < n; ++j) {
+            const double d = K[(int64_t)j * n + j];
+            if (!(d > 0.0)) { ok = false; break; }
+            const double ljj = sqrt(d);
+            const double il = 1.0 / ljj;
+            if (lane > j && lane < n) K[(int64_t)j * n + lane] *= il;
+            if (lane == j) K[(int64_t)j * n + j] = ljj;
+            wave_sync();
+            if (lane > j && lane < n) {
+                const double lrj = K[(int64_t)j * n + lane];
+                for (int c = j + 1; c <= lane; ++c) K[(int64_t)c * n + lane] -= lrj * K[(int64_t)j * n + c];
+            }
+            wave_sync();
+        }
+        return ok;
+    };
+
+    // x = -(L L')^{-1} q with lane i holding entry i (n <= 32): column-oriented substitution,
+    // the solved entry broadcast by readlane
+    auto chol_neg_solve = [&](double* x) {
+        double v = (lane < n) ? -q[lane] : 0.0;
+        for (int i = 0; i < n; ++i) {                     // L y = -q
+            const double yi = rl(v, i) / K[(int64_t)i * n + i];
+            if (lane == i) v = yi;
+            else if (lane > i && lane < n) v -= K[(int64_t)i * n + lane] * yi;
+        }
+        for (int i = n - 1; i >= 0; --i) {                // L' x = y
+            const double xi = rl(v, i) / K[(int64_t)i * n + i];
+            if (lane == i) v = xi;
+            else if (lane < i) v -= K[(int64_t)lane * n + i] * xi;
+        }
+        if (lane < n) x[lane] = v;
+        wave_sync();
+    };
+
+    auto solve = [&]() {
+        for (int r = lane; r < m; r += 64) dlA[r] = (lA[r] * riA[r] - rcA[r]) / tA[r];
+        wave_sync();
+        for (int j = lane; j < n; j += 64) {
+            double v = rd[j];
+            for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * dlA[r];
+            if (up_present(j)) v += (lB[j] * riB[j] - rcB[j]) / tB[j];
+            if (lo_present(j)) v -= (lB[n + j] * riB[n + j] - rcB[n + j]) / tB[n + j];
+            q[j] = v;
+        }
+        wave_sync();
+        chol_neg_solve(dz);
+        for (int r = lane; r < m; r += 64) {
+            double v = 0.0;
+            for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * dz[j];
+            dtA[r] = -riA[r] - v;
+            dlA[r] = (-rcA[r] - lA[r] * dtA[r]) / tA[r];
+        }
+        for (int j = lane; j < n; j += 64) {
+            dtB[j] = dlB[j] = dtB[n + j] = dlB[n + j] = 0.0;
+            if (up_present(j)) { dtB[j] = -riB[j] - dz[j]; dlB[j] = (-rcB[j] - lB[j] * dtB[j]) / tB[j]; }
+            if (lo_present(j)) { dtB[n + j] = -riB[n + j] + dz[j]; dlB[n + j] = (-rcB[n + j] - lB[n + j] * dtB[n + j]) / tB[n + j]; }
+        }
+        wave_sync();
+    };
+    auto max_step = [&]() -> double {
+        double al = 1.0;
+#define DW_RATIO(v, dv) if ((dv) < 0.0) al = fmin(al, -(v) / (dv));
+        for (int r = lane; r < m; r += 64) { DW_RATIO(tA[r], dtA[r]); DW_RATIO(lA[r], dlA[r]); }
+        for (int j = lane; j < n; j += 64) {
+            if (up_present(j)) { DW_RATIO(tB[j], dtB[j]); DW_RATIO(lB[j], dlB[j]); }
+            if (lo_present(j)) { DW_RATIO(tB[n + j], dtB[n + j]); DW_RATIO(lB[n + j], dlB[n + j]); }
+        }
+#undef DW_RATIO
+        return wmin(al);
+    };
+    auto comp_after = [&](double al) -> double {
+        double c = 0.0;
+        for (int r = lane; r < m; r += 64) c += (tA[r] + al * dtA[r]) * (lA[r] + al * dlA[r]);
+        for (int j = lane; j < n; j += 64) {
+            if (up_present(j)) c += (tB[j] + al * dtB[j]) * (lB[j] + al * dlB[j]);
+            if (lo_present(j)) c += (tB[n + j] + al * dtB[n + j]) * (lB[n + j] + al * dlB[n + j]);
+        }
+        return wsum(c);
+    };
+
+    // initial point (as dense_ipm_kernel)
+    for (int j = lane; j < n; j += 64) {
+        z[j] = 0.0;
+        tB[j] = tB[n + j] = 1.0;
+        lB[j] = up_present(j) ? 1.0 : 0.0;
+        lB[n + j] = lo_present(j) ? 1.0 : 0.0;
+        rcB[j] = up_present(j) ? 1.0 : 0.0;
+        rcB[n + j] = lo_present(j) ? 1.0 : 0.0;
+    }
+    for (int r = lane; r < m; r += 64) { tA[r] = 1.0; lA[r] = 1.0; rcA[r] = 1.0; }
+    wave_sync();
+    double bsl = 0.0;
+    for (int r = lane; r < m; r += 64) bsl = fmax(bsl, fabs(b[r]));
+    for (int j = lane; j < n; j += 64) {
+        if (up_present(j)) bsl = fmax(bsl, fabs(ub[j]));
+        if (lo_present(j)) bsl = fmax(bsl, fabs(lb[j]));
+    }
+    const double bscale = wmax(bsl);
+    double stat, feas, csum, gscale;
+    residuals(stat, feas, csum, gscale);
+    int flag = 0;
+    if (!factor()) flag = -8;
+    if (flag == 0) {
+        solve();
+        double tmin = INFINITY, tmax = -INFINITY;
+        for (int j = lane; j < n; j += 64) z[j] += dz[j];
+        for (int r = lane; r < m; r += 64) { const double t = 1.0 + dtA[r]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+        for (int j = lane; j < n; j += 64) {
+            if (up_present(j)) { const double t = 1.0 + dtB[j]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+            if (lo_present(j)) { const double t = 1.0 + dtB[n + j]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+        }
+        tmin = wmin(tmin);
+        tmax = wmax(tmax);
+        const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
+        const double shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
+        for (int r = lane; r < m; r += 64) { const double t = 1.0 + dtA[r]; tA[r] = t + shp; lA[r] = -t + shd; }
+        for (int j = lane; j < n; j += 64) {
+            const double tu = 1.0 + dtB[j], tl = 1.0 + dtB[n + j];
+            tB[j] = up_present(j) ? tu + shp : 1.0; lB[j] = up_present(j) ? -tu + shd : 0.0;
+            tB[n + j] = lo_present(j) ? tl + shp : 1.0; lB[n + j] = lo_present(j) ? -tl + shd : 0.0;
+        }
+        wave_sync();
+    }
+    int it = 0;
+    double mu = 0.0;
+    if (flag == 0) {
+        for (it = 0; it <= a.max_iter; ++it) {
+            residuals(stat, feas, csum, gscale);
+            mu = csum * minv;
+            if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
+                mu <= a.tol_comp) { flag = 1; break; }
+            if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
+            if (it == a.max_iter) break;
+            if (!factor()) { flag = -8; break; }
+            for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r];
+            for (int j = lane; j < 2 * n; j += 64) rcB[j] = tB[j] * lB[j];
+            wave_sync();
+            solve();
+            double al = max_step();
+            const double mua = comp_after(al) * minv;
+            double sg = mua / mu;
+            sg = sg * sg * sg;
+            const double smu = sg * mu;
+            for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r] + dtA[r] * dlA[r] - smu;
+            for (int j = lane; j < n; j += 64) {
+                rcB[j] = up_present(j) ? tB[j] * lB[j] + dtB[j] * dlB[j] - smu : 0.0;
+                rcB[n + j] = lo_present(j) ? tB[n + j] * lB[n + j] + dtB[n + j] * dlB[n + j] - smu : 0.0;
+            }
+            wave_sync();
+            solve();
+            al = fmin(1.0, max_step() * a.tau);
+            for (int j = lane; j < n; j += 64) {
+                z[j] += al * dz[j];
+                if (up_present(j)) { tB[j] += al * dtB[j]; lB[j] += al * dlB[j]; }
+                if (lo_present(j)) { tB[n + j] += al * dtB[n + j]; lB[n + j] += al * dlB[n + j]; }
+            }
+            for (int r = lane; r < m; r += 64) { tA[r] += al * dtA[r]; lA[r] += al * dlA[r]; }
+            wave_sync();
+        }
+    }
+    double fv = 0.0;
+    for (int j = lane; j < n; j += 64) {
+        double hz = 0.0;
+        for (int i = 0; i < n; ++i) hz += H[(int64_t)j * n + i] * z[i];
+        fv += z[j] * (0.5 * hz + f[j]);
+        a.x[(int64_t)inst * n + j] = z[j];
+        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = lo_present(j) ? lB[n + j] : 0.0;
+        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = up_present(j) ? lB[j] : 0.0;
+    }
+    for (int r = lane; r < m; r += 64)
+        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = lA[r];
+    fv = wsum(fv);
+    if (lane == 0) {
+        if (a.fval) a.fval[inst] = fv;
+        a.exitflag[inst] = flag;
+        double* so = a.stats + (int64_t)inst * 4;
+        so[0] = (double)it; so[1] = stat; so[2] = feas; so[3] = mu;
+    }
+}
+
 hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
     if (a.n > 256 || a.me > 256) return hipErrorInvalidValue;
+    if (a.me == 0 && a.n <= SW_NMAX && small_lds_doubles(a.n, a.m) <= SW_LDS_MAX) {
+        hipLaunchKernelGGL(dense_wave_kernel, dim3(a.batch), dim3(64),
+                           sizeof(double) * small_lds_doubles(a.n, a.m), st, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(dense_ipm_kernel, dim3(a.batch), dim3(DT), 0, st, a);
     return hipGetLastError();
 }

@@ -168,11 +168,11 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C3', 'C4', 'C5', 'CL'])
+    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C3', 'C4', 'C5', 'CL'])
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
     args = ap.parse_args()
-    if args.config in ('C1', 'CL'):
+    if args.config in ('C1', 'CL', 'C2H'):
         return bench_aux(args)
 
     import torch
@@ -331,8 +331,26 @@ def bench_aux(args):
     torch.cuda.set_device(0)
     d, ts = _mg_design()
     h = bqp.Handle(0)
-    from oracle.mg_model import mg_problem   # test-side data only for the CPU leg below
-    if args.config == 'C1':
+    if args.config == 'C2H':
+        # the C2 workload through the HOST-pointer entry point: PCIe-inclusive rate (inputs
+        # copied in, trajectories copied out every call) - reported in DESIGN.md, never `value`
+        wl = workload('C2', args.batch, 0, 1)
+        for _ in range(args.warmup):
+            bqp.solve_ocp(wl['prob'], wl['X'], handle=h)
+        t0 = _t.perf_counter()
+        for _ in range(args.steps):
+            r = bqp.solve_ocp(wl['prob'], wl['X'], handle=h)
+        el = _t.perf_counter() - t0
+        B = wl['X'].shape[0]
+        line = dict(metric='QP-steps/s, host-pointer API (PCIe-inclusive)', value=round(B * args.steps / el, 1),
+                    unit='QP-steps/s', n_gpus=1, steps=args.steps, warmup=args.warmup,
+                    ms_per_step=round(1e3 * el / args.steps, 4), higher_is_better=True, scaling='weak',
+                    vs_baseline=None, dtype='f64', data=wl['data'],
+                    config={'workload': wl['text'] + ', host buffers', 'batch_per_gpu': B, 'horizon': 20,
+                            'parallelism': 'dp1'},
+                    roofline=None, kernel_ms=round(h.kernel_ms()[0], 4), cpu_baseline=None,
+                    check=dict(converged_frac=float((r.exitflag == 1).mean())))
+    elif args.config == 'C1':
         g = np.load(os.path.join(GOLD, 'lbmpc_instance.npz'))
         td = np.load(os.path.join(GOLD, 'train_data.npz'))['data'][:, :100]
         lb = bqp.LBMPC(d['A'], d['B'], d['K'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
@@ -352,7 +370,8 @@ def bench_aux(args):
             kms.append(h.kernel_ms()[0])
         el = _t.perf_counter() - t0
         # CPU leg: the oracle's numpy SQP (interpreted) on the first instances
-        from oracle import lbmpc as olb
+        from oracle import lbmpc as olb               # CPU leg only
+        from oracle.mg_model import mg_problem
         p = olb.f3_problem(mg_problem(), 10, td, g['F_w_N'], g['h_w_N'], g['F_x_d'], g['h_x_d'])
         ns = min(B, 8)
         c0 = _t.perf_counter()
@@ -383,8 +402,8 @@ def bench_aux(args):
         r = bqp.closed_loop(tl, X0, args.steps, handle=h)
         el = _t.perf_counter() - t0
         kms = h.kernel_ms()[0]
-        from oracle import cpu_ref, qp_forms
-        from oracle.mg_model import mg_rk4
+        from oracle import cpu_ref, qp_forms          # CPU leg only
+        from oracle.mg_model import mg_problem, mg_rk4
         mgp = mg_problem()
         ocp = qp_forms.dms_ocp(mgp, 100, ts['F_w_N'], ts['h_w_N'])
         c0 = _t.perf_counter()

@@ -1233,6 +1233,83 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
         return 0.0;
     };
 
+    // ---- predictor pass 2 fused with the corrector right-hand side: the complementarity sum
+    //      (t + al dt)(lam + al dlam) along the predictor direction, the stored products
+    //      dt dlam, and the corrector terms WITHOUT their sigma mu part,
+    //      e0 = (lam ri - t lam - dt dlam)/t (box slots in place, polytope rows as Fp'e0), plus
+    //      Fp'(1/t): e = e0 + sigma mu / t once sigma is known (rhs_corr_finish) ----
+    auto comp_rhs0 = [&](double al, double (&gpe0)[NV], double (&gpi)[NV]) __attribute__((always_inline)) -> double {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    double e0 = 0.0;
+                    if (pres(j, sl, h)) {
+                        const double t = tx[j][sl][h], l = lx[j][sl][h];
+                        const double it = frcp(t);
+                        const double rc = t * l;
+                        const double dt = box_dir(j, k, sl, h, L.dsv, L.duv);
+                        const double dl = (-rc - l * dt) * it;
+                        acc += (t + al * dt) * (l + al * dl);
+                        e0 = (l * box_res(j, k, sl, h) - (rc + dt * dl)) * it;
+                    }
+                    W[L.ebox + (k * NB + sl) * 2 + h] = e0;
+                }
+        }
+#pragma unroll
+        for (int c = 0; c < NV; ++c) { gpe0[c] = 0.0; gpi[c] = 0.0; }
+        double dvp[NV];
+        load_v(dvp, L.dsv, L.duv);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            ROW_FENCE(q);
+            const int r = lane + WAVE * q;
+            if (r >= mp) continue;
+            double f[NV];
+#pragma unroll
+            for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
+            double fd = 0.0;
+#pragma unroll
+            for (int c = 0; c < NV; ++c) fd += f[c] * dvp[c];
+            const double t = tp[q], l = lp[q];
+            const double it = frcp(t);
+            const double rc = t * l;
+            const double dt = -rp[q] - fd;
+            const double dl = (-rc - l * dt) * it;
+            acc += (t + al * dt) * (l + al * dl);
+            const double pr = dt * dl;
+            W[L.prp + r] = pr;
+            const double e0 = (l * rp[q] - (rc + pr)) * it;
+#pragma unroll
+            for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }
+        }
+        return wsum(acc);
+    };
+    auto rhs_corr_finish = [&](double smu, double (&gpe0)[NV], double (&gpi)[NV]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (pres(j, sl, h)) W[L.ebox + (k * NB + sl) * 2 + h] += smu * frcp(tx[j][sl][h]);
+        }
+        double g[NV];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) g[c] = wsum(gpe0[c]) + smu * wsum(gpi[c]);
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NV; ++c) W[L.gpe + c] = g[c];
+        }
+    };
+
     // ======================= initial point ==================================================
     lam_side();
     BARRIER();                                            // I0
@@ -1297,11 +1374,12 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
         const double mu = X[X_CS] * minv;
         const double rm_a = row_pass(0, false, 0.0, 0.0, L.dsv, L.duv);
         const double al_aff = rm_a > 1.0 ? 1.0 / rm_a : 1.0;
-        const double mua = row_pass(1, false, 0.0, al_aff, L.dsv, L.duv) * minv;
+        double gpe0[NV], gpi[NV];
+        const double mua = comp_rhs0(al_aff, gpe0, gpi) * minv;
         double sg = mua / mu;
         sg = sg * sg * sg;
         const double smu = sg * mu;
-        rhs_terms(true, smu);
+        rhs_corr_finish(smu, gpe0, gpi);
         STAMP(5);
         BARRIER();                                        // B4
         BARRIER();                                        // B5: corrector direction in (dsc, duc)

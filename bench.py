@@ -171,6 +171,8 @@ def main():
     ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C3', 'C4', 'C5', 'CL'])
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32'],
+                    help='structured solver arithmetic (C5 compares both)')
     args = ap.parse_args()
     if args.config in ('C1', 'CL', 'C2H'):
         return bench_aux(args)
@@ -219,7 +221,7 @@ def main():
     oe = torch.empty((B,), dtype=torch.int32, device=dev)
     lib = bqp.load()
     h = bqp.Handle(local)
-    opt = _lib.options()
+    opt = _lib.options(precision=1 if args.precision == 'fp32' else 0)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -267,6 +269,13 @@ def main():
         err = max([abs(u0[b] - g['du_star'][pos[int(wl['gidx'][b])]])
                    for b in range(B) if int(wl['gidx'][b]) in pos] or [0.0])
         check['max_abs_du0_vs_exact'] = float(err)
+    if args.config == 'C5':
+        g5 = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
+        pos = {int(i): j for j, i in enumerate(g5['idx'])}
+        u_eq = float(np.atleast_1d(_mg_design()[0]['u_wp'])[0])
+        err = max([abs(u0[b] + u_eq - g5['u_star'][pos[int(wl['gidx'][b])]])
+                   for b in range(B) if int(wl['gidx'][b]) in pos] or [0.0])
+        check['max_abs_u0_vs_exact'] = float(err)
 
     if rank == 0:
         value = wl['total'] / (elapsed / args.steps) if wl['scaling'] == 'strong' \
@@ -294,7 +303,8 @@ def main():
             'metric': METRIC,
             'value': round(value, 1), 'unit': 'QP-steps/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
-            'higher_is_better': True, 'scaling': wl['scaling'], 'vs_baseline': None, 'dtype': 'f64',
+            'higher_is_better': True, 'scaling': wl['scaling'], 'vs_baseline': None,
+            'dtype': 'f32' if args.precision == 'fp32' else 'f64',
             'data': wl['data'],
             'config': {'workload': wl['text'], 'batch_per_gpu': B, 'horizon': N,
                        'parallelism': 'dp%d' % world},

@@ -51,7 +51,8 @@ typedef struct {
     double tol_feas;   /* primal residual inf-norm / (1 + |bounds, rhs|_inf), default 1e-10 */
     double tol_comp;   /* average complementarity mu (absolute), default 1e-14 */
     double tau;        /* fraction-to-boundary, default 0.995 */
-    int precision;     /* 0 = fp64 (default) */
+    int precision;     /* 0 = fp64 (default); 1 = fp32 solver arithmetic/LDS state (structured API; inputs
+                          and outputs stay fp64; tolerances floored at 1e-5 / 1e-6 / 1e-9) */
     int want_duals;    /* 1: fill the multiplier outputs (structured API) */
 } bqp_options;
 

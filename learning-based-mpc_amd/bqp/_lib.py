@@ -177,9 +177,11 @@ class Handle:
 
 
 def options(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995,
-            want_duals=0):
+            want_duals=0, precision=0):
+    """precision: 0 fp64, 1 fp32 (structured solver; see include/bqp.h)"""
     o = Options()
     load().bqp_default_options(C.byref(o))
     o.max_iter, o.tol_stat, o.tol_feas, o.tol_comp, o.tau = max_iter, tol_stat, tol_feas, tol_comp, tau
     o.want_duals = want_duals
+    o.precision = precision
     return o

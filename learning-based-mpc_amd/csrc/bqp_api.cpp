@@ -188,14 +188,22 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     hipStream_t st = (hipStream_t)stream;
     bqp_options o;
     resolve(opt, &o);
+    const bool f32 = o.precision == 1;     // fp32 instantiation (bqp_ocp_f32.hip), config C5
+    if (f32) {
+        // fp32 arithmetic cannot resolve the fp64 defaults: floor the stopping tolerances
+        o.tol_stat = std::max(o.tol_stat, 1e-5);
+        o.tol_feas = std::max(o.tol_feas, 1e-6);
+        o.tol_comp = std::max(o.tol_comp, 1e-9);
+    }
     const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
     const int nv = nx + nu + np;
     const int mp = d->n_poly;
     const int hstride = nv * nv + 1;
     const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));   // = the kernel's RPL * 64
-    const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;
-    const int per_wave = bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
-    const size_t lds_budget = 160 * 1024 / sizeof(double);
+    const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;   // elements
+    const int per_wave = f32 ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad)
+                             : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
+    const size_t lds_budget = 160 * 1024 / (f32 ? sizeof(float) : sizeof(double));
     int wpb = 4;   // instances per workgroup (two waves each)
     while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
     if ((size_t)shared_doubles + (size_t)per_wave > lds_budget) return BQP_E_UNSUPPORTED;
@@ -232,7 +240,10 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     h->last_batch = batch;
 #endif
     HIP_TRY(hipEventRecord(h->ev0, st));
-    HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
+    if (f32)
+        HIP_TRY(bqp::launch_ocp_f32(a, nx, nu, np, st));
+    else
+        HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->timed = true;
     h->launches = 1;

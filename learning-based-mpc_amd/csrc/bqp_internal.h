@@ -28,6 +28,9 @@ bool ocp_supported(int nx, int nu, int np);
 int ocp_rpl_for(int mp);
 int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad);
 hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
+// fp32 instantiation (bqp_ocp_f32.hip): LDS element count per instance (floats) and launch
+int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad);
+hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,
                            hipStream_t st);

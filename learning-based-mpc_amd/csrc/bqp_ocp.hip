@@ -32,8 +32,30 @@
 
 namespace bqp {
 
+// One source, two instantiations: fp64 (this file) and fp32 (bqp_ocp_f32.hip defines BQP_F32 and
+// includes this file).  The element type of the solver's LDS state and arithmetic is `real`;
+// the caller's arrays in HBM stay fp64 (converted on load/store).  Each precision lives in its own
+// inner namespace so the two template instantiations never merge at link time.
+#ifdef BQP_F32
+typedef float real;
+typedef float2 real2;
+#define BQP_SFX _f32
+namespace sp {
+#else
+typedef double real;
+typedef double2 real2;
+#define BQP_SFX
+namespace dp {
+#endif
+#define BQP_CAT2(a, b) a##b
+#define BQP_CAT(a, b) BQP_CAT2(a, b)
+
 #define WAVE 64
+#ifdef BQP_F32
+#define PIV_FLOOR 1e-7
+#else
 #define PIV_FLOOR 1e-14
+#endif
 #define MU_BLOWUP 1e6
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
@@ -47,18 +69,22 @@ __device__ __forceinline__ double frcp(double t) {
     e = __builtin_fma(-t, r, 1.0);
     return __builtin_fma(r, e, r);
 }
+__device__ __forceinline__ float frcp(float t) {
+    float r = __builtin_amdgcn_rcpf(t);
+    return __builtin_fmaf(r, __builtin_fmaf(-t, r, 1.0f), r);
+}
 
 template <int N>
-__device__ __forceinline__ bool chol_small(const double (&M)[N][N], double (&L)[N][N]) {
+__device__ __forceinline__ bool chol_small(const real (&M)[N][N], real (&L)[N][N]) {
     bool ok = true;
-    double d0 = M[0][0];
+    real d0 = M[0][0];
     if (!(d0 > PIV_FLOOR * M[0][0])) d0 = PIV_FLOOR * M[0][0];
     ok = ok && (d0 > 0.0);
     L[0][0] = sqrt(d0);
     if constexpr (N == 2) {
         L[0][1] = 0.0;
         L[1][0] = M[1][0] / L[0][0];
-        double d1 = M[1][1] - L[1][0] * L[1][0];
+        real d1 = M[1][1] - L[1][0] * L[1][0];
         if (!(d1 > PIV_FLOOR * M[1][1])) d1 = PIV_FLOOR * M[1][1];
         ok = ok && (d1 > 0.0);
         L[1][1] = sqrt(d1);
@@ -68,7 +94,7 @@ __device__ __forceinline__ bool chol_small(const double (&M)[N][N], double (&L)[
 // b <- M^{-1} b with M = L L' (substitution, same order as oracle/cpu_ipm.c spd_solve); L row-major.
 // For n = 1 the factor slot holds 1/M instead (one reciprocal, no square root).
 template <int N>
-__device__ __forceinline__ void chol_solve_small(const double* L, double (&b)[N]) {
+__device__ __forceinline__ void chol_solve_small(const real* L, real (&b)[N]) {
     if constexpr (N == 2) {
         b[0] = b[0] / L[0];
         b[1] = (b[1] - L[2] * b[0]) / L[3];
@@ -181,13 +207,13 @@ struct QpLds {
 // stage wave
 // ==========================================================================================
 template <int NX, int NU, int NP, int SPL>
-__device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, const QpLds& L,
-                                           const double* Hs, int lane, int inst) {
+__device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
+                                           const real* Hs, int lane, int inst) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     constexpr int NB = NX + NU;
     const int N = a.N, kp = a.kp, hstride = a.hstride;
-    double* X = W + L.xch;
+    real* X = W + L.xch;
     STAMP_DECL;
 
     // ---------------- per-instance model -> LDS (Abar row-major, Bbar) ---------------------
@@ -204,22 +230,22 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         }
     }
     wave_sync();
-    auto Abar = [&](int i, int j) __attribute__((always_inline)) -> double { return W[L.AB + i * NS + j]; };
-    auto Bbar = [&](int i, int j) __attribute__((always_inline)) -> double { return W[L.AB + NS * NS + i * NU + j]; };
-    double cb[NS];
+    auto Abar = [&](int i, int j) __attribute__((always_inline)) -> real { return W[L.AB + i * NS + j]; };
+    auto Bbar = [&](int i, int j) __attribute__((always_inline)) -> real { return W[L.AB + NS * NS + i * NU + j]; };
+    real cb[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) cb[i] = (i < NX && a.c) ? a.c[(int64_t)inst * a.sc + i] : 0.0;
     const double* wb = a.w ? a.w + (int64_t)inst * a.sw : nullptr;
     // linear cost term of stage k, internal index i ([x; theta; u] from external [x; u; theta])
-    auto gterm = [&](int k, int i) __attribute__((always_inline)) -> double {
+    auto gterm = [&](int k, int i) __attribute__((always_inline)) -> real {
         if (!wb || (k == N && i >= NS)) return 0.0;
         const int e = (i < NX) ? i : (i < NS ? NX + NU + (i - NX) : NX + (i - NS));
         return wb[(int64_t)k * NV + e];
     };
 
-    double s[SPL][NS], u[SPL][NU], pi[SPL][NS], kff[SPL][NU];
+    real s[SPL][NS], u[SPL][NU], pi[SPL][NS], kff[SPL][NU];
     const double* x0 = a.x0 + (int64_t)inst * a.sx0;
-    double x0max = 0.0;
+    real x0max = 0.0;
 #pragma unroll
     for (int i = 0; i < NX; ++i) x0max = fmax(x0max, fabs(x0[i]));
 #pragma unroll
@@ -252,33 +278,33 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
 
     // ---- stage residuals without the row multipliers: rs' = g + Abar' pi_{k+1} - pi_k,
     //      ru' = g_u + Bbar' pi_{k+1}, re = Abar s + Bbar u + c - s_{k+1}; returns max|re|, max|g|
-    auto stage_partials = [&](double& feasA, double& gsA) __attribute__((always_inline)) {
-        double fe = 0, gs = 0;
+    auto stage_partials = [&](real& feasA, real& gsA) __attribute__((always_inline)) {
+        real fe = 0, gs = 0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k > N) continue;
-            const double* Hk = Hs + k * hstride;
-            double v[NV];
+            const real* Hk = Hs + k * hstride;
+            real v[NV];
 #pragma unroll
             for (int i = 0; i < NS; ++i) v[i] = s[j][i];
 #pragma unroll
             for (int i = 0; i < NU; ++i) v[NS + i] = (k < N) ? u[j][i] : 0.0;
-            double gv[NV];
+            real gv[NV];
 #pragma unroll
             for (int i = 0; i < NV; ++i) {
-                double acc = gterm(k, i);
+                real acc = gterm(k, i);
 #pragma unroll
                 for (int c = 0; c < NV; ++c) acc += Hk[i * NV + c] * v[c];
                 gv[i] = acc;
                 gs = fmax(gs, fabs(acc));
             }
-            double pn[NS];
+            real pn[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) pn[i] = (k < N) ? W[L.qt_xpi + (k + 1) * NS + i] : 0.0;
 #pragma unroll
             for (int i = 0; i < NS; ++i) {
-                double acc = gv[i];
+                real acc = gv[i];
                 if (k < N) {
 #pragma unroll
                     for (int c = 0; c < NS; ++c) acc += Abar(c, i) * pn[c];
@@ -288,7 +314,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                double acc = gv[NS + i];
+                real acc = gv[NS + i];
 #pragma unroll
                 for (int c = 0; c < NS; ++c) acc += Bbar(c, i) * pn[c];
                 W[L.ru + k * NU + i] = (k < N) ? acc : 0.0;
@@ -296,7 +322,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
             if (k < N) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double acc = cb[i] - W[L.xs + (k + 1) * NS + i];
+                    real acc = cb[i] - W[L.xs + (k + 1) * NS + i];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
 #pragma unroll
@@ -312,16 +338,16 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
 
     // ---- add the row multipliers (box [upper, lower] in that order, polytope at kp) and
     //      return the stationarity norm ----
-    auto combine = [&]() __attribute__((always_inline)) -> double {
-        double gpp[NV];
+    auto combine = [&]() __attribute__((always_inline)) -> real {
+        real gpp[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) gpp[c] = W[L.gpp + c];
-        double st = 0;
+        real st = 0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k > N) continue;
-            double r[NS], ru[NU];
+            real r[NS], ru[NU];
 #pragma unroll
             for (int i = 0; i < NS; ++i) r[i] = W[L.rs + k * NS + i];
 #pragma unroll
@@ -367,7 +393,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     constexpr int PST = pk_stride(NS);
     // the model operands of the factor and of the sweeps are re-read from LDS at the start of
     // each phase (not kept live across the iteration: register budget at two waves per SIMD)
-    auto load_ab = [&](double (&Ai)[NS], double (&Aj)[NS], double (&Bl)[NS][NU]) __attribute__((always_inline)) {
+    auto load_ab = [&](real (&Ai)[NS], real (&Aj)[NS], real (&Bl)[NS][NU]) __attribute__((always_inline)) {
 #pragma unroll
         for (int a_ = 0; a_ < NS; ++a_) {
             Ai[a_] = Abar(a_, ib);
@@ -377,14 +403,14 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         }
     };
     auto factor = [&]() __attribute__((always_inline)) -> bool {
-        double Ai[NS], Aj[NS], Bl[NS][NU];
+        real Ai[NS], Aj[NS], Bl[NS][NU];
         load_ab(Ai, Aj, Bl);
         // stage-k entries each lane needs, prefetched one stage ahead as RAW operands (cost
         // entry, box diagonal) and combined only when the stage is processed; the polytope term
         // F'DF enters at stage kp only (a uniform branch).  Operation order (H + D) + FD.
-        struct StageH { double hij, dij, hui[NU], huj[NU], huu[NU][NU], duu[NU]; };
+        struct StageH { real hij, dij, hui[NU], huj[NU], huu[NU][NU], duu[NU]; };
         auto load_h = [&](int k, StageH& sh) __attribute__((always_inline)) {
-            const double* Hk = Hs + k * hstride;
+            const real* Hk = Hs + k * hstride;
             sh.hij = Hk[ib * NV + jb];
             sh.dij = W[L.Dx + k * NV + ib];
 #pragma unroll
@@ -416,18 +442,18 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
                 }
             }
         };
-        double pu[PST];
+        real pu[PST];
         auto bcast_p = [&](int k) __attribute__((always_inline)) {
             wave_sync();
-            const double2* src = reinterpret_cast<const double2*>(W + L.P + k * PST);
+            const real2* src = reinterpret_cast<const real2*>(W + L.P + k * PST);
 #pragma unroll
             for (int q = 0; q < PST / 2; ++q) {
-                const double2 t2 = src[q];
+                const real2 t2 = src[q];
                 pu[2 * q] = t2.x;
                 pu[2 * q + 1] = t2.y;
             }
         };
-        auto Pm = [&](int a_, int b_) __attribute__((always_inline)) -> double { return pu[pk_idx(NS, a_, b_)]; };
+        auto Pm = [&](int a_, int b_) __attribute__((always_inline)) -> real { return pu[pk_idx(NS, a_, b_)]; };
         {
             StageH rN, cN;
             load_h(N, rN);
@@ -442,48 +468,48 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
             combine_h(k, raw, cur);
             if (k > 0) load_h(k - 1, nxt);
             // g = P_{k+1} Bbar (uniform) and G_jb = P_{k+1} Abar(:, jb)
-            double g[NS][NU], Gj[NS];
+            real g[NS][NU], Gj[NS];
 #pragma unroll
             for (int a_ = 0; a_ < NS; ++a_) {
-                double gj = 0.0;
+                real gj = 0.0;
 #pragma unroll
                 for (int b = 0; b < NS; ++b) gj += Pm(a_, b) * Aj[b];
                 Gj[a_] = gj;
 #pragma unroll
                 for (int x = 0; x < NU; ++x) {
-                    double acc = 0.0;
+                    real acc = 0.0;
 #pragma unroll
                     for (int b = 0; b < NS; ++b) acc += Pm(a_, b) * Bl[b][x];
                     g[a_][x] = acc;
                 }
             }
             // input rows of M = Ht + F' P F for columns ib, jb and Rhat = M_uu
-            double mi[NU], mj[NU], Ruu[NU][NU];
+            real mi[NU], mj[NU], Ruu[NU][NU];
 #pragma unroll
             for (int x = 0; x < NU; ++x) {
-                double vi = cur.hui[x], vj = cur.huj[x];
+                real vi = cur.hui[x], vj = cur.huj[x];
 #pragma unroll
                 for (int a_ = 0; a_ < NS; ++a_) { vi += g[a_][x] * Ai[a_]; vj += g[a_][x] * Aj[a_]; }
                 mi[x] = vi;
                 mj[x] = vj;
 #pragma unroll
                 for (int y = 0; y < NU; ++y) {
-                    double r = cur.huu[x][y];
+                    real r = cur.huu[x][y];
 #pragma unroll
                     for (int a_ = 0; a_ < NS; ++a_) r += g[a_][x] * Bl[a_][y];
                     Ruu[x][y] = r;
                 }
             }
             // K columns ib, jb:  K = -Rhat^{-1} M_us  (nu = 1: one reciprocal; else Cholesky)
-            double Ki[NU], Kj[NU], Lf[NU * NU];
+            real Ki[NU], Kj[NU], Lf[NU * NU];
             if constexpr (NU == 1) {
                 ok = ok && (Ruu[0][0] > 0.0);
-                const double rinv = 1.0 / Ruu[0][0];
+                const real rinv = 1.0 / Ruu[0][0];
                 Lf[0] = rinv;
                 Ki[0] = -mi[0] * rinv;
                 Kj[0] = -mj[0] * rinv;
             } else {
-                double Lc[NU][NU];
+                real Lc[NU][NU];
                 ok = chol_small<NU>(Ruu, Lc) && ok;
 #pragma unroll
                 for (int x = 0; x < NU; ++x)
@@ -495,24 +521,24 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
                 chol_solve_small<NU>(Lf, Kj);
             }
             // Phi(:, ib) = Abar(:, ib) + Bbar K_ib ; T_jb = P Phi(:, jb) = G_jb + g K_jb
-            double Phi_i[NS], Tj[NS];
+            real Phi_i[NS], Tj[NS];
 #pragma unroll
             for (int a_ = 0; a_ < NS; ++a_) {
-                double vi = Ai[a_], vt = Gj[a_];
+                real vi = Ai[a_], vt = Gj[a_];
 #pragma unroll
                 for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vt += g[a_][x] * Kj[x]; }
                 Phi_i[a_] = vi;
                 Tj[a_] = vt;
             }
             // Joseph form  P_k(ib, jb) = [I;K]' Ht [I;K] + Phi(:, ib)' P Phi(:, jb)
-            double v = cur.hij;
+            real v = cur.hij;
 #pragma unroll
             for (int x = 0; x < NU; ++x) {
                 v += Ki[x] * cur.huj[x] + cur.hui[x] * Kj[x];
 #pragma unroll
                 for (int y = 0; y < NU; ++y) v += Ki[x] * cur.huu[x][y] * Kj[y];
             }
-            double acc = 0.0;
+            real acc = 0.0;
 #pragma unroll
             for (int a_ = 0; a_ < NS; ++a_) acc += Phi_i[a_] * Tj[a_];
             v += acc;
@@ -529,7 +555,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
             raw = nxt;
         }
         // factor of the theta block of P_0 (np = 1: its reciprocal)
-        double Pt[NP][NP], L0[NP][NP];
+        real Pt[NP][NP], L0[NP][NP];
 #pragma unroll
         for (int x = 0; x < NP; ++x)
 #pragma unroll
@@ -555,7 +581,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
     const int li = lane < NS ? lane : NS - 1;
     auto solve = [&](int ods, int odu) __attribute__((always_inline)) {
-        double Acol[NS], Arow[NS], Bli[NU], Bl[NS][NU];  // Abar(:, li), Abar(li, :), Bbar(li, :), Bbar
+        real Acol[NS], Arow[NS], Bli[NU], Bl[NS][NU];  // Abar(:, li), Abar(li, :), Bbar(li, :), Bbar
 #pragma unroll
         for (int c = 0; c < NS; ++c) {
             Acol[c] = Abar(c, li);
@@ -565,8 +591,8 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         }
 #pragma unroll
         for (int x = 0; x < NU; ++x) Bli[x] = Bbar(li, x);
-        double qs[SPL][NS], qu[SPL][NU];
-        double gpe[NV];
+        real qs[SPL][NS], qu[SPL][NU];
+        real gpe[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) gpe[c] = W[L.gpe + c];
 #pragma unroll
@@ -577,14 +603,14 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
             for (int i = 0; i < NS; ++i) qs[j][i] = W[L.rs + kk * NS + i];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                double e = 0.0;
+                real e = 0.0;
                 e += W[L.ebox + (kk * NB + i) * 2];
                 e -= W[L.ebox + (kk * NB + i) * 2 + 1];
                 qs[j][i] += e;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                double e = W[L.ru + kk * NU + i];
+                real e = W[L.ru + kk * NU + i];
                 e += W[L.ebox + (kk * NB + NX + i) * 2];
                 e -= W[L.ebox + (kk * NB + NX + i) * 2 + 1];
                 qu[j][i] = e;
@@ -605,9 +631,9 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
-                const double* Pn = W + L.P + (k + 1) * PST;
-                const double* Kk = W + L.K + k * NU * NS;
-                double rek[NS], wk[NS], qtk[NS], Kl[NU][NS];
+                const real* Pn = W + L.P + (k + 1) * PST;
+                const real* Kk = W + L.K + k * NU * NS;
+                real rek[NS], wk[NS], qtk[NS], Kl[NU][NS];
 #pragma unroll
                 for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
 #pragma unroll
@@ -616,12 +642,12 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
                     for (int c = 0; c < NS; ++c) Kl[x][c] = Kk[x * NS + c];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double v = 0.0;
+                    real v = 0.0;
 #pragma unroll
                     for (int c = 0; c < NS; ++c) v += Pn[pk_idx(NS, i, c)] * rek[c];
                     wk[i] = v;
                     W[L.wv + k * NS + i] = v;
-                    double qq = qs[j][i];
+                    real qq = qs[j][i];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) qq += Kl[x][i] * qu[j][x];
                     qtk[i] = qq;
@@ -629,10 +655,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
                 // Phi_k = Abar + Bbar K_k, column i formed as in the factorisation
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double v = qtk[i];
+                    real v = qtk[i];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) {
-                        double ph = Abar(c, i);
+                        real ph = Abar(c, i);
 #pragma unroll
                         for (int x = 0; x < NU; ++x) ph += Bbar(c, x) * Kl[x][i];
                         v += ph * wk[c];
@@ -651,23 +677,23 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         // vector is broadcast with readlane (scalar registers); two register sets used
         // alternately (stages k, k-1), each refilled two stages ahead
         {
-            double p[NS];
+            real p[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) p[i] = W[L.pv + N * NS + i];
             // Phi_k column li = Abar(:, li) + Bbar K_k(:, li)
-            auto load_b = [&](int k, double (&kc)[NU], double& q) __attribute__((always_inline)) {
+            auto load_b = [&](int k, real (&kc)[NU], real& q) __attribute__((always_inline)) {
                 q = W[L.qt_xpi + k * NS + li];
 #pragma unroll
                 for (int x = 0; x < NU; ++x) kc[x] = W[L.K + k * NU * NS + x * NS + li];
             };
-            double k0[NU], q0, k1[NU], q1;
+            real k0[NU], q0, k1[NU], q1;
             load_b(N - 1, k0, q0);
             if (N >= 2) load_b(N - 2, k1, q1);
-            auto step_b = [&](int k, const double (&kc)[NU], double q) __attribute__((always_inline)) {
-                double acc = q;
+            auto step_b = [&](int k, const real (&kc)[NU], real q) __attribute__((always_inline)) {
+                real acc = q;
 #pragma unroll
                 for (int c = 0; c < NS; ++c) {
-                    double ph = Acol[c];
+                    real ph = Acol[c];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) ph += Bl[c][x] * kc[x];
                     acc += ph * p[c];
@@ -690,12 +716,12 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
-                double y[NS], r[NU];
+                real y[NS], r[NU];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) y[i] = W[L.pv + (k + 1) * NS + i] + W[L.wv + k * NS + i];
 #pragma unroll
                 for (int x = 0; x < NU; ++x) {
-                    double v = qu[j][x];
+                    real v = qu[j][x];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) v += Bbar(c, x) * y[c];
                     r[x] = -v;
@@ -705,7 +731,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
                 for (int x = 0; x < NU; ++x) kff[j][x] = r[x];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double v = W[L.re + k * NS + i];
+                    real v = W[L.re + k * NS + i];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) v += Bbar(i, x) * kff[j][x];
                     W[L.fv + k * NS + i] = v;
@@ -715,10 +741,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         wave_sync();
         // theta_0 step + forward sweep: lane i < NS computes entry i of ds_{k+1} = Phi_k ds_k + f_k
         {
-            double d[NS];
+            real d[NS];
 #pragma unroll
             for (int i = 0; i < NX; ++i) d[i] = 0.0;
-            double r0[NP];
+            real r0[NP];
 #pragma unroll
             for (int x = 0; x < NP; ++x) r0[x] = -W[L.pv + NX + x];
             chol_solve_small<NP>(W + L.L0, r0);
@@ -729,21 +755,21 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
                 for (int i = 0; i < NS; ++i) W[ods + i] = d[i];
             }
             // Phi_k row li = Abar(li, :) + Bbar(li, :) K_k
-            auto load_f = [&](int k, double (&kr)[NU][NS], double& f) __attribute__((always_inline)) {
+            auto load_f = [&](int k, real (&kr)[NU][NS], real& f) __attribute__((always_inline)) {
                 f = W[L.fv + k * NS + li];
 #pragma unroll
                 for (int x = 0; x < NU; ++x)
 #pragma unroll
                     for (int c = 0; c < NS; ++c) kr[x][c] = W[L.K + k * NU * NS + x * NS + c];
             };
-            double k0[NU][NS], f0, k1[NU][NS], f1;
+            real k0[NU][NS], f0, k1[NU][NS], f1;
             load_f(0, k0, f0);
             if (N >= 2) load_f(1, k1, f1);
-            auto step_f = [&](int k, const double (&kr)[NU][NS], double f) __attribute__((always_inline)) {
-                double acc = f;
+            auto step_f = [&](int k, const real (&kr)[NU][NS], real f) __attribute__((always_inline)) {
+                real acc = f;
 #pragma unroll
                 for (int c = 0; c < NS; ++c) {
-                    double ph = Arow[c];
+                    real ph = Arow[c];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) ph += Bli[x] * kr[x][c];
                     acc += ph * d[c];
@@ -766,10 +792,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
-                const double* Kk = W + L.K + k * NU * NS;
+                const real* Kk = W + L.K + k * NU * NS;
 #pragma unroll
                 for (int x = 0; x < NU; ++x) {
-                    double v = kff[j][x];
+                    real v = kff[j][x];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) v += Kk[x * NS + c] * W[ods + k * NS + c];
                     W[odu + k * NU + x] = v;
@@ -783,19 +809,19 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     };
 
     // primal/dual stage update by alpha along (ids, idu); dpi_k = P_k ds_k + p_k
-    auto update_stage = [&](double al, int ids, int idu) __attribute__((always_inline)) {
+    auto update_stage = [&](real al, int ids, int idu) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k > N) continue;
-            double dsk[NS];
+            real dsk[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) dsk[i] = W[ids + k * NS + i];
             if (k >= 1) {
-                const double* Pk = W + L.P + k * PST;
+                const real* Pk = W + L.P + k * PST;
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    double v = W[L.pv + k * NS + i];
+                    real v = W[L.pv + k * NS + i];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) v += Pk[pk_idx(NS, i, c)] * dsk[c];
                     pi[j][i] += al * v;
@@ -811,12 +837,12 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     };
 
     // ======================= initial point ==================================================
-    double feasA = 0, gsA = 0;
+    real feasA = 0, gsA = 0;
     write_state();
     stage_partials(feasA, gsA);
     BARRIER();                                            // I0: row-side tables of t = lam = 1
-    const double minv = 1.0 / fmax(X[X_CNT], 1.0);
-    const double bscale = fmax(x0max, X[X_BSR]);
+    const real minv = 1.0 / fmax(X[X_CNT], 1.0);
+    const real bscale = fmax(x0max, X[X_BSR]);
     combine();
     int flag = 0;
     if (!factor()) flag = -8;
@@ -830,7 +856,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
 
     // ======================= main loop ======================================================
     int it = 0;
-    double mu = 0.0, mu_min = INFINITY, stat = 0.0, feas = 0.0;
+    real mu = 0.0, mu_min = INFINITY, stat = 0.0, feas = 0.0;
     const int max_iter = a.max_iter;
     for (it = 0;; ++it) {
         BARRIER();                                        // B0: row multipliers / D / F'DF ready
@@ -847,6 +873,13 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         } else if (stat <= a.tol_stat * (1.0 + gsA) && feas <= a.tol_feas * (1.0 + bscale) &&
                    mu <= a.tol_comp) {
             flag = 1; stop = true;
+#ifdef BQP_F32
+        } else if (mu <= a.tol_comp && feas <= a.tol_feas * (1.0 + bscale) && isfinite(stat)) {
+            // fp32: complementarity and feasibility have converged; the stationarity residual
+            // sums terms of |P x| ~ 1e3 and is resolved only to fp32 round-off of those terms,
+            // and the next barrier factorisation (D = lam / t ~ 1/mu) would exceed fp32 range
+            flag = 1; stop = true;
+#endif
         } else if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) {
             flag = -8; stop = true;
         } else if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) {
@@ -871,7 +904,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
         BARRIER();                                        // B5: corrector direction out
         BARRIER();                                        // B6: step length ready
         STAMP(8);
-        const double al = X[X_ALPHA];
+        const real al = X[X_ALPHA];
         update_stage(al, L.dsc, L.duc);
         write_state();
         stage_partials(feasA, gsA);
@@ -879,7 +912,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
     }
 
     // ======================= outputs =======================================================
-    double fv = 0.0;
+    real fv = 0.0;
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
         const int k = lane + WAVE * j;
@@ -896,15 +929,15 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
 #pragma unroll
             for (int i = 0; i < NP; ++i) a.theta[(int64_t)inst * NP + i] = s[j][NX + i];
         }
-        const double* Hk = Hs + k * hstride;
-        double v[NV];
+        const real* Hk = Hs + k * hstride;
+        real v[NV];
 #pragma unroll
         for (int i = 0; i < NS; ++i) v[i] = s[j][i];
 #pragma unroll
         for (int i = 0; i < NU; ++i) v[NS + i] = (k < N) ? u[j][i] : 0.0;
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            double hv = 0.0;
+            real hv = 0.0;
 #pragma unroll
             for (int c = 0; c < NV; ++c) hv += Hk[i * NV + c] * v[c];
             fv += v[i] * (0.5 * hv + gterm(k, i));
@@ -931,19 +964,19 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, double* W, co
 // row wave
 // ==========================================================================================
 template <int NX, int NU, int NP, int SPL, int RPL>
-__device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, const QpLds& L,
-                                         const double* Fs, int lane, int inst) {
+__device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
+                                         const real* Fs, int lane, int inst) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     constexpr int NB = NX + NU;          // box slots per stage: x then u, each [upper, lower]
     const int N = a.N, mp = a.mp, kp = a.kp;
     constexpr int mpad = RPL * WAVE;     // polytope table stride (host sets a.mpad to the same)
-    double* X = W + L.xch;
+    real* X = W + L.xch;
     STAMP_DECL;
 
     // ---------------- box rows of stage k = lane + 64 j: bounds to LDS, presence mask -------
     unsigned msk[SPL];
-    double bsl = 0.0, mcount = 0.0;
+    real bsl = 0.0, mcount = 0.0;
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
         const int k = lane + WAVE * j;
@@ -951,7 +984,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
         msk[j] = 0;
 #pragma unroll
         for (int sl = 0; sl < NB; ++sl) {
-            double ub = INFINITY, lb = -INFINITY;
+            real ub = INFINITY, lb = -INFINITY;
             if (sl < NX) {
                 if (act && k > 0) {
                     if (a.xub) ub = a.xub[(int64_t)inst * a.sxb + (int64_t)k * NX + sl];
@@ -974,7 +1007,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     }
     auto pres = [&](int j, int sl, int h) __attribute__((always_inline)) -> bool { return (msk[j] >> (2 * sl + h)) & 1u; };
     // polytope rows l, l+64, ...
-    double* hpi = W + L.hp;
+    real* hpi = W + L.hp;
     {
         const double* hg = a.hp + (int64_t)inst * a.shp;
         for (int r = lane; r < mp; r += WAVE) hpi[r] = hg[r];
@@ -987,14 +1020,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     mcount = wsum(mcount);
     bsl = wmax(bsl);
     if (lane == 0) { X[X_CNT] = mcount; X[X_BSR] = bsl; }
-    const double minv = 1.0 / fmax(mcount, 1.0);
-    auto fdot = [&](int r, const double (&v)[NV]) __attribute__((always_inline)) -> double {
-        double acc = 0.0;
+    const real minv = 1.0 / fmax(mcount, 1.0);
+    auto fdot = [&](int r, const real (&v)[NV]) __attribute__((always_inline)) -> real {
+        real acc = 0.0;
 #pragma unroll
         for (int c = 0; c < NV; ++c) acc += Fs[c * mpad + r] * v[c];
         return acc;
     };
-    auto load_v = [&](double (&v)[NV], int bs, int bu) __attribute__((always_inline)) {
+    auto load_v = [&](real (&v)[NV], int bs, int bu) __attribute__((always_inline)) {
 #pragma unroll
         for (int c = 0; c < NS; ++c) v[c] = W[bs + kp * NS + c];
 #pragma unroll
@@ -1003,8 +1036,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 
     // row state: slack t, multiplier lam, 1/t; polytope rows also their residual ri (box-row
     // residuals are re-formed from the LDS stage vector and bounds when needed)
-    double tx[SPL][NB][2], lx[SPL][NB][2];
-    double tp[RPL], lp[RPL], rp[RPL];
+    real tx[SPL][NB][2], lx[SPL][NB][2];
+    real tp[RPL], lp[RPL], rp[RPL];
 #pragma unroll
     for (int j = 0; j < SPL; ++j)
 #pragma unroll
@@ -1017,7 +1050,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     // ---- multiplier-side tables (depend on t, lam only): box multipliers, Fp'lam, 1/t,
     //      D = lam/t per stage, F'DF, sum t.lam ----
     auto lam_side = [&]() __attribute__((always_inline)) {
-        double cs = 0.0;
+        real cs = 0.0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1026,7 +1059,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                 for (int sl = 0; sl < NB; ++sl) {
                     W[L.blam + (k * NB + sl) * 2] = pres(j, sl, 0) ? lx[j][sl][0] : 0.0;
                     W[L.blam + (k * NB + sl) * 2 + 1] = pres(j, sl, 1) ? lx[j][sl][1] : 0.0;
-                    double d = 0;
+                    real d = 0;
                     if (pres(j, sl, 0)) d += lx[j][sl][0] * frcp(tx[j][sl][0]);
                     if (pres(j, sl, 1)) d += lx[j][sl][1] * frcp(tx[j][sl][1]);
                     W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
@@ -1037,8 +1070,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                 for (int i = NX; i < NS; ++i) W[L.Dx + k * NV + i] = 0.0;
             }
         }
-        double gpp[NV];
-        double fd[NV * (NV + 1) / 2];
+        real gpp[NV];
+        real fd[NV * (NV + 1) / 2];
 #pragma unroll
         for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
 #pragma unroll
@@ -1048,17 +1081,17 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r < mp) {
-                double f[NV];
+                real f[NV];
 #pragma unroll
                 for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpp[c] += f[c] * lp[q];
                 cs += tp[q] * lp[q];
-                const double d = lp[q] * frcp(tp[q]);
+                const real d = lp[q] * frcp(tp[q]);
                 int idx = 0;
 #pragma unroll
                 for (int i2 = 0; i2 < NV; ++i2) {
-                    const double di = d * f[i2];
+                    const real di = d * f[i2];
 #pragma unroll
                     for (int j2 = i2; j2 < NV; ++j2) fd[idx++] += di * f[j2];
                 }
@@ -1087,14 +1120,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 
     // box-row residual of the current iterate: v + t - ub (upper), -v + t + lb (lower); the
     // stage vector in LDS is the iterate's until the stage wave writes the next one (after B6)
-    auto box_res = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> double {
-        const double v = sl < NX ? W[L.xs + k * NS + sl] : W[L.xu + k * NU + (sl - NX)];
-        const double b = W[L.bnd + (k * NB + sl) * 2 + h];
+    auto box_res = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> real {
+        const real v = sl < NX ? W[L.xs + k * NS + sl] : W[L.xu + k * NU + (sl - NX)];
+        const real b = W[L.bnd + (k * NB + sl) * 2 + h];
         return h == 0 ? v + tx[j][sl][0] - b : -v + tx[j][sl][1] + b;
     };
     // ---- row residuals of the current iterate (box: +-v + t -+ b; polytope: Fp v + t - hp) ----
     auto row_residuals = [&]() __attribute__((always_inline)) {
-        double fe = 0.0;
+        real fe = 0.0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1105,14 +1138,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                 for (int h = 0; h < 2; ++h)
                     if (pres(j, sl, h)) fe = fmax(fe, fabs(box_res(j, k, sl, h)));
         }
-        double vp[NV];
+        real vp[NV];
         load_v(vp, L.xs, L.xu);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r < mp) {
-                const double ri = fdot(r, vp) + tp[q] - hpi[r];
+                const real ri = fdot(r, vp) + tp[q] - hpi[r];
                 rp[q] = ri;
                 fe = fmax(fe, fabs(ri));
             }
@@ -1122,23 +1155,23 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     };
 
     // complementarity right-hand side of a row: predictor t*lam, corrector + dt_a*dlam_a - sigma*mu
-    auto rcv = [&](double t, double l, double pr, bool corr, double smu) __attribute__((always_inline)) -> double {
+    auto rcv = [&](real t, real l, real pr, bool corr, real smu) __attribute__((always_inline)) -> real {
         return corr ? t * l + pr - smu : t * l;
     };
     // box-row step dt = -ri - (+-dv) along the direction (ids, idu)
-    auto box_dir = [&](int j, int k, int sl, int h, int ids, int idu) __attribute__((always_inline)) -> double {
-        const double dv = sl < NX ? W[ids + k * NS + sl] : W[idu + k * NU + (sl - NX)];
+    auto box_dir = [&](int j, int k, int sl, int h, int ids, int idu) __attribute__((always_inline)) -> real {
+        const real dv = sl < NX ? W[ids + k * NS + sl] : W[idu + k * NU + (sl - NX)];
         return -box_res(j, k, sl, h) - (h == 0 ? dv : -dv);
     };
     // box-row predictor product dt_a * dlam_a (recomputed from the predictor direction)
-    auto box_pred_prod = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> double {
-        const double dt = box_dir(j, k, sl, h, L.dsv, L.duv);
-        const double dl = (-(tx[j][sl][h] * lx[j][sl][h]) - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
+    auto box_pred_prod = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> real {
+        const real dt = box_dir(j, k, sl, h, L.dsv, L.duv);
+        const real dl = (-(tx[j][sl][h] * lx[j][sl][h]) - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
         return dt * dl;
     };
 
     // ---- right-hand-side terms (lam o ri - rc)/t: box [upper, lower] per stage, Fp'e ----
-    auto rhs_terms = [&](bool corr, double smu) __attribute__((always_inline)) {
+    auto rhs_terms = [&](bool corr, real smu) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1147,15 +1180,15 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             for (int sl = 0; sl < NB; ++sl)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    double e = 0.0;
+                    real e = 0.0;
                     if (pres(j, sl, h)) {
-                        const double pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
+                        const real pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
                         e = (lx[j][sl][h] * box_res(j, k, sl, h) - rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu)) * frcp(tx[j][sl][h]);
                     }
                     W[L.ebox + (k * NB + sl) * 2 + h] = e;
                 }
         }
-        double gpe[NV];
+        real gpe[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) gpe[c] = 0.0;
 #pragma unroll
@@ -1163,8 +1196,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r < mp) {
-                const double pr = corr ? W[L.prp + r] : 0.0;
-                const double e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * frcp(tp[q]);
+                const real pr = corr ? W[L.prp + r] : 0.0;
+                const real e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * frcp(tp[q]);
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpe[c] += Fs[c * mpad + r] * e;
             }
@@ -1180,8 +1213,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     // ---- row passes along the direction (ids, idu): dt = -ri - C dv, dlam = (-rc - lam dt)/t.
     //      mode 0: ratio max(-dt/t, -dlam/lam); 1: sum (t+al dt)(lam+al dlam) and store the
     //      polytope predictor products; 2: apply t += al dt, lam += al dlam ----
-    auto row_pass = [&](int mode, bool corr, double smu, double al, int ids, int idu) __attribute__((always_inline)) -> double {
-        double acc = 0.0;
+    auto row_pass = [&](int mode, bool corr, real smu, real al, int ids, int idu) __attribute__((always_inline)) -> real {
+        real acc = 0.0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1191,10 +1224,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (!pres(j, sl, h)) continue;
-                    const double pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
-                    const double rc = rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu);
-                    const double dt = box_dir(j, k, sl, h, ids, idu);
-                    const double dl = (-rc - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
+                    const real pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
+                    const real rc = rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu);
+                    const real dt = box_dir(j, k, sl, h, ids, idu);
+                    const real dl = (-rc - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
                     if (mode == 0) {
                         acc = fmax(acc, -dt * frcp(tx[j][sl][h]));
                         acc = fmax(acc, -dl * frcp(lx[j][sl][h]));
@@ -1206,17 +1239,17 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                     }
                 }
         }
-        double dvp[NV];
+        real dvp[NV];
         load_v(dvp, ids, idu);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r >= mp) continue;
-            const double pr = corr ? W[L.prp + r] : 0.0;
-            const double rc = rcv(tp[q], lp[q], pr, corr, smu);
-            const double dt = -rp[q] - fdot(r, dvp);
-            const double dl = (-rc - lp[q] * dt) * frcp(tp[q]);
+            const real pr = corr ? W[L.prp + r] : 0.0;
+            const real rc = rcv(tp[q], lp[q], pr, corr, smu);
+            const real dt = -rp[q] - fdot(r, dvp);
+            const real dl = (-rc - lp[q] * dt) * frcp(tp[q]);
             if (mode == 0) {
                 acc = fmax(acc, -dt * frcp(tp[q]));
                 acc = fmax(acc, -dl * frcp(lp[q]));
@@ -1238,8 +1271,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     //      dt dlam, and the corrector terms WITHOUT their sigma mu part,
     //      e0 = (lam ri - t lam - dt dlam)/t (box slots in place, polytope rows as Fp'e0), plus
     //      Fp'(1/t): e = e0 + sigma mu / t once sigma is known (rhs_corr_finish) ----
-    auto comp_rhs0 = [&](double al, double (&gpe0)[NV], double (&gpi)[NV]) __attribute__((always_inline)) -> double {
-        double acc = 0.0;
+    auto comp_rhs0 = [&](real al, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) -> real {
+        real acc = 0.0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1248,13 +1281,13 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             for (int sl = 0; sl < NB; ++sl)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    double e0 = 0.0;
+                    real e0 = 0.0;
                     if (pres(j, sl, h)) {
-                        const double t = tx[j][sl][h], l = lx[j][sl][h];
-                        const double it = frcp(t);
-                        const double rc = t * l;
-                        const double dt = box_dir(j, k, sl, h, L.dsv, L.duv);
-                        const double dl = (-rc - l * dt) * it;
+                        const real t = tx[j][sl][h], l = lx[j][sl][h];
+                        const real it = frcp(t);
+                        const real rc = t * l;
+                        const real dt = box_dir(j, k, sl, h, L.dsv, L.duv);
+                        const real dl = (-rc - l * dt) * it;
                         acc += (t + al * dt) * (l + al * dl);
                         e0 = (l * box_res(j, k, sl, h) - (rc + dt * dl)) * it;
                     }
@@ -1263,34 +1296,34 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
         }
 #pragma unroll
         for (int c = 0; c < NV; ++c) { gpe0[c] = 0.0; gpi[c] = 0.0; }
-        double dvp[NV];
+        real dvp[NV];
         load_v(dvp, L.dsv, L.duv);
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r >= mp) continue;
-            double f[NV];
+            real f[NV];
 #pragma unroll
             for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
-            double fd = 0.0;
+            real fd = 0.0;
 #pragma unroll
             for (int c = 0; c < NV; ++c) fd += f[c] * dvp[c];
-            const double t = tp[q], l = lp[q];
-            const double it = frcp(t);
-            const double rc = t * l;
-            const double dt = -rp[q] - fd;
-            const double dl = (-rc - l * dt) * it;
+            const real t = tp[q], l = lp[q];
+            const real it = frcp(t);
+            const real rc = t * l;
+            const real dt = -rp[q] - fd;
+            const real dl = (-rc - l * dt) * it;
             acc += (t + al * dt) * (l + al * dl);
-            const double pr = dt * dl;
+            const real pr = dt * dl;
             W[L.prp + r] = pr;
-            const double e0 = (l * rp[q] - (rc + pr)) * it;
+            const real e0 = (l * rp[q] - (rc + pr)) * it;
 #pragma unroll
             for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }
         }
         return wsum(acc);
     };
-    auto rhs_corr_finish = [&](double smu, double (&gpe0)[NV], double (&gpi)[NV]) __attribute__((always_inline)) {
+    auto rhs_corr_finish = [&](real smu, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1301,7 +1334,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
                 for (int h = 0; h < 2; ++h)
                     if (pres(j, sl, h)) W[L.ebox + (k * NB + sl) * 2 + h] += smu * frcp(tx[j][sl][h]);
         }
-        double g[NV];
+        real g[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) g[c] = wsum(gpe0[c]) + smu * wsum(gpi[c]);
         if (lane == 0) {
@@ -1320,7 +1353,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
     {
         // t~ = t + dt (t = 1) at the unit-scaled least-squares point; lam~ = -t~; shift
         row_pass(2, false, 0.0, 1.0, L.dsv, L.duv);
-        double tmin = INFINITY, tmax = -INFINITY;
+        real tmin = INFINITY, tmax = -INFINITY;
 #pragma unroll
         for (int j = 0; j < SPL; ++j)
 #pragma unroll
@@ -1333,22 +1366,22 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
             if (prow(q)) { tmin = fmin(tmin, tp[q]); tmax = fmax(tmax, tp[q]); }
         tmin = wmin(tmin);
         tmax = wmax(tmax);
-        const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
-        const double shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
+        const real shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
+        const real shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j)
 #pragma unroll
             for (int sl = 0; sl < NB; ++sl)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const double t = tx[j][sl][h];
+                    const real t = tx[j][sl][h];
                     const bool pr = pres(j, sl, h);
                     tx[j][sl][h] = pr ? t + shp : 1.0;
                     lx[j][sl][h] = pr ? -t + shd : 0.0;
                 }
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            const double t = tp[q];
+            const real t = tp[q];
             const bool pr = prow(q);
             tp[q] = pr ? t + shp : 1.0;
             lp[q] = pr ? -t + shd : 0.0;
@@ -1371,21 +1404,21 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, double* W, cons
         if (X[X_STOP] != 0.0) break;
         BARRIER();                                        // B3: predictor direction in (dsv, duv)
         STAMP(4);
-        const double mu = X[X_CS] * minv;
-        const double rm_a = row_pass(0, false, 0.0, 0.0, L.dsv, L.duv);
-        const double al_aff = rm_a > 1.0 ? 1.0 / rm_a : 1.0;
-        double gpe0[NV], gpi[NV];
-        const double mua = comp_rhs0(al_aff, gpe0, gpi) * minv;
-        double sg = mua / mu;
+        const real mu = X[X_CS] * minv;
+        const real rm_a = row_pass(0, false, 0.0, 0.0, L.dsv, L.duv);
+        const real al_aff = rm_a > 1.0 ? 1.0 / rm_a : 1.0;
+        real gpe0[NV], gpi[NV];
+        const real mua = comp_rhs0(al_aff, gpe0, gpi) * minv;
+        real sg = mua / mu;
         sg = sg * sg * sg;
-        const double smu = sg * mu;
+        const real smu = sg * mu;
         rhs_corr_finish(smu, gpe0, gpi);
         STAMP(5);
         BARRIER();                                        // B4
         BARRIER();                                        // B5: corrector direction in (dsc, duc)
         STAMP(6);
-        const double rm = row_pass(0, true, smu, 0.0, L.dsc, L.duc);
-        double al = (rm > 1.0 ? 1.0 / rm : 1.0) * a.tau;
+        const real rm = row_pass(0, true, smu, 0.0, L.dsc, L.duc);
+        real al = (rm > 1.0 ? 1.0 / rm : 1.0) * a.tau;
         if (al > 1.0) al = 1.0;
         if (lane == 0) X[X_ALPHA] = al;
         row_pass(2, true, smu, al, L.dsc, L.duc);
@@ -1434,14 +1467,15 @@ template <int NX, int NU, int NP, int SPL, int RPL>
 __global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
-    extern __shared__ double lds[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    real* lds = reinterpret_cast<real*>(lds_raw);
     const int N = a.N;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int qpb = a.wpb;
     // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
-    double* Hs = lds;
-    double* Fs = lds + (N + 1) * a.hstride;
+    real* Hs = lds;
+    real* Fs = lds + (N + 1) * a.hstride;
     for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
     for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
     __syncthreads();
@@ -1450,23 +1484,34 @@ __global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
     const int inst = blockIdx.x * qpb + slot;
     if (inst >= a.batch) return;       // both waves of an empty slot leave together
     const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad);
-    double* W = lds + a.shared_doubles + slot * L.total;
+    real* W = lds + a.shared_doubles + slot * L.total;
     if (!rowwave)
         stage_wave<NX, NU, NP, SPL>(a, W, L, Hs, lane, inst);
     else
         row_wave<NX, NU, NP, SPL, RPL>(a, W, L, Fs, lane, inst);
 }
 
+}  // namespace dp / sp
+
 // ------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------------
-int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad) {
-    return QpLds::make(N, nx, nu, np, mpad).total;
+// LDS elements (of the instantiation's precision) per instance
+int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad) {
+#ifdef BQP_F32
+    return sp::QpLds::make(N, nx, nu, np, mpad).total;
+#else
+    return dp::QpLds::make(N, nx, nu, np, mpad).total;
+#endif
 }
 
 template <int NX, int NU, int NP, int SPL, int RPL>
 static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipStream_t st) {
-    auto k = ocp_ipm_kernel<NX, NU, NP, SPL, RPL>;
+#ifdef BQP_F32
+    auto k = sp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL>;
+#else
+    auto k = dp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL>;
+#endif
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -1493,6 +1538,7 @@ static hipError_t launch_spl(const OcpKernelArgs& a, int spl, int rpl, int block
     return hipErrorInvalidValue;
 }
 
+#ifndef BQP_F32
 bool ocp_supported(int nx, int nu, int np) {
     return (nx == 4 && nu == 1 && np == 1) || (nx == 2 && nu == 2 && np == 2);
 }
@@ -1505,12 +1551,14 @@ int ocp_rpl_for(int mp) {
     return -1;
 }
 
-hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st) {
+#endif
+
+hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st) {
     const int spl = (a.N + 1 <= 64) ? 1 : 2;
     const int rpl = ocp_rpl_for(a.mp);
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
-    const size_t lds = sizeof(double) * ((size_t)a.shared_doubles +
-                                         (size_t)a.wpb * ocp_wave_lds_doubles(a.N, nx, nu, np, a.mpad));
+    const size_t lds = sizeof(real) * ((size_t)a.shared_doubles +
+                                       (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad));
 #ifdef BQP_ISA_ONLY_MG10
     // codegen inspection build (make isa): the MG N<64, 616-row instance only
     if (nx == 4 && nu == 1 && np == 1 && spl == 1 && rpl == 10) return launch_t<4, 1, 1, 1, 10>(a, blocks, lds, st);

@@ -60,4 +60,37 @@ __device__ __forceinline__ double rl(double v, int src) {
     return __builtin_bit_cast(double, r);
 }
 
+// fp32 overloads (the structured kernel's fp32 instantiation, bqp_ocp_f32.hip)
+template <int CTRL, int ROWM>
+__device__ __forceinline__ float dpp_mov(float old, float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                  __builtin_bit_cast(int, v), CTRL,
+                                                                  ROWM, 0xf, false));
+}
+__device__ __forceinline__ float lane63(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ float wsum(float v) {
+    v += dpp_mov<0xB1, 0xf>(0.0f, v);
+    v += dpp_mov<0x4E, 0xf>(0.0f, v);
+    v += dpp_mov<0x141, 0xf>(0.0f, v);
+    v += dpp_mov<0x140, 0xf>(0.0f, v);
+    v += dpp_mov<0x142, 0xa>(0.0f, v);
+    v += dpp_mov<0x143, 0xc>(0.0f, v);
+    return lane63(v);
+}
+__device__ __forceinline__ float wmax(float v) {
+    v = fmaxf(v, dpp_mov<0xB1, 0xf>(-INFINITY, v));
+    v = fmaxf(v, dpp_mov<0x4E, 0xf>(-INFINITY, v));
+    v = fmaxf(v, dpp_mov<0x141, 0xf>(-INFINITY, v));
+    v = fmaxf(v, dpp_mov<0x140, 0xf>(-INFINITY, v));
+    v = fmaxf(v, dpp_mov<0x142, 0xa>(-INFINITY, v));
+    v = fmaxf(v, dpp_mov<0x143, 0xc>(-INFINITY, v));
+    return lane63(v);
+}
+__device__ __forceinline__ float wmin(float v) { return -wmax(-v); }
+__device__ __forceinline__ float rl(float v, int src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
 }  // namespace bqp

@@ -13,7 +13,7 @@
 //               tests, mu_aff / sigma, and the slack/multiplier updates.
 //
 // The waves exchange per-stage tables and scalars through the instance's LDS slot and meet at
-// seven workgroup barriers per iteration (B0..B6 below; I0..I3 for the starting point); both waves take the same decisions
+// six workgroup barriers per iteration (B0, B2..B6 below; I0..I3 for the starting point); both waves take the same decisions
 // from the same exchanged values, so the barrier sequence is identical and an instance whose
 // iteration ends leaves the loop on both waves at the same barrier (terminated waves drop out
 // of s_barrier).  Each wave keeps only its own state in registers, and the row work that does
@@ -859,11 +859,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     real mu = 0.0, mu_min = INFINITY, stat = 0.0, feas = 0.0;
     const int max_iter = a.max_iter;
     for (it = 0;; ++it) {
-        BARRIER();                                        // B0: row multipliers / D / F'DF ready
+        BARRIER();                                        // B0: row multipliers / D / F'DF, row residual norm, comp sum ready
         STAMP(0);
         stat = combine();
         STAMP(1);
-        BARRIER();                                        // B1: row residual norm, comp sum
         STAMP(2);
         feas = fmax(feasA, X[X_FEASB]);
         mu = X[X_CS] * minv;
@@ -1234,6 +1233,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                     } else if (mode == 1) {
                         acc += (tx[j][sl][h] + al * dt) * (lx[j][sl][h] + al * dl);
                     } else {
+                        // residual of the stepped iterate: r + al (+-dv + dt) = (1 - al) r
+                        acc = fmax(acc, fabs((1.0 - al) * box_res(j, k, sl, h)));
                         tx[j][sl][h] += al * dt;
                         lx[j][sl][h] += al * dl;
                     }
@@ -1248,7 +1249,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             if (r >= mp) continue;
             const real pr = corr ? W[L.prp + r] : 0.0;
             const real rc = rcv(tp[q], lp[q], pr, corr, smu);
-            const real dt = -rp[q] - fdot(r, dvp);
+            const real fd = fdot(r, dvp);
+            const real dt = -rp[q] - fd;
             const real dl = (-rc - lp[q] * dt) * frcp(tp[q]);
             if (mode == 0) {
                 acc = fmax(acc, -dt * frcp(tp[q]));
@@ -1257,13 +1259,17 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 acc += (tp[q] + al * dt) * (lp[q] + al * dl);
                 W[L.prp + r] = dt * dl;
             } else {
+                // the polytope residual Fp v + t - hp of the stepped iterate, by the linear
+                // update r + al (Fp dv + dt): the next iteration needs no residual pass (and
+                // no barrier) before its factorisation
+                rp[q] += al * (fd + dt);
+                acc = fmax(acc, fabs(rp[q]));
                 tp[q] += al * dt;
                 lp[q] += al * dl;
             }
         }
-        if (mode == 0) return wmax(acc);
         if (mode == 1) return wsum(acc);
-        return 0.0;
+        return wmax(acc);   // mode 0: max ratio; mode 2: max |row residual| after the step
     };
 
     // ---- predictor pass 2 fused with the corrector right-hand side: the complementarity sum
@@ -1368,6 +1374,23 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         tmax = wmax(tmax);
         const real shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
         const real shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
+        {
+            // residuals of the shifted start: the full step zeroes them (linear rows), the
+            // positivity shift of t adds shp to every present row
+            real fe = 0.0;
+#pragma unroll
+            for (int j = 0; j < SPL; ++j)
+#pragma unroll
+                for (int sl = 0; sl < NB; ++sl)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        if (pres(j, sl, h)) fe = fmax(fe, fabs(shp));
+#pragma unroll
+            for (int q = 0; q < RPL; ++q)
+                if (prow(q)) { rp[q] += shp; fe = fmax(fe, fabs(rp[q])); }
+            fe = wmax(fe);
+            if (lane == 0) X[X_FEASB] = fe;
+        }
 #pragma unroll
         for (int j = 0; j < SPL; ++j)
 #pragma unroll
@@ -1394,9 +1417,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     for (;;) {
         BARRIER();                                        // B0
         STAMP(0);
-        row_residuals();
         STAMP(1);
-        BARRIER();                                        // B1
         rhs_terms(false, 0.0);
         STAMP(2);
         BARRIER();                                        // B2
@@ -1421,7 +1442,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         real al = (rm > 1.0 ? 1.0 / rm : 1.0) * a.tau;
         if (al > 1.0) al = 1.0;
         if (lane == 0) X[X_ALPHA] = al;
-        row_pass(2, true, smu, al, L.dsc, L.duc);
+        const real fe = row_pass(2, true, smu, al, L.dsc, L.duc);
+        if (lane == 0) X[X_FEASB] = fe;                   // row residual norm of the new iterate
         STAMP(7);
         BARRIER();                                        // B6
         lam_side();

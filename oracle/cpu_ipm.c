@@ -43,6 +43,10 @@ typedef struct {
     double *Dx, *Du, *FD;
     double *itx, *ilx, *itu, *ilu, *itp, *ilp;   /* 1/t, 1/lam (once per iteration) */
     double P0inv[MAXNS * MAXNS];
+    /* row residuals carried by the linear update r+ = r + a (C dv + dt) after the start, as the
+     * kernel's row wave does (no residual pass before the factorisation); fe_rows is their norm */
+    int rip_live;
+    double fe_rows;
 } work_t;
 
 static int perm_of(const prob_t* P, int i) {
@@ -188,7 +192,7 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
                 a += F[j] * v[j];
                 gp[j] += F[j] * W->lp[r];
             }
-            W->rip[r] = a;
+            if (!W->rip_live) W->rip[r] = a;
             cs += W->tp[r] * W->lp[r]; ++mc;
         }
         for (int i = 0; i < ns; ++i) W->rs[kp * ns + i] += gp[i];
@@ -202,11 +206,15 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
         for (int i = 0; i < nu; ++i) st = fmax(st, fabs(W->ru[k * nu + i]));
         for (int i = 0; i < ns; ++i) fe = fmax(fe, fabs(W->re[k * ns + i]));
     }
-    for (int k = 0; k <= N; ++k)
-        for (int i = 0; i < 2 * nx; ++i) fe = fmax(fe, fabs(W->rix[k * nx * 2 + i]));
-    for (int k = 0; k < N; ++k)
-        for (int i = 0; i < 2 * nu; ++i) fe = fmax(fe, fabs(W->riu[k * nu * 2 + i]));
-    for (int r = 0; r < P->mp; ++r) fe = fmax(fe, fabs(W->rip[r]));
+    if (W->rip_live) {
+        fe = fmax(fe, W->fe_rows);
+    } else {
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < 2 * nx; ++i) fe = fmax(fe, fabs(W->rix[k * nx * 2 + i]));
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < 2 * nu; ++i) fe = fmax(fe, fabs(W->riu[k * nu * 2 + i]));
+        for (int r = 0; r < P->mp; ++r) fe = fmax(fe, fabs(W->rip[r]));
+    }
     *stat = st; *feas = fe; *musum = cs; *mcount = mc; *gscale = gs;
 }
 
@@ -551,8 +559,20 @@ typedef struct {
     double tol_stat, tol_feas, tol_comp, tau;
 } opts_t;
 
+/* Fp(r,:) [ds_kp; du_kp] in the kernel's order (fdot) */
+static double poly_fdv(const prob_t* P, const work_t* W, int r) {
+    const int ns = P->ns, nu = P->nu, nv = P->nv, kp = P->kp;
+    const double* F = P->Fp + (size_t)r * nv;
+    double acc = 0.0;
+    for (int j = 0; j < ns; ++j) acc += F[j] * W->ds[kp * ns + j];
+    for (int j = 0; j < nu; ++j) acc += F[ns + j] * ((kp < P->N) ? W->du[kp * nu + j] : 0.0);
+    return acc;
+}
+
 static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, double* kkt) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns;
+    W->rip_live = 0;
+    W->fe_rows = 0.0;
     const int nxr = (N + 1) * nx * 2, nur = N * nu * 2;
     double stat, feas, cs, gs;
     int mc;
@@ -622,6 +642,26 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
                     W->tu[o] = t + shp; W->lu[o] = -t + shd;
                 } else { W->tu[o] = 1.0; W->lu[o] = 0.0; }
             }
+    {
+        /* residuals of the shifted start (the kernel's update): full step, then + shp */
+        double fe = 0.0;
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < nx; ++i)
+                for (int h = 0; h < 2; ++h)
+                    if (PRESENT_X(k, i, h)) fe = fmax(fe, fabs(shp));
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i)
+                for (int h = 0; h < 2; ++h)
+                    if (PRESENT_U(k, i, h)) fe = fmax(fe, fabs(shp));
+        for (int r = 0; r < P->mp; ++r) {
+            const double fd = poly_fdv(P, W, r);
+            W->rip[r] += 1.0 * (fd + W->dtp[r]);
+            W->rip[r] += shp;
+            fe = fmax(fe, fabs(W->rip[r]));
+        }
+        W->fe_rows = fe;
+        W->rip_live = 1;
+    }
     for (int r = 0; r < P->mp; ++r) {
         double t = 1.0 + W->dtp[r];
         W->tp[r] = t + shp; W->lp[r] = -t + shd;
@@ -652,6 +692,24 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         solve_kkt(P, W, rcx, rcu, rcp);
         a = max_step(P, W) * op->tau;
         if (a > 1.0) a = 1.0;
+        {
+            /* row residuals of the stepped iterate (the kernel's linear update) */
+            double fe = 0.0;
+            for (int k = 0; k <= N; ++k)
+                for (int i = 0; i < nx; ++i)
+                    for (int h = 0; h < 2; ++h)
+                        if (PRESENT_X(k, i, h)) fe = fmax(fe, fabs((1.0 - a) * W->rix[(k * nx + i) * 2 + h]));
+            for (int k = 0; k < N; ++k)
+                for (int i = 0; i < nu; ++i)
+                    for (int h = 0; h < 2; ++h)
+                        if (PRESENT_U(k, i, h)) fe = fmax(fe, fabs((1.0 - a) * W->riu[(k * nu + i) * 2 + h]));
+            for (int r = 0; r < P->mp; ++r) {
+                const double fd = poly_fdv(P, W, r);
+                W->rip[r] += a * (fd + W->dtp[r]);
+                fe = fmax(fe, fabs(W->rip[r]));
+            }
+            W->fe_rows = fe;
+        }
         for (int i = 0; i < (N + 1) * ns; ++i) { W->s[i] += a * W->ds[i]; W->pi[i] += a * W->dpi[i]; }
         for (int i = 0; i < N * nu; ++i) W->u[i] += a * W->du[i];
         for (int k = 0; k <= N; ++k)

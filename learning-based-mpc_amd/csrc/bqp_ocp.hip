@@ -1210,12 +1210,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 for (int c = 0; c < NV; ++c) gpe[c] += Fs[c * mpad + r] * e;
             }
         }
-#pragma unroll
-        for (int c = 0; c < NV; ++c) gpe[c] = wsum(gpe[c]);
-        if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < NV; ++c) W[L.gpe + c] = gpe[c];
-        }
+        const real tot = wsum_t(gpe, lane);           // lane c < NV: Fp'e (c)
+        if (lane < NV) W[L.gpe + lane] = tot;
     };
 
     // ---- row passes along the direction (ids, idu): dt = -ri - C dv, dlam = (-rc - lam dt)/t.

@@ -15,9 +15,11 @@ Other configs - measured the same way, reported in DESIGN.md:
       contiguously over the ranks (strong scaling), per-instance models;
   C5  long-horizon MG DMS tracking LMPC (F2), N=100, 8192 per GPU, fp64 (no fp32 path yet).
 
-N > 1: launched by torch.distributed.run, one rank per GPU; each rank solves its own shard
-(no collective in the timed region); the first moves and exit flags are all-gathered once
-after timing (RCCL over xGMI) - bqp.dist.
+N > 1: one rank per GPU.  Without a launcher (`python bench.py --gpus N`) this script starts
+torch.distributed.run itself as a child process before touching the GPU; each rank solves its
+own shard (no collective in the timed region); the first moves and exit flags are all-gathered
+once after timing (RCCL over xGMI) - bqp.dist.  `--dry-run` rehearses the same multi-rank code
+on CPU (gloo, stub solver; tests/test_bench_dist.py).
 
 Prints ONE JSON line (rank 0): value = QP-steps/s over all ranks; roofline of the solve kernel
 (algorithmic FP64 flops / kernel time from hipEvents on the launch stream; HBM traffic from the
@@ -163,6 +165,132 @@ def cpu_reference(prob, sample, threads, timed):
                        '(same IPM, fp64, -O3 -march=native, OpenMP)' % (len(Xa), n1)), kref
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """bench.py --gpus N without a torch.distributed launcher: start N ranks (one process per
+    GPU) through torch.distributed.run as a child process - before this process touches the
+    GPU - and exit with its status.  Rank 0 of the children prints the JSON line."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(cmd, env=env)
+
+
+class GpuSolver:
+    """One batched structured solve per step through bqp_solve_ocp_batched_device (inputs and
+    outputs resident in HBM, caller stream)."""
+
+    def __init__(self, wl, local, precision):
+        import torch
+        import bqp
+        from bqp import _lib
+        from bqp.ocp import _cm
+        self.torch, self._lib = torch, _lib
+        prob, X = wl['prob'], wl['X']
+        self.B = B = X.shape[0]
+        N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
+        nv = nx + nu + npar
+        dev = self.dev = torch.device('cuda', local)
+
+        def dt(a):
+            return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+
+        self.keep = [dt(_cm(prob.A) if wl['A'] is None else _cm(wl['A'])),
+                     dt(_cm(prob.B) if wl['B'] is None else _cm(wl['B'])),
+                     dt(prob.w if wl['w'] is None else wl['w']), dt(_cm(prob.W)), dt(prob.c),
+                     dt(prob.xlb), dt(prob.xub), dt(prob.ulb), dt(prob.uub), dt(_cm(prob.Fp)),
+                     dt(prob.hp), dt(X)]
+        dA, dB, dw, dW, dc, dxlb, dxub, dulb, duub, dF, dh, dx0 = self.keep
+        P = _lib.dptr
+        self.data = _lib.OcpData(A=P(dA), B=P(dB), c=P(dc), W=P(dW), w=P(dw), xlb=P(dxlb),
+                                 xub=P(dxub), ulb=P(dulb), uub=P(duub), Fp=P(dF), hp=P(dh),
+                                 x0=P(dx0), sA=0 if wl['A'] is None else nx * nx,
+                                 sB=0 if wl['B'] is None else nx * nu, sc=0, sW=0,
+                                 sw=0 if wl['w'] is None else (N + 1) * nv, sxb=0, sub=0,
+                                 sFp=0, shp=0, sx0=nx)
+        self.dims = _lib.OcpDims(nx, nu, npar, N, mp, prob.poly_stage)
+        self.ox = torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev)
+        self.ou = torch.empty((B, N, nu), dtype=torch.float64, device=dev)
+        self.ot = torch.empty((B, npar), dtype=torch.float64, device=dev)
+        self.of = torch.empty((B,), dtype=torch.float64, device=dev)
+        self.oe = torch.empty((B,), dtype=torch.int32, device=dev)
+        self.oo = torch.empty((B * C.sizeof(_lib.Output),), dtype=torch.uint8, device=dev)
+        self.lib = bqp.load()
+        self.h = bqp.Handle(local)
+        self.opt = _lib.options(precision=1 if precision == 'fp32' else 0)
+        self.stream = torch.cuda.current_stream(dev)
+
+    def step(self, with_out=False):
+        P = self._lib.dptr
+        rc = self.lib.bqp_solve_ocp_batched_device(
+            self.h.value, C.byref(self.dims), self.B, C.byref(self.data), C.byref(self.opt),
+            P(self.ox), P(self.ou), P(self.ot), P(self.of),
+            C.cast(C.c_void_p(self.oe.data_ptr()), C.POINTER(C.c_int)),
+            C.c_void_p(self.oo.data_ptr()) if with_out else None, None,
+            C.c_void_p(self.stream.cuda_stream))
+        self._lib.check(rc, 'bqp_solve_ocp_batched_device')
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def kernel_ms(self):
+        return self.h.kernel_ms()[0]
+
+    def first_moves(self):
+        return self.ou[:, 0, :].contiguous(), self.oe
+
+    def outputs(self):
+        """per-instance exit statistics (bqp_output) of a step(with_out=True)"""
+        raw = self.oo.cpu().numpy().tobytes()
+        out = (self._lib.Output * self.B).from_buffer_copy(raw)
+        return dict(iterations=np.array([o.iterations for o in out]),
+                    kkt=np.array([list(o.kkt) for o in out]))
+
+
+class StubSolver:
+    """CPU dry run of the multi-rank harness (bench.py --dry-run, gloo): a deterministic stand-in
+    for the solve (first move = a fixed function of the instance's x0 / A / B), so the sharding,
+    timing barrier, max-over-ranks and all-gather code of this file runs without a GPU and its
+    gathered rows can be compared with the unsharded run."""
+
+    def __init__(self, wl):
+        import torch
+        self.torch = torch
+        self.B = wl['X'].shape[0]
+        self.wl = wl
+
+    @staticmethod
+    def moves(wl):
+        X = np.asarray(wl['X'], float)
+        u = X.sum(axis=1) + 0.5 * X[:, 0] ** 2
+        if wl['A'] is not None:
+            u = u + np.trace(wl['A'], axis1=1, axis2=2) + wl['B'].reshape(len(X), -1).sum(axis=1)
+        return u.reshape(-1, 1), (np.floor(np.abs(u) * 7) % 3 - 1).astype(np.int32)
+
+    def step(self, with_out=False):
+        self.u, self.e = self.moves(self.wl)
+
+    def sync(self):
+        pass
+
+    def kernel_ms(self):
+        return None
+
+    def first_moves(self):
+        return self.torch.from_numpy(self.u), self.torch.from_numpy(self.e)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -173,156 +301,160 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32'],
                     help='structured solver arithmetic (C5 compares both)')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
     args = ap.parse_args()
     if args.config in ('C1', 'CL', 'C2H'):
         return bench_aux(args)
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return launch_ranks(args)
 
     import torch
     import torch.distributed as dist
-    import bqp
-    from bqp import _lib, dist as bd
-    from bqp.ocp import _cm
+    from bqp import dist as bd
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
-        dist.init_process_group('nccl')
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+        dist.init_process_group('gloo' if args.dry_run else 'nccl')
+    if args.dry_run:
+        dev = torch.device('cpu')
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device('cuda', local)
 
     wl = workload(args.config, args.batch, rank, world)
-    prob, X = wl['prob'], wl['X']
-    B = X.shape[0]
+    prob, B = wl['prob'], wl['X'].shape[0]
     N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
-    nv = nx + nu + npar
-
-    # ---- resident device inputs / outputs (torch is only the allocator) ------------------
-    def dt(a):
-        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
-
-    dA = dt(_cm(prob.A) if wl['A'] is None else _cm(wl['A']))
-    dB = dt(_cm(prob.B) if wl['B'] is None else _cm(wl['B']))
-    dw = dt(prob.w if wl['w'] is None else wl['w'])
-    dW, dc = dt(_cm(prob.W)), dt(prob.c)
-    dxlb, dxub, dulb, duub = dt(prob.xlb), dt(prob.xub), dt(prob.ulb), dt(prob.uub)
-    dF, dh, dx0 = dt(_cm(prob.Fp)), dt(prob.hp), dt(X)
-    P = _lib.dptr
-    data = _lib.OcpData(A=P(dA), B=P(dB), c=P(dc), W=P(dW), w=P(dw), xlb=P(dxlb), xub=P(dxub),
-                        ulb=P(dulb), uub=P(duub), Fp=P(dF), hp=P(dh), x0=P(dx0),
-                        sA=0 if wl['A'] is None else nx * nx, sB=0 if wl['B'] is None else nx * nu,
-                        sc=0, sW=0, sw=0 if wl['w'] is None else (N + 1) * nv, sxb=0, sub=0,
-                        sFp=0, shp=0, sx0=nx)
-    dims = _lib.OcpDims(nx, nu, npar, N, mp, prob.poly_stage)
-    ox = torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev)
-    ou = torch.empty((B, N, nu), dtype=torch.float64, device=dev)
-    ot = torch.empty((B, npar), dtype=torch.float64, device=dev)
-    of = torch.empty((B,), dtype=torch.float64, device=dev)
-    oe = torch.empty((B,), dtype=torch.int32, device=dev)
-    lib = bqp.load()
-    h = bqp.Handle(local)
-    opt = _lib.options(precision=1 if args.precision == 'fp32' else 0)
-    stream = torch.cuda.current_stream(dev)
-
-    def step():
-        rc = lib.bqp_solve_ocp_batched_device(
-            h.value, C.byref(dims), B, C.byref(data), C.byref(opt), P(ox), P(ou), P(ot), P(of),
-            C.cast(C.c_void_p(oe.data_ptr()), C.POINTER(C.c_int)), None, None,
-            C.c_void_p(stream.cuda_stream))
-        _lib.check(rc, 'bqp_solve_ocp_batched_device')
+    solver = StubSolver(wl) if args.dry_run else GpuSolver(wl, local, args.precision)
 
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+        solver.step()
+    solver.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    solver.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
+        solver.step()
+    solver.sync()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = bd.max_over_ranks(t1 - t0, dev, world)
     # kernel-only timing: hipEvents on the launch stream, separate pass (one event pair / step)
-    kms = []
-    for _ in range(min(args.steps, 20)):
-        step()
-        ms, _ = h.kernel_ms()
-        kms.append(ms)
-    kernel_ms = float(np.mean(kms))
+    kernel_ms = None
+    if not args.dry_run:
+        kms = []
+        for _ in range(min(args.steps, 20)):
+            solver.step()
+            kms.append(solver.kernel_ms())
+        kernel_ms = float(np.mean(kms))
     # one all-gather of the first moves + status after timing (result collection, bqp.dist)
     total_rows = wl['total'] if wl['scaling'] == 'strong' else B * world
-    u0_all = bd.gather_rows(ou[:, 0, :].contiguous(), total_rows, world)
-    fl_all = bd.gather_rows(oe, total_rows, world).cpu().numpy()
-    flags = oe.cpu().numpy()
-    u0 = ou[:, 0, 0].cpu().numpy()
+    u0_loc, fl_loc = solver.first_moves()
+    u0_all = bd.gather_rows(u0_loc, total_rows, world).cpu().numpy()
+    fl_all = bd.gather_rows(fl_loc, total_rows, world).cpu().numpy()
+    flags = fl_loc.cpu().numpy()
+    u0 = u0_loc[:, 0].cpu().numpy()
 
-    # correctness on the bench batch (C2: vs the fixture's exact optima)
     check = {'converged_frac': float((flags == 1).mean()),
+             'converged_frac_all_ranks': float((fl_all == 1).mean()),
              'infeasible_count_all_ranks': int((fl_all == -2).sum()),
              'gathered_rows': int(u0_all.shape[0])}
-    if args.config == 'C2':
-        g = np.load(os.path.join(GOLD, 'lmpc_N20.npz'))
-        pos = {int(i): j for j, i in enumerate(g['idx'])}
-        err = max([abs(u0[b] - g['du_star'][pos[int(wl['gidx'][b])]])
-                   for b in range(B) if int(wl['gidx'][b]) in pos] or [0.0])
-        check['max_abs_du0_vs_exact'] = float(err)
-    if args.config == 'C5':
-        g5 = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
-        pos = {int(i): j for j, i in enumerate(g5['idx'])}
-        u_eq = float(np.atleast_1d(_mg_design()[0]['u_wp'])[0])
-        err = max([abs(u0[b] + u_eq - g5['u_star'][pos[int(wl['gidx'][b])]])
-                   for b in range(B) if int(wl['gidx'][b]) in pos] or [0.0])
-        check['max_abs_u0_vs_exact'] = float(err)
+    if args.dry_run and rank == 0:
+        # the gathered rows must equal the unsharded run of the same workload
+        full = workload(args.config, args.batch if wl['scaling'] == 'strong' else B * world, 0, 1)
+        uf, ef = StubSolver.moves(full)
+        check['gather_matches_unsharded'] = bool(np.array_equal(u0_all, uf) and
+                                                 np.array_equal(fl_all, ef))
+    if not args.dry_run:
+        # KKT residuals of this batch at exit (bqp_output: stationarity, primal eq, primal
+        # ineq, complementarity mu) and the first move against MATLAB's stored moves and the
+        # exact optima of the fixtures
+        solver.step(with_out=True)
+        solver.sync()
+        o = solver.outputs()
+        conv = flags == 1
+        kk = o['kkt'][conv] if conv.any() else np.zeros((1, 4))
+        check.update(kkt_stationarity_max=float(kk[:, 0].max()),
+                     kkt_primal_eq_max=float(kk[:, 1].max()),
+                     kkt_primal_ineq_max=float(kk[:, 2].max()),
+                     kkt_mu_max=float(kk[:, 3].max()),
+                     iterations_mean=float(o['iterations'].mean()))
+        if args.config == 'C2':
+            g = np.load(os.path.join(GOLD, 'lmpc_N20.npz'))
+            pos = {int(i): j for j, i in enumerate(g['idx'])}
+            gi = wl['gidx']
+            err = [abs(u0[b] - g['du_star'][pos[int(gi[b])]]) for b in range(B) if int(gi[b]) in pos]
+            check['max_abs_du0_vs_exact'] = float(max(err or [0.0]))
+            # fmincon's stored applied moves (LMPC_N20_sys_full.mat, tolerance ~1e-6 of fmincon)
+            dm = np.abs(u0 - g['du_matlab'][gi])
+            check['du0_vs_matlab_median'] = float(np.median(dm))
+            check['du0_vs_matlab_max'] = float(dm.max())
+        if args.config == 'C5':
+            g5 = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
+            pos = {int(i): j for j, i in enumerate(g5['idx'])}
+            u_eq = float(np.atleast_1d(_mg_design()[0]['u_wp'])[0])
+            err = [abs(u0[b] + u_eq - g5['u_star'][pos[int(wl['gidx'][b])]])
+                   for b in range(B) if int(wl['gidx'][b]) in pos]
+            check['max_abs_u0_vs_exact'] = float(max(err or [0.0]))
 
     if rank == 0:
         value = wl['total'] / (elapsed / args.steps) if wl['scaling'] == 'strong' \
             else world * B * args.steps / elapsed
         ms_per_step = 1e3 * elapsed / args.steps
-        threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
-        timed = not args.no_cpu
-        cpu, kref_u = cpu_reference(prob, wl['sample'], threads, timed)
-        # algorithmic flops per launch: sum over the batch of K_ref x F_iter;
-        # instances the reference solver does not converge on (infeasible) count with their
-        # own iteration count
-        kref = kref_u[wl['uniq']]
-        F_it = flops_per_iter(N, nx + npar, nu, nx, mp)
-        flops_launch = float((kref * F_it).sum())
-        achieved = flops_launch / (kernel_ms * 1e-3) / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
-        if args.config == 'C2' and os.path.exists(pmc):
-            try:
-                traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
-            except Exception:
-                traffic = None
-        check['mean_iterations_ref'] = float(kref.mean())
+        roof, cpu = None, None
+        if not args.dry_run:
+            present = len(os.sched_getaffinity(0))
+            threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or present
+            cpu, kref_u = cpu_reference(prob, wl['sample'], threads, not args.no_cpu)
+            if cpu is not None:
+                cpu['cores_present'] = present
+                cpu['cores_note'] = ('threads = OMP_NUM_THREADS (the per-GPU CPU share the box '
+                                     'sets) when set, else every core in the affinity mask')
+            # algorithmic flops per launch: sum over the batch of K_ref x F_iter;
+            # instances the reference solver does not converge on (infeasible) count with their
+            # own iteration count
+            kref = kref_u[wl['uniq']]
+            F_it = flops_per_iter(N, nx + npar, nu, nx, mp)
+            flops_launch = float((kref * F_it).sum())
+            achieved = flops_launch / (kernel_ms * 1e-3) / 1e12
+            traffic = None
+            pmc = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
+            if args.config == 'C2' and os.path.exists(pmc):
+                try:
+                    traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+                except Exception:
+                    traffic = None
+            check['mean_iterations_ref'] = float(kref.mean())
+            roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
+                    'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                    'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
+                    'kernel_ms': round(kernel_ms, 4), 'flops_per_launch': flops_launch,
+                    'note': 'FP64 vector-ALU roof (78.6 TF/s; the kernel issues no MFMA: 5x5 '
+                            'stage blocks); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
+                            'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
+                            '(profiles/)'}
         line = {
             'metric': METRIC,
             'value': round(value, 1), 'unit': 'QP-steps/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
             'higher_is_better': True, 'scaling': wl['scaling'], 'vs_baseline': None,
             'dtype': 'f32' if args.precision == 'fp32' else 'f64',
-            'data': wl['data'],
+            'data': wl['data'] + (' [CPU dry run: stub solver, gloo]' if args.dry_run else ''),
             'config': {'workload': wl['text'], 'batch_per_gpu': B, 'horizon': N,
                        'parallelism': 'dp%d' % world},
-            'roofline': {'bound': 'mfma', 'achieved': round(achieved, 4),
-                         'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
-                         'kernel_ms': round(kernel_ms, 4),
-                         'flops_per_launch': flops_launch,
-                         'note': 'FP64 vector ALU roof (MI355X FP64 matrix peak is the same 78.6 TF/s); '
-                                 'algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); traffic = HBM '
-                                 'bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE (profiles/)'},
+            'roofline': roof,
             'cpu_baseline': cpu,
             'check': check,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 def bench_aux(args):
@@ -438,4 +570,4 @@ def bench_aux(args):
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

@@ -7,7 +7,8 @@
  *
  *   fmincon(COSTFUN, opt_var, [],[],[],[],[],[], CONSFUN, options)
  *       matlab/LBMPC/functions/ocpLMPC.m:20-24      (LMPC, form F1)
- *       matlab/LBMPC/functions/ocpLBMPC.m:157-161    (LBMPC QP sub-problem, form F3)
+ *       matlab/LBMPC/functions/ocpLBMPC.m:27-31      (LBMPC, form F3: Gauss-Newton SQP whose
+ *                                                     QP sub-problems run in the dense kernel)
  *       matlab/trackingMPC/RunExample.m:134-136      (tracking MPC, form F5)
  *   solver('x0',..,'lbx',..,'ubx',..,'lbg',..,'ubg',..)  (CasADi nlpsol/IPOPT)
  *       matlab/LBMPC/examples/DMS_tracking_LMPC_casadi.m:163-167  (form F2)
@@ -53,7 +54,8 @@ typedef struct {
     double tau;        /* fraction-to-boundary, default 0.995 */
     int precision;     /* 0 = fp64 (default); 1 = fp32 solver arithmetic/LDS state (structured API; inputs
                           and outputs stay fp64; tolerances floored at 1e-5 / 1e-6 / 1e-9) */
-    int want_duals;    /* 1: fill the multiplier outputs (structured API) */
+    int want_duals;    /* reserved (set 0): the structured API writes the multiplier outputs
+                          whenever its `duals` argument is non-NULL */
 } bqp_options;
 
 typedef struct {
@@ -61,7 +63,8 @@ typedef struct {
     double constrviolation;  /* max(primal eq, primal ineq) at exit */
     double firstorderopt;    /* stationarity inf-norm at exit */
     double mu;               /* average complementarity at exit */
-    double kkt[4];           /* stationarity, primal eq, primal ineq, complementarity (inf) */
+    double kkt[4];           /* stationarity, primal eq, primal ineq (inf-norms of the solver's
+                                residuals at exit), complementarity (average t.lam = mu) */
 } bqp_output;
 
 /* ------------------------------------------------------------------------------------------
@@ -100,7 +103,9 @@ typedef struct {
     int64_t sA, sB, sc, sW, sw, sxb, sub, sFp, shp, sx0;
 } bqp_ocp_data;
 
-/* Optional multiplier outputs of the structured solve (NULL members are skipped). */
+/* Optional multiplier outputs of the structured solve (NULL members are skipped).  Sign
+ * convention: the Lagrangian is  cost + sum_k pi_k'(A x_k + B u_k + c - x_{k+1})
+ * + sum lam_upper (v - ub) + sum lam_lower (lb - v) + lam_p'(Fp v - hp), all lam >= 0. */
 typedef struct {
     double* pi;     /* batch*N*nx: dynamics multipliers for x_{k+1} = A x_k + B u_k + c   */
     double* lam_x;  /* batch*(N+1)*nx*2: [lower, upper] per stage (0 for absent bounds) */

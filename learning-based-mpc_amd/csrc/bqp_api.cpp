@@ -208,7 +208,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
     if ((size_t)shared_doubles + (size_t)per_wave > lds_budget) return BQP_E_UNSUPPORTED;
     // workspace: H, Fp, stats
-    const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * 4;
+    const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * bqp::STATS_W;
 #ifdef BQP_STAMPS
     HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + (size_t)batch * 32)));
 #else
@@ -362,7 +362,7 @@ int bqp_quadprog_batched_device(bqp_handle h, const bqp_dims* d, int batch, cons
     bqp_options o;
     resolve(opt, &o);
     const int64_t wst = bqp::dense_work_doubles(d->n, d->m, d->me);
-    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * batch + (size_t)batch * 4 + 8)));
+    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * batch + (size_t)batch * bqp::STATS_W + 8)));
     double* wk = (double*)h->dwork.p;
     double* Sd = wk + (size_t)wst * batch;
     bqp::DenseKernelArgs a;
@@ -553,7 +553,7 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     HIP_TRY(hipMemsetAsync(a.flag, 0, sizeof(int) * B, st));
     // QP sub-problem (dense kernel): min 0.5 d'Hd + f'd  s.t.  Ain d <= bin - Ain z
     const int64_t wst = bqp::dense_work_doubles(n, m, 0);
-    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * B + B * 4 + 8)));
+    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * B + B * bqp::STATS_W + 8)));
     bqp::DenseKernelArgs q;
     memset(&q, 0, sizeof(q));
     q.n = n; q.m = m; q.me = 0; q.batch = batch; q.max_iter = 100;
@@ -696,6 +696,10 @@ int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bq
     if (!h || !cl || !x_init || !X || !U) return BQP_E_ARG;
     int rc = ocp_check(d, batch, D);
     if (rc) return rc;
+    // validate the loop description before sizing the staging buffers from it
+    if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
+        return BQP_E_ARG;
+    if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;
     DevScope ds(h->device);
     const int nx = d->nx, nu = d->nu, np = d->np, N = d->N, mp = d->n_poly;
     const int nv = nx + nu + np;
@@ -756,7 +760,7 @@ int bqp_debug_stamps(bqp_handle h, int N, int nv, int mp, double* out) {
     DevScope ds(h->device);
     const int hstride = nv * nv + 1;
     const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));
-    const size_t off = (size_t)(N + 1) * hstride + (size_t)nv * mpad + (size_t)h->last_batch * 4 + 8;
+    const size_t off = (size_t)(N + 1) * hstride + (size_t)nv * mpad + (size_t)h->last_batch * bqp::STATS_W + 8;
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, (double*)h->work.p + off, sizeof(double) * h->last_batch * 32, hipMemcpyDeviceToHost));

@@ -8,6 +8,15 @@
 // corrector) that reuse the factors.  Same step rules as the structured kernel (bqp_ocp.hip):
 // CVXOPT-style unit-scaled start, sigma = (mu_aff/mu)^3, fraction-to-boundary tau.
 // Fixed variables (lb == ub) must be passed as equality rows (the Python/MEX shims do that).
+//
+// quadprog exit flags (algorithm statement with the same rules: oracle/dense_ipm.py):
+//    1 converged;  0 iteration limit;
+//   -6 non-convex: H + CONVEX_EPS max(1, max H_ii) I has no Cholesky factor (tested once);
+//   -8 non-finite residuals;
+//   -3 unbounded: |z|_inf > Z_BIG (1 + data scale) - the iterates run along a recession
+//      direction (K keeps a static pivot floor, so it always factors on a convex problem);
+//   -2 primal infeasible: mu grew MU_BLOWUP-fold over its minimum with the primal residual
+//      stalled (the structured kernel's rule, bqp_ocp.hip).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -18,6 +27,10 @@ namespace bqp {
 
 #define DT 256
 #define TILE 32
+#define DQ_PIV_FLOOR 1e-14    // static pivot floor of K, relative to its largest diagonal entry
+#define DQ_CONVEX_EPS 1e-10   // shift of the convexity test (relative)
+#define DQ_MU_BLOWUP 1e6
+#define DQ_Z_BIG 1e12
 
 struct DWork {
     int64_t K, Y, S, z, y, q, w, dz, dy, rd, re, tA, lA, riA, rcA, dtA, dlA, tB, lB, riB, rcB, dtB, dlB, total;
@@ -78,12 +91,15 @@ struct Red {
     }
 };
 
-// in-place lower Cholesky of an n x n column-major matrix (global/L2); returns false if not PD
-__device__ bool block_cholesky(double* K, int n, double* sc) {
+// in-place lower Cholesky of an n x n column-major matrix (global/L2).  fl >= 0: every pivot is
+// floored at fl (static pivoting; never fails on finite input); fl < 0: returns false at the
+// first non-positive pivot (the convexity test)
+__device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
     const int tid = threadIdx.x;
     for (int j = 0; j < n; ++j) {
         if (tid == 0) {
-            const double d = K[(int64_t)j * n + j];
+            double d = K[(int64_t)j * n + j];
+            if (fl >= 0.0 && !(d > fl)) d = fl;
             sc[8] = d;
             K[(int64_t)j * n + j] = (d > 0.0) ? sqrt(d) : d;
         }
@@ -178,8 +194,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const double minv = 1.0 / fmax(mtot, 1.0);
 
     // ---------------------------------------------------------------- residuals
-    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) {
-        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0;
+    auto residuals = [&](double& stat, double& feq, double& fin, double& csum, double& gscale, double& zmax) {
+        double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0;
         for (int r = tid; r < m; r += DT) {
             double v = tA[r] - b[r];
             for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
@@ -191,7 +207,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             double v = -e[r];
             for (int j = 0; j < n; ++j) v += E[(int64_t)j * me + r] * z[j];
             re[r] = v;
-            fe = fmax(fe, fabs(v));
+            fq = fmax(fq, fabs(v));
         }
         for (int j = tid; j < n; j += DT) {
             double v = f[j];
@@ -213,17 +229,21 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
             rd[j] = v;
             st = fmax(st, fabs(v));
+            zm = fmax(zm, fabs(z[j]));
         }
         stat = red.max(st);
-        feas = red.max(fe);
+        fin = red.max(fe);
+        feq = red.max(fq);
         csum = red.sum(cs);
         gscale = red.max(gs);
+        zmax = red.max(zm);
     };
 
     // ---------------------------------------------------------------- factorisation
     auto factor = [&]() -> bool {
         // K upper entries (i <= j) = H_ij + sum_r A_ri D_r A_rj (+ bound diagonal)
         const int ne = n * (n + 1) / 2;
+        double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
         for (int base = 0; base < ne; base += DT * 8) {
             double acc[8];
             int ii[8], jj[8];
@@ -268,13 +288,14 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     const int j = jj[q2];
                     if (up_present(j)) v += lB[j] / tB[j];
                     if (lo_present(j)) v += lB[n + j] / tB[n + j];
+                    dmx = fmax(dmx, fabs(v));
                 }
                 K[(int64_t)ii[q2] * n + jj[q2]] = v;   // lower part (row jj, col ii) col-major
                 K[(int64_t)jj[q2] * n + ii[q2]] = v;
             }
         }
-        __syncthreads();
-        if (!block_cholesky(K, n, sc)) return false;
+        const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
+        if (!block_cholesky(K, n, sc, kfl)) return false;
         // Y = K^{-1} Aeq' (one thread per equality row), S = Aeq Y
         for (int r = tid; r < me; r += DT) {
             double* yc = Y + (int64_t)r * n;
@@ -282,14 +303,16 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             chol_solve_col(K, n, yc);
         }
         __syncthreads();
+        double smx = 0.0;
         for (int t2 = tid; t2 < me * me; t2 += DT) {
             const int r1 = t2 % me, r2 = t2 / me;
             double s = 0.0;
             for (int j = 0; j < n; ++j) s += E[(int64_t)j * me + r1] * Y[(int64_t)r2 * n + j];
             S[(int64_t)r2 * me + r1] = s;
+            if (r1 == r2) smx = fmax(smx, fabs(s));
         }
-        __syncthreads();
-        if (me > 0 && !block_cholesky(S, me, sc)) return false;
+        const double sfl = DQ_PIV_FLOOR * fmax(red.max(smx), 1e-300);
+        if (me > 0 && !block_cholesky(S, me, sc, sfl)) return false;
         return true;
     };
 
@@ -390,10 +413,25 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         if (lo_present(j)) bsl = fmax(bsl, fabs(lb[j]));
     }
     const double bscale = red.max(bsl);
-    double stat, feas, csum, gscale;
-    residuals(stat, feas, csum, gscale);
+    double fmx = 0.0;
+    for (int j = tid; j < n; j += DT) fmx = fmax(fmx, fabs(f[j]));
+    const double zbig = DQ_Z_BIG * (1.0 + bscale + red.max(fmx));
     int flag = 0;
-    if (!factor()) flag = -8;
+    {
+        // convexity test: Cholesky of H + CONVEX_EPS max(1, max H_ii) I without pivot floor
+        double hd = 0.0;
+        for (int j = tid; j < n; j += DT) hd = fmax(hd, fabs(H[(int64_t)j * n + j]));
+        const double sh = DQ_CONVEX_EPS * fmax(1.0, red.max(hd));
+        for (int e2 = tid; e2 < n * n; e2 += DT) {
+            const int i = e2 % n, j = e2 / n;
+            K[e2] = H[e2] + (i == j ? sh : 0.0);
+        }
+        __syncthreads();
+        if (!block_cholesky(K, n, sc, -1.0)) flag = -6;
+    }
+    double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0;
+    residuals(stat, feq, fin, csum, gscale, zmax);
+    if (flag == 0 && !factor()) flag = -8;
     if (flag == 0) {
         solve();
         double tmin = INFINITY, tmax = -INFINITY;
@@ -418,14 +456,18 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     }
     // ---------------------------------------------------------------- main loop
     int it = 0;
-    double mu = 0.0;
+    double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
         for (it = 0; it <= a.max_iter; ++it) {
-            residuals(stat, feas, csum, gscale);
+            residuals(stat, feq, fin, csum, gscale, zmax);
+            const double feas = fmax(feq, fin);
             mu = csum * minv;
             if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
                 mu <= a.tol_comp) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
+            if (zmax > zbig) { flag = -3; break; }
+            if (mu > DQ_MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) { flag = -2; break; }
+            mu_min = fmin(mu_min, mu);
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }
             for (int r = tid; r < m; r += DT) rcA[r] = tA[r] * lA[r];
@@ -462,19 +504,19 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         for (int i = 0; i < n; ++i) hz += H[(int64_t)j * n + i] * z[i];
         fv += z[j] * (0.5 * hz + f[j]);
         a.x[(int64_t)inst * n + j] = z[j];
-        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = lo_present(j) ? lB[n + j] : 0.0;
-        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = up_present(j) ? lB[j] : 0.0;
+        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = (lo_present(j) && flag != -6) ? lB[n + j] : 0.0;
+        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = (up_present(j) && flag != -6) ? lB[j] : 0.0;
     }
     for (int r = tid; r < m; r += DT)
-        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = lA[r];
+        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = flag != -6 ? lA[r] : 0.0;
     for (int r = tid; r < me; r += DT)
-        if (a.lam_eqlin) a.lam_eqlin[(int64_t)inst * me + r] = y[r];
+        if (a.lam_eqlin) a.lam_eqlin[(int64_t)inst * me + r] = flag != -6 ? y[r] : 0.0;
     fv = red.sum(fv);
     if (tid == 0) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
-        double* so = a.stats + (int64_t)inst * 4;
-        so[0] = (double)it; so[1] = stat; so[2] = feas; so[3] = mu;
+        double* so = a.stats + (int64_t)inst * STATS_W;
+        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin;
     }
 }
 
@@ -535,8 +577,8 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     for (int j = lane; j < n; j += 64) cnt += (up_present(j) ? 1.0 : 0.0) + (lo_present(j) ? 1.0 : 0.0);
     const double minv = 1.0 / fmax(wsum(cnt) + (double)m, 1.0);
 
-    auto residuals = [&](double& stat, double& feas, double& csum, double& gscale) {
-        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0;
+    auto residuals = [&](double& stat, double& fin, double& csum, double& gscale, double& zmax) {
+        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0;
         for (int r = lane; r < m; r += 64) {
             double v = tA[r] - b[r];
             for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
@@ -555,33 +597,19 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
             rd[j] = v;
             st = fmax(st, fabs(v));
+            zm = fmax(zm, fabs(z[j]));
         }
-        stat = wmax(st); feas = wmax(fe); csum = wsum(cs); gscale = wmax(gs);
+        stat = wmax(st); fin = wmax(fe); csum = wsum(cs); gscale = wmax(gs); zmax = wmax(zm);
         wave_sync();
     };
 
-    // K = H + A'DA + bound diagonal; lower Cholesky in place (lane r owns row r)
-    auto factor = [&]() -> bool {
-        for (int r = lane; r < m; r += 64) DA[r] = lA[r] / tA[r];
-        wave_sync();
-        const int ne = n * (n + 1) / 2;
-        for (int e2 = lane; e2 < ne; e2 += 64) {
-            int j = (int)((sqrt(8.0 * e2 + 1.0) - 1.0) / 2.0);
-            while (j * (j + 1) / 2 > e2) --j;
-            while ((j + 1) * (j + 2) / 2 <= e2) ++j;
-            const int i = e2 - j * (j + 1) / 2;          // i <= j
-            double v = H[(int64_t)j * n + i];
-            for (int r = 0; r < m; ++r) v += A[(int64_t)i * m + r] * DA[r] * A[(int64_t)j * m + r];
-            if (i == j) {
-                if (up_present(j)) v += lB[j] / tB[j];
-                if (lo_present(j)) v += lB[n + j] / tB[n + j];
-            }
-            K[(int64_t)i * n + j] = v;                   // lower: row j, column i
-        }
-        wave_sync();
+    // in-place lower Cholesky of K (lane r owns row r).  fl >= 0: pivots floored at fl (static
+    // pivoting); fl < 0: false at the first non-positive pivot (the convexity test)
+    auto chol = [&](double fl) -> bool {
         bool ok = true;
         for (int j = 0; j < n; ++j) {
-            const double d = K[(int64_t)j * n + j];
+            double d = K[(int64_t)j * n + j];
+            if (fl >= 0.0 && !(d > fl)) d = fl;
             if (!(d > 0.0)) { ok = false; break; }
             const double ljj = sqrt(d);
             const double il = 1.0 / ljj;
@@ -595,6 +623,30 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             wave_sync();
         }
         return ok;
+    };
+    // K = H + A'DA + bound diagonal, factored with the static pivot floor
+    auto factor = [&]() -> bool {
+        for (int r = lane; r < m; r += 64) DA[r] = lA[r] / tA[r];
+        wave_sync();
+        const int ne = n * (n + 1) / 2;
+        double dmx = 0.0;
+        for (int e2 = lane; e2 < ne; e2 += 64) {
+            int j = (int)((sqrt(8.0 * e2 + 1.0) - 1.0) / 2.0);
+            while (j * (j + 1) / 2 > e2) --j;
+            while ((j + 1) * (j + 2) / 2 <= e2) ++j;
+            const int i = e2 - j * (j + 1) / 2;          // i <= j
+            double v = H[(int64_t)j * n + i];
+            for (int r = 0; r < m; ++r) v += A[(int64_t)i * m + r] * DA[r] * A[(int64_t)j * m + r];
+            if (i == j) {
+                if (up_present(j)) v += lB[j] / tB[j];
+                if (lo_present(j)) v += lB[n + j] / tB[n + j];
+                dmx = fmax(dmx, fabs(v));
+            }
+            K[(int64_t)i * n + j] = v;                   // lower: row j, column i
+        }
+        const double kfl = DQ_PIV_FLOOR * fmax(wmax(dmx), 1e-300);
+        wave_sync();
+        return chol(kfl);
     };
 
     // x = -(L L')^{-1} q with lane i holding entry i (n <= 32): column-oriented substitution,
@@ -679,10 +731,26 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         if (lo_present(j)) bsl = fmax(bsl, fabs(lb[j]));
     }
     const double bscale = wmax(bsl);
-    double stat, feas, csum, gscale;
-    residuals(stat, feas, csum, gscale);
+    double fmx = 0.0;
+    for (int j = lane; j < n; j += 64) fmx = fmax(fmx, fabs(f[j]));
+    const double zbig = DQ_Z_BIG * (1.0 + bscale + wmax(fmx));
     int flag = 0;
-    if (!factor()) flag = -8;
+    {
+        // convexity test: Cholesky of H + CONVEX_EPS max(1, max H_ii) I without pivot floor
+        double hd = 0.0;
+        for (int j = lane; j < n; j += 64) hd = fmax(hd, fabs(H[(int64_t)j * n + j]));
+        const double sh = DQ_CONVEX_EPS * fmax(1.0, wmax(hd));
+        for (int e2 = lane; e2 < n * n; e2 += 64) {
+            const int i = e2 % n, j = e2 / n;
+            K[e2] = H[e2] + (i == j ? sh : 0.0);
+        }
+        wave_sync();
+        if (!chol(-1.0)) flag = -6;
+    }
+    const double feq = 0.0;                 // no equality rows on this path
+    double stat = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0;
+    residuals(stat, fin, csum, gscale, zmax);
+    if (flag == 0 && !factor()) flag = -8;
     if (flag == 0) {
         solve();
         double tmin = INFINITY, tmax = -INFINITY;
@@ -705,14 +773,18 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         wave_sync();
     }
     int it = 0;
-    double mu = 0.0;
+    double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
         for (it = 0; it <= a.max_iter; ++it) {
-            residuals(stat, feas, csum, gscale);
+            residuals(stat, fin, csum, gscale, zmax);
+            const double feas = fin;
             mu = csum * minv;
             if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
                 mu <= a.tol_comp) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
+            if (zmax > zbig) { flag = -3; break; }
+            if (mu > DQ_MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) { flag = -2; break; }
+            mu_min = fmin(mu_min, mu);
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }
             for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r];
@@ -747,17 +819,17 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         for (int i = 0; i < n; ++i) hz += H[(int64_t)j * n + i] * z[i];
         fv += z[j] * (0.5 * hz + f[j]);
         a.x[(int64_t)inst * n + j] = z[j];
-        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = lo_present(j) ? lB[n + j] : 0.0;
-        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = up_present(j) ? lB[j] : 0.0;
+        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = (lo_present(j) && flag != -6) ? lB[n + j] : 0.0;
+        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = (up_present(j) && flag != -6) ? lB[j] : 0.0;
     }
     for (int r = lane; r < m; r += 64)
-        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = lA[r];
+        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = flag != -6 ? lA[r] : 0.0;
     fv = wsum(fv);
     if (lane == 0) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
-        double* so = a.stats + (int64_t)inst * 4;
-        so[0] = (double)it; so[1] = stat; so[2] = feas; so[3] = mu;
+        double* so = a.stats + (int64_t)inst * STATS_W;
+        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin;
     }
 }
 

@@ -6,6 +6,11 @@
 
 namespace bqp {
 
+// per-instance exit statistics written by every solve kernel and turned into bqp_output by
+// finalize_kernel: iterations, stationarity, max(primal eq, primal ineq), mu, primal eq,
+// primal ineq (inf-norms at exit)
+constexpr int STATS_W = 6;
+
 // Structured OCP kernel arguments (device pointers).  H and Fp are the prepared shared tables:
 //   H  : (N+1) stages x hstride doubles, stage cost in internal order [x; theta; u], row-major
 //   Fp : column-major [NV][mpad] polytope matrix in internal order
@@ -19,7 +24,7 @@ struct OcpKernelArgs {
     int64_t sA, sB, sc, sw, sxb, sub, shp, sx0;
     double *x, *u, *theta, *fval;
     int* exitflag;
-    double* stats;  // batch x 4: iterations, stationarity, feasibility, mu
+    double* stats;  // batch x STATS_W (see STATS_W)
     double *pi_out, *lamx_out, *lamu_out, *lamp_out;
     double* stamps;  // diagnostic build (BQP_STAMPS): batch x 16 phase cycle counts
 };

@@ -4,7 +4,7 @@
 // Reference: functions/oracleL2NW.m:26-36 / examples/hybrid_LBMPC_casadi.m:331-358 (the NW
 // oracle), models/learnedModel.m:25 (x+ = A x + B u + g), functions/costLBMPC.m:20-45 and
 // constraintsLBMPC.m:18-45 (F3), examples/hybrid_LBMPC_casadi.m:250-311 (F4).  The algorithm
-// is stated in oracle/lbmpc.py; the host loop is bqp_lbmpc_solve_batched_device (bqp_lbmpc_api.cpp).
+// is stated in oracle/lbmpc.py; the host loop is bqp_lbmpc_solve_batched_device (bqp_api.cpp).
 //
 // Kernels (one SQP iteration = rollout(GN) -> normal -> dense QP -> rollout(trials) -> update):
 //   nw_oracle_kernel      one wave per query point: g(xi), dg/dxi; lanes over the data window
@@ -377,7 +377,12 @@ __global__ void __launch_bounds__(64) lbmpc_update_kernel(LbmpcArgs a) {
         for (int j = lane; j < n; j += LB_WAVE) z[j] += al * d[j];
         if (lane == 0) a.cprev[b] = J0;
         ++it;
-        if (it >= a.max_iter) { flag = 0; fin = true; }
+        if (it >= a.max_iter) {
+            flag = 0;
+            fin = true;
+            // the returned z is the stepped iterate: its cost is the trial cost of that step
+            if (lane == 0) a.cost0[b] = a.costT[(int64_t)b * a.ntrial + tsel];
+        }
     }
     if (lane == 0) {
         a.iters[b] = it;

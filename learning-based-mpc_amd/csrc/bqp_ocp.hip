@@ -856,7 +856,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 
     // ======================= main loop ======================================================
     int it = 0;
-    real mu = 0.0, mu_min = INFINITY, stat = 0.0, feas = 0.0;
+    real mu = 0.0, mu_min = INFINITY, stat = 0.0, feas = 0.0, feq = 0.0, fin = 0.0;
     const int max_iter = a.max_iter;
     for (it = 0;; ++it) {
         BARRIER();                                        // B0: row multipliers / D / F'DF, row residual norm, comp sum ready
@@ -864,7 +864,9 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         stat = combine();
         STAMP(1);
         STAMP(2);
-        feas = fmax(feasA, X[X_FEASB]);
+        feq = feasA;
+        fin = X[X_FEASB];
+        feas = fmax(feq, fin);
         mu = X[X_CS] * minv;
         bool stop = false;
         if (flag != 0) {
@@ -953,8 +955,8 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
         if (a.stats) {
-            double* so = a.stats + (int64_t)inst * 4;
-            so[0] = (double)it; so[1] = stat; so[2] = feas; so[3] = mu;
+            double* so = a.stats + (int64_t)inst * STATS_W;
+            so[0] = (double)it; so[1] = stat; so[2] = feas; so[3] = mu; so[4] = feq; so[5] = fin;
         }
     }
 }

@@ -60,15 +60,15 @@ hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, in
 __global__ void finalize_kernel(const double* __restrict__ stats, int batch, bqp_output* out) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
-    const double* s = stats + (size_t)b * 4;
+    const double* s = stats + (size_t)b * STATS_W;
     bqp_output o;
     o.iterations = (int)s[0];
     o.firstorderopt = s[1];
     o.constrviolation = s[2];
     o.mu = s[3];
     o.kkt[0] = s[1];
-    o.kkt[1] = s[2];
-    o.kkt[2] = s[2];
+    o.kkt[1] = s[4];
+    o.kkt[2] = s[5];
     o.kkt[3] = s[3];
     out[b] = o;
 }

@@ -2,7 +2,8 @@
  * quadprog_gpu.c — MATLAB MEX gateway for libbqp (source only: MATLAB's mex.h is not available in
  * the build image, so this file is compiled by a MATLAB user with
  *     mex -R2018a quadprog_gpu.c -I<repo>/include -L<repo>/learning-based-mpc_amd/bqp -lbqp
- * and exercised here only through tests/test_abi.py's C-ABI checks).
+ * and exercised here by tests/test_mex_gateway.py, which compiles it against a stub mex.h
+ * (tests/mex_stub/) and drives the gateway from C).
  *
  * Drop-in for the per-step QP solve of the reference:
  *     [x,fval,exitflag,output,lambda] = quadprog_gpu(H,f,A,b,Aeq,beq,lb,ub,x0,options)
@@ -64,9 +65,21 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const int64_t slb = stride_of(lb, n, batch), sub = stride_of(ub, n, batch);
     int nfix = 0;
     int* fix = (int*)mxCalloc(n, sizeof(int));
-    if (lbp && ubp)
+    if (lbp && ubp) {
         for (int j = 0; j < n; ++j)
             if (isfinite(lbp[j]) && lbp[j] == ubp[j]) fix[nfix++] = j;
+        /* the kernel takes one equality-row pattern for the batch: every instance must fix the
+           same variables (bqp/quadprog.py raises the same error) */
+        for (int i = 1; i < batch; ++i)
+            for (int j = 0, r = 0; j < n; ++j) {
+                const int fx = isfinite(lbp[i * slb + j]) && lbp[i * slb + j] == ubp[i * sub + j];
+                const int f0 = r < nfix && fix[r] == j;
+                if (f0) ++r;
+                if (fx != f0)
+                    mexErrMsgIdAndTxt("bqp:fixed", "fixed variables (lb == ub) must be the same "
+                                      "for every instance (instance %d, variable %d)", i + 1, j + 1);
+            }
+    }
     const int me = me0 + nfix;
     double* E = (double*)mxCalloc((size_t)me * n * batch + 1, sizeof(double));
     double* e = (double*)mxCalloc((size_t)me * batch + 1, sizeof(double));

@@ -1,0 +1,194 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Algorithm specification (numpy, one instance) of the dense Mehrotra predictor-corrector IPM
+that ``learning-based-mpc_amd/csrc/bqp_dense.hip`` runs on the GPU for
+``bqp_quadprog_batched`` (MATLAB ``quadprog`` semantics):
+
+    min 0.5 z'Hz + f'z  s.t.  A z <= b,  Aeq z = beq,  lb <= z <= ub.
+
+Rows: the m rows of A, then the finite upper bounds, then the finite lower bounds (slack t,
+multiplier lam).  Newton system per step (D = lam / t):
+
+    K dz + Aeq' dy = -(rd + A'((lam ri - rc)/t) + bound terms),  Aeq dz = -re,
+    K = H + A'DA + diag(bound D)
+
+solved by a Cholesky factor of K (static pivot floor) and the equality Schur complement.
+
+Status (quadprog exitflag), decided in this order at the top of every iteration:
+   1  converged: stationarity <= tol_stat (1 + |Hz + f|), feasibility <= tol_feas (1 + |data|),
+      mu <= tol_comp;
+  -6  non-convex: before the first iteration, H + CONVEX_EPS max(1, max H_ii) I has no
+      Cholesky factor (a negative curvature direction of H beyond round-off);
+  -8  non-finite residuals / factor;
+  -3  unbounded (dual infeasible): |z|_inf > Z_BIG (1 + data scale) - along a recession
+      direction v of the feasible set with Hv = 0 and f'v < 0 the iterates run away (the
+      static pivot floor keeps K factorable there);
+  -2  primal infeasible: mu grew by MU_BLOWUP over its minimum while the primal residual
+      stalled above 1e-6 (1 + data scale) - the structured kernel's rule (bqp_ocp.hip);
+   0  iteration limit.
+"""
+import numpy as np
+
+PIV_FLOOR = 1e-14     # static pivot floor of K, relative to its largest diagonal entry
+CONVEX_EPS = 1e-10    # convexity test shift (relative)
+MU_BLOWUP = 1e6
+Z_BIG = 1e12
+
+
+def _chol_floor(K, floor):
+    """Lower Cholesky with every pivot floored at `floor` (never fails on finite input)."""
+    n = K.shape[0]
+    L = np.zeros_like(K)
+    for j in range(n):
+        d = K[j, j] - L[j, :j] @ L[j, :j]
+        if not d > floor:
+            d = floor
+        L[j, j] = np.sqrt(d)
+        L[j + 1:, j] = (K[j + 1:, j] - L[j + 1:, :j] @ L[j, :j]) / L[j, j]
+    return L
+
+
+def _chol_ok(K):
+    n = K.shape[0]
+    L = np.zeros_like(K)
+    for j in range(n):
+        d = K[j, j] - L[j, :j] @ L[j, :j]
+        if not d > 0.0:
+            return False
+        L[j, j] = np.sqrt(d)
+        L[j + 1:, j] = (K[j + 1:, j] - L[j + 1:, :j] @ L[j, :j]) / L[j, j]
+    return True
+
+
+def _lsolve(L, b):
+    y = np.linalg.solve(np.tril(L), b)
+    return np.linalg.solve(np.tril(L).T, y)
+
+
+def convex(H):
+    """quadprog's -6 test (see module doc)."""
+    n = H.shape[0]
+    if n == 0:
+        return True
+    sh = CONVEX_EPS * max(1.0, np.abs(np.diag(H)).max())
+    return _chol_ok(H + sh * np.eye(n))
+
+
+def solve(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, max_iter=50,
+          tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995):
+    H = np.asarray(H, float)
+    n = H.shape[0]
+    f = np.asarray(f, float).ravel()
+    A = np.zeros((0, n)) if A is None else np.asarray(A, float).reshape(-1, n)
+    b = np.zeros(0) if b is None else np.asarray(b, float).ravel()
+    E = np.zeros((0, n)) if Aeq is None else np.asarray(Aeq, float).reshape(-1, n)
+    e = np.zeros(0) if beq is None else np.asarray(beq, float).ravel()
+    lb = np.full(n, -np.inf) if lb is None else np.asarray(lb, float).ravel()
+    ub = np.full(n, np.inf) if ub is None else np.asarray(ub, float).ravel()
+    iu = np.flatnonzero(np.isfinite(ub))
+    il = np.flatnonzero(np.isfinite(lb))
+    # all rows as G z <= h
+    G = np.vstack([A, np.eye(n)[iu], -np.eye(n)[il]])
+    h = np.concatenate([b, ub[iu], -lb[il]])
+    m = G.shape[0]
+    minv = 1.0 / max(m, 1)
+    bscale = max([0.0] + [np.abs(v).max() for v in (b, e, ub[iu], lb[il]) if v.size])
+    zscale = Z_BIG * (1.0 + bscale + np.abs(f).max(initial=0.0))
+    res = dict(iterations=0, exitflag=0)
+    if not convex(H):
+        res.update(x=np.zeros(n), exitflag=-6, lam=np.zeros(m), y=np.zeros(E.shape[0]))
+        return res
+    z = np.zeros(n)
+    y = np.zeros(E.shape[0])
+    t = np.ones(m)
+    lam = np.ones(m)
+
+    def resid():
+        rd = H @ z + f + E.T @ y + G.T @ lam
+        re = E @ z - e
+        ri = G @ z + t - h
+        gs = np.abs(H @ z + f).max(initial=0.0)
+        return rd, re, ri, gs
+
+    def factor():
+        K = H + G.T @ ((lam / t)[:, None] * G)
+        fl = PIV_FLOOR * max(np.abs(np.diag(K)).max(initial=0.0), 1e-300)
+        L = _chol_floor(K, fl)
+        if E.shape[0]:
+            Y = _lsolve(L, E.T)
+            S = E @ Y
+            Ls = _chol_floor(S, PIV_FLOOR * max(np.abs(np.diag(S)).max(), 1e-300))
+        else:
+            Y = Ls = None
+        return L, Y, Ls
+
+    def newton(fac, rd, re, ri, rc):
+        L, Y, Ls = fac
+        q = rd + G.T @ ((lam * ri - rc) / t)
+        w = -_lsolve(L, q)
+        if E.shape[0]:
+            dy = _lsolve(Ls, E @ w + re)
+            dz = w - Y @ dy
+        else:
+            dy = np.zeros(0)
+            dz = w
+        dt = -ri - G @ dz
+        dl = (-rc - lam * dt) / t
+        return dz, dy, dt, dl
+
+    def max_step(dt, dl):
+        a = 1.0
+        for v, dv in ((t, dt), (lam, dl)):
+            neg = dv < 0
+            if neg.any():
+                a = min(a, (-v[neg] / dv[neg]).min())
+        return a
+
+    # start: unit-scaled least-squares point (t = lam = 1), then positivity shifts
+    rd, re, ri, gs = resid()
+    fac = factor()
+    dz, dy, dt, dl = newton(fac, rd, re, ri, t * lam)
+    z = z + dz
+    y = y + dy
+    tt = 1.0 + dt
+    shp = 1.0 - tt.min() if m and tt.min() <= 0 else 0.0
+    shd = 1.0 + tt.max() if m and tt.max() >= 0 else 0.0
+    t = tt + shp
+    lam = -tt + shd
+    mu_min = np.inf
+    it = 0
+    flag = 0
+    for it in range(max_iter + 1):
+        rd, re, ri, gs = resid()
+        stat = np.abs(rd).max(initial=0.0)
+        feas = max(np.abs(re).max(initial=0.0), np.abs(ri).max(initial=0.0))
+        mu = (t @ lam) * minv
+        if stat <= tol_stat * (1 + gs) and feas <= tol_feas * (1 + bscale) and mu <= tol_comp:
+            flag = 1
+            break
+        if not (np.isfinite(stat) and np.isfinite(feas) and np.isfinite(mu)):
+            flag = -8
+            break
+        if np.abs(z).max(initial=0.0) > zscale:
+            flag = -3
+            break
+        if mu > MU_BLOWUP * mu_min and feas > 1e-6 * (1 + bscale):
+            flag = -2
+            break
+        mu_min = min(mu_min, mu)
+        if it == max_iter:
+            break
+        fac = factor()
+        dz, dy, dt, dl = newton(fac, rd, re, ri, t * lam)
+        a = max_step(dt, dl)
+        mua = (t + a * dt) @ (lam + a * dl) * minv
+        sg = (mua / mu) ** 3
+        dz, dy, dt, dl = newton(fac, rd, re, ri, t * lam + dt * dl - sg * mu)
+        a = min(1.0, tau * max_step(dt, dl))
+        z = z + a * dz
+        y = y + a * dy
+        t = t + a * dt
+        lam = lam + a * dl
+    res.update(x=z, y=y, lam=lam, t=t, exitflag=flag, iterations=it, mu=mu, stat=stat,
+               feas=feas, fval=0.5 * z @ H @ z + f @ z)
+    return res

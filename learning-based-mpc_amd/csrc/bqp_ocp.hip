@@ -74,6 +74,10 @@ __device__ __forceinline__ float frcp(float t) {
     return __builtin_fmaf(r, __builtin_fmaf(-t, r, 1.0f), r);
 }
 
+// fused multiply-add in the instantiation's precision (no promotion of the fp32 path to fp64)
+__device__ __forceinline__ double fmar(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fmar(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
 template <int N>
 __device__ __forceinline__ bool chol_small(const real (&M)[N][N], real (&L)[N][N]) {
     bool ok = true;
@@ -384,174 +388,178 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     };
 
     // ======================= Riccati factorisation =========================================
-    // lane (ib, jb) = (lane / NS, lane % NS), ib <= jb < NS, owns entry (ib, jb) of P_k.  Every
-    // lane forms the input-row quantities of ITS two columns itself (g = P_{k+1} Bbar,
-    // M_u(:, ib), M_u(:, jb), Rhat, K_ib, K_jb), so the only cross-lane traffic per stage is P_k
-    // itself, broadcast through the packed LDS table.
-    const int ib = (lane < NS * NS) ? lane / NS : 0, jb = (lane < NS * NS) ? lane % NS : 0;
-    const bool blane = lane < NS * NS && ib <= jb;
+    // Standard form on the stage matrix M_k = Ht_k + F' P_{k+1} F, F = [Abar Bbar]:
+    //   K_k = -M_uu^{-1} M_us,   P_k = M_ss - M_su M_uu^{-1} M_us.
+    // M is linear in the packed upper triangle of P_{k+1} with CONSTANT coefficients
+    //   C(r, c; a, b) = F(a,r) F(b,c) + [a != b] F(b,r) F(a,c)
+    // (per instance, formed once per solve), so one entry of M is one NPK-term dot product.
+    // Lane layout: quad e (lanes 4e..4e+3, e < NPK) owns packed entry e = (ie, je) of P_k.  The
+    // VAL values that entry needs - M(ie,je), M(ie,u), M(je,u), M_uu - are spread over the quad
+    // (lane q: values q, q+4, ...), each lane holding the coefficient rows of its values in
+    // registers; lane 4e gathers them with quad DPP broadcasts, forms P_k(ie, je) (and, on the
+    // diagonal, the column je of K_k) and stores it; the packed P_k is read back by every lane
+    // (ds_read_b128 broadcasts).  Per stage: one dot product per lane, one LDS round trip.
+    // Same association as oracle/cpu_ipm.c factor(): partial sums over m mod 4,
+    // (s0 + s1) + (s2 + s3), then Ht + sum.
     constexpr int PST = pk_stride(NS);
-    // the model operands of the factor and of the sweeps are re-read from LDS at the start of
-    // each phase (not kept live across the iteration: register budget at two waves per SIMD)
-    auto load_ab = [&](real (&Ai)[NS], real (&Aj)[NS], real (&Bl)[NS][NU]) __attribute__((always_inline)) {
+    constexpr int NPK = pk_len(NS);
+    constexpr int NUT = NU * (NU + 1) / 2;
+    constexpr int VAL = 1 + 2 * NU + NUT;           // values one P_k entry needs
+    constexpr int VPL = (VAL + 3) / 4;              // values per lane of the quad
+    static_assert(4 * NPK <= WAVE, "one quad per packed entry of P");
+    const int fq = lane >> 2, fql = lane & 3;
+    const bool fquad = fq < NPK;
+    int ie = 0, je = 0;                             // packed entry fq -> (ie <= je)
+    {
+        int e = 0;
 #pragma unroll
-        for (int a_ = 0; a_ < NS; ++a_) {
-            Ai[a_] = Abar(a_, ib);
-            Aj[a_] = Abar(a_, jb);
+        for (int i = 0; i < NS; ++i)
 #pragma unroll
-            for (int x = 0; x < NU; ++x) Bl[a_][x] = Bbar(a_, x);
+            for (int j = i; j < NS; ++j, ++e)
+                if (e == fq) { ie = i; je = j; }
+    }
+    // (row, col) in the internal [s; u] index space of value v of entry (ie, je)
+    auto vrc = [&](int v, int& r, int& c) __attribute__((always_inline)) {
+        if (v == 0) { r = ie; c = je; }
+        else if (v <= NU) { r = ie; c = NS + v - 1; }
+        else if (v <= 2 * NU) { r = je; c = NS + v - NU - 1; }
+        else {
+            int t = v - 2 * NU - 1, x = 0;
+#pragma unroll
+            for (int xx = 0; xx < NU; ++xx) if (t >= NU - xx) { t -= NU - xx; x = xx + 1; } else break;
+            r = NS + x; c = NS + x + t;
         }
     };
-    auto factor = [&]() __attribute__((always_inline)) -> bool {
-        real Ai[NS], Aj[NS], Bl[NS][NU];
-        load_ab(Ai, Aj, Bl);
-        // stage-k entries each lane needs, prefetched one stage ahead as RAW operands (cost
-        // entry, box diagonal) and combined only when the stage is processed; the polytope term
-        // F'DF enters at stage kp only (a uniform branch).  Operation order (H + D) + FD.
-        struct StageH { real hij, dij, hui[NU], huj[NU], huu[NU][NU], duu[NU]; };
-        auto load_h = [&](int k, StageH& sh) __attribute__((always_inline)) {
-            const real* Hk = Hs + k * hstride;
-            sh.hij = Hk[ib * NV + jb];
-            sh.dij = W[L.Dx + k * NV + ib];
+    auto Fab = [&](int a_, int r) __attribute__((always_inline)) -> real {
+        return r < NS ? Abar(a_, r) : Bbar(a_, r - NS);
+    };
+    real cf[VPL][NPK];                              // coefficient rows of this lane's values
+    int vr[VPL], vc[VPL];
 #pragma unroll
-            for (int x = 0; x < NU; ++x) {
-                sh.hui[x] = Hk[(NS + x) * NV + ib];
-                sh.huj[x] = Hk[(NS + x) * NV + jb];
-                sh.duu[x] = W[L.Dx + k * NV + NS + x];
+    for (int t = 0; t < VPL; ++t) {
+        const int v = fql + 4 * t;
+        int r = 0, c = 0;
+        if (v < VAL) vrc(v, r, c);
+        vr[t] = r; vc[t] = c;
+        int m = 0;
 #pragma unroll
-                for (int y = 0; y < NU; ++y) sh.huu[x][y] = Hk[(NS + x) * NV + NS + y];
+        for (int a_ = 0; a_ < NS; ++a_)
+#pragma unroll
+            for (int b = a_; b < NS; ++b, ++m) {
+                real x = Fab(a_, r) * Fab(b, c);
+                if (a_ != b) x = fmar(Fab(b, r), Fab(a_, c), x);
+                cf[t][m] = (v < VAL) ? x : real(0);
             }
-        };
-        auto combine_h = [&](int k, const StageH& sh, StageH& o) __attribute__((always_inline)) {
-            o.hij = sh.hij + (ib == jb ? sh.dij : 0.0);
+    }
+    // Ht entry (r, c) of stage k: raw cost entry, box diagonal, polytope term at kp; the raw
+    // operands are prefetched one stage ahead and combined as (H + D) + FD
+    struct HRaw { real h[VPL], d[VPL]; };
+    auto load_h = [&](int k, HRaw& o) __attribute__((always_inline)) {
+        const real* Hk = Hs + k * hstride;
 #pragma unroll
-            for (int x = 0; x < NU; ++x) {
-                o.hui[x] = sh.hui[x];
-                o.huj[x] = sh.huj[x];
-#pragma unroll
-                for (int y = 0; y < NU; ++y) o.huu[x][y] = sh.huu[x][y] + (x == y ? sh.duu[x] : 0.0);
-            }
-            if (k == kp) {
-                o.hij += W[L.FD + ib * NV + jb];
-#pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    o.hui[x] += W[L.FD + (NS + x) * NV + ib];
-                    o.huj[x] += W[L.FD + (NS + x) * NV + jb];
-#pragma unroll
-                    for (int y = 0; y < NU; ++y) o.huu[x][y] += W[L.FD + (NS + x) * NV + NS + y];
-                }
-            }
-        };
-        real pu[PST];
-        auto bcast_p = [&](int k) __attribute__((always_inline)) {
-            wave_sync();
-            const real2* src = reinterpret_cast<const real2*>(W + L.P + k * PST);
-#pragma unroll
-            for (int q = 0; q < PST / 2; ++q) {
-                const real2 t2 = src[q];
-                pu[2 * q] = t2.x;
-                pu[2 * q + 1] = t2.y;
-            }
-        };
-        auto Pm = [&](int a_, int b_) __attribute__((always_inline)) -> real { return pu[pk_idx(NS, a_, b_)]; };
-        {
-            StageH rN, cN;
-            load_h(N, rN);
-            combine_h(N, rN, cN);
-            if (blane) W[L.P + N * PST + pk_idx(NS, ib, jb)] = cN.hij;
+        for (int t = 0; t < VPL; ++t) {
+            o.h[t] = Hk[vr[t] * NV + vc[t]];
+            o.d[t] = W[L.Dx + k * NV + vr[t]];
         }
-        bcast_p(N);
+    };
+    auto ht = [&](int k, const HRaw& o, int t) __attribute__((always_inline)) -> real {
+        real v = o.h[t] + (vr[t] == vc[t] ? o.d[t] : real(0));
+        if (k == kp) v += W[L.FD + vr[t] * NV + vc[t]];
+        return v;
+    };
+    real pu[PST];
+    auto read_p = [&](int k) __attribute__((always_inline)) {
+        wave_sync();
+        const real2* src = reinterpret_cast<const real2*>(W + L.P + k * PST);
+#pragma unroll
+        for (int q = 0; q < PST / 2; ++q) {
+            const real2 t2 = src[q];
+            pu[2 * q] = t2.x;
+            pu[2 * q + 1] = t2.y;
+        }
+    };
+    auto Pm = [&](int a_, int b_) __attribute__((always_inline)) -> real { return pu[pk_idx(NS, a_, b_)]; };
+    auto factor = [&]() __attribute__((always_inline)) -> bool {
+        HRaw raw, nxt;
+        {
+            // P_N = Ht_N(s, s)
+            load_h(N, raw);
+            const real v0 = ht(N, raw, 0);
+            if (fquad && fql == 0) W[L.P + N * PST + fq] = v0;
+        }
+        read_p(N);
         bool ok = true;
-        StageH raw, nxt, cur;
         load_h(N - 1, raw);
         for (int k = N - 1; k >= 0; --k) {
-            combine_h(k, raw, cur);
             if (k > 0) load_h(k - 1, nxt);
-            // g = P_{k+1} Bbar (uniform) and G_jb = P_{k+1} Abar(:, jb)
-            real g[NS][NU], Gj[NS];
+            real mv[VPL];
 #pragma unroll
-            for (int a_ = 0; a_ < NS; ++a_) {
-                real gj = 0.0;
+            for (int t = 0; t < VPL; ++t) {
+                real sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
 #pragma unroll
-                for (int b = 0; b < NS; ++b) gj += Pm(a_, b) * Aj[b];
-                Gj[a_] = gj;
-#pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    real acc = 0.0;
-#pragma unroll
-                    for (int b = 0; b < NS; ++b) acc += Pm(a_, b) * Bl[b][x];
-                    g[a_][x] = acc;
+                for (int m = 0; m < NPK; ++m) {
+                    if ((m & 3) == 0) sp0 = fmar(cf[t][m], pu[m], sp0);
+                    if ((m & 3) == 1) sp1 = fmar(cf[t][m], pu[m], sp1);
+                    if ((m & 3) == 2) sp2 = fmar(cf[t][m], pu[m], sp2);
+                    if ((m & 3) == 3) sp3 = fmar(cf[t][m], pu[m], sp3);
                 }
+                mv[t] = ht(k, raw, t) + ((sp0 + sp1) + (sp2 + sp3));
             }
-            // input rows of M = Ht + F' P F for columns ib, jb and Rhat = M_uu
-            real mi[NU], mj[NU], Ruu[NU][NU];
+            // gather the VAL values in lane 4e: value v sits in lane v % 4, slot v / 4
+            real g[VAL];
 #pragma unroll
-            for (int x = 0; x < NU; ++x) {
-                real vi = cur.hui[x], vj = cur.huj[x];
-#pragma unroll
-                for (int a_ = 0; a_ < NS; ++a_) { vi += g[a_][x] * Ai[a_]; vj += g[a_][x] * Aj[a_]; }
-                mi[x] = vi;
-                mj[x] = vj;
-#pragma unroll
-                for (int y = 0; y < NU; ++y) {
-                    real r = cur.huu[x][y];
-#pragma unroll
-                    for (int a_ = 0; a_ < NS; ++a_) r += g[a_][x] * Bl[a_][y];
-                    Ruu[x][y] = r;
-                }
+            for (int v = 0; v < VAL; ++v) {
+                const int s = v & 3;
+                const real src = mv[v >> 2];
+                g[v] = (s == 0) ? dpp_mov<0x00, 0xf>(real(0), src)
+                     : (s == 1) ? dpp_mov<0x55, 0xf>(real(0), src)
+                     : (s == 2) ? dpp_mov<0xAA, 0xf>(real(0), src)
+                                : dpp_mov<0xFF, 0xf>(real(0), src);
             }
-            // K columns ib, jb:  K = -Rhat^{-1} M_us  (nu = 1: one reciprocal; else Cholesky)
-            real Ki[NU], Kj[NU], Lf[NU * NU];
+            real pv, Kc[NU], Lf[NU * NU];
             if constexpr (NU == 1) {
-                ok = ok && (Ruu[0][0] > 0.0);
-                const real rinv = frcp(Ruu[0][0]);   // Ruu > 0 checked above
+                ok = ok && (g[3] > 0.0);
+                const real rinv = frcp(g[3]);          // M_uu > 0 checked above
                 Lf[0] = rinv;
-                Ki[0] = -mi[0] * rinv;
-                Kj[0] = -mj[0] * rinv;
+                pv = fmar(-(g[1] * rinv), g[2], g[0]);
+                Kc[0] = -(g[2] * rinv);
             } else {
-                real Lc[NU][NU];
-                ok = chol_small<NU>(Ruu, Lc) && ok;
+                real Mu[NU][NU], Lc[NU][NU];
+                {
+                    int t = 2 * NU + 1;
+#pragma unroll
+                    for (int x = 0; x < NU; ++x)
+#pragma unroll
+                        for (int y = x; y < NU; ++y, ++t) { Mu[x][y] = g[t]; Mu[y][x] = g[t]; }
+                }
+                ok = chol_small<NU>(Mu, Lc) && ok;
 #pragma unroll
                 for (int x = 0; x < NU; ++x)
 #pragma unroll
                     for (int y = 0; y < NU; ++y) Lf[x * NU + y] = Lc[x][y];
+                real y[NU];
 #pragma unroll
-                for (int x = 0; x < NU; ++x) { Ki[x] = -mi[x]; Kj[x] = -mj[x]; }
-                chol_solve_small<NU>(Lf, Ki);
-                chol_solve_small<NU>(Lf, Kj);
+                for (int x = 0; x < NU; ++x) y[x] = g[1 + NU + x];   // M(je, u)
+                chol_solve_small<NU>(Lf, y);
+                real acc = g[1] * y[0];
+#pragma unroll
+                for (int x = 1; x < NU; ++x) acc = fmar(g[1 + x], y[x], acc);
+                pv = g[0] - acc;
+#pragma unroll
+                for (int x = 0; x < NU; ++x) Kc[x] = -y[x];
             }
-            // Phi(:, ib) = Abar(:, ib) + Bbar K_ib ; T_jb = P Phi(:, jb) = G_jb + g K_jb
-            real Phi_i[NS], Tj[NS];
+            if (fquad && fql == 0) {
+                W[L.P + k * PST + fq] = pv;
+                if (ie == je) {
 #pragma unroll
-            for (int a_ = 0; a_ < NS; ++a_) {
-                real vi = Ai[a_], vt = Gj[a_];
+                    for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + je] = Kc[x];
+                }
+                if (fq == 0) {
 #pragma unroll
-                for (int x = 0; x < NU; ++x) { vi += Bl[a_][x] * Ki[x]; vt += g[a_][x] * Kj[x]; }
-                Phi_i[a_] = vi;
-                Tj[a_] = vt;
+                    for (int x = 0; x < NU * NU; ++x) W[L.Lr + k * NU * NU + x] = Lf[x];
+                }
             }
-            // Joseph form  P_k(ib, jb) = [I;K]' Ht [I;K] + Phi(:, ib)' P Phi(:, jb)
-            real v = cur.hij;
-#pragma unroll
-            for (int x = 0; x < NU; ++x) {
-                v += Ki[x] * cur.huj[x] + cur.hui[x] * Kj[x];
-#pragma unroll
-                for (int y = 0; y < NU; ++y) v += Ki[x] * cur.huu[x][y] * Kj[y];
-            }
-            real acc = 0.0;
-#pragma unroll
-            for (int a_ = 0; a_ < NS; ++a_) acc += Phi_i[a_] * Tj[a_];
-            v += acc;
-            if (blane) W[L.P + k * PST + pk_idx(NS, ib, jb)] = v;
-            if (lane < NS) {        // lane (0, jb): column jb of K
-#pragma unroll
-                for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + jb] = Kj[x];
-            }
-            if (lane == 0) {
-#pragma unroll
-                for (int x = 0; x < NU * NU; ++x) W[L.Lr + k * NU * NU + x] = Lf[x];
-            }
-            bcast_p(k);
+            read_p(k);
             raw = nxt;
         }
         // factor of the theta block of P_0 (np = 1: its reciprocal)
@@ -673,6 +681,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             }
         }
         wave_sync();
+        STAMP(10);
         // backward sweep: lane i < NS computes entry i of p_k = Phi_k' p_{k+1} + qh_k; the new
         // vector is broadcast with readlane (scalar registers); two register sets used
         // alternately (stages k, k-1), each refilled two stages ahead
@@ -711,6 +720,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             }
         }
         wave_sync();
+        STAMP(11);
         // post-backward: kff_k = -Rhat^{-1}(qu_k + Bbar'(p_{k+1} + w_k)); f_k = Bbar kff_k + re_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -739,6 +749,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             }
         }
         wave_sync();
+        STAMP(12);
         // theta_0 step + forward sweep: lane i < NS computes entry i of ds_{k+1} = Phi_k ds_k + f_k
         {
             real d[NS];
@@ -787,6 +798,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             }
         }
         wave_sync();
+        STAMP(13);
         // post-forward: du_k = K_k ds_k + kff_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -806,6 +818,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             }
         }
         wave_sync();
+        STAMP(14);
     };
 
     // primal/dual stage update by alpha along (ids, idu); dpi_k = P_k ds_k + p_k

@@ -219,6 +219,11 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
 }
 
 /* ---------------- factorisation ---------------- */
+/* column r of F = [Abar Bbar] (internal [s; u] order), row a */
+static double fab(const prob_t* P, int a, int r) {
+    return r < P->ns ? P->Abar[a][r] : P->Bbar[a][r - P->ns];
+}
+
 static int factor(const prob_t* P, work_t* W) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv;
     /* one reciprocal of t and lam per row per iteration; every later quotient is a product */
@@ -261,78 +266,62 @@ static int factor(const prob_t* P, work_t* W) {
     double* PN = W->Ptab + (size_t)N * ns * ns;
     for (int i = 0; i < ns; ++i)
         for (int j = 0; j < ns; ++j) PN[i * ns + j] = HT(N, i, j);
+    /* Riccati recursion in standard form on the stage matrix M_k = Ht_k + F' P_{k+1} F,
+     * F = [Abar Bbar]:  K_k = -M_uu^{-1} M_us,  P_k = M_ss - M_su M_uu^{-1} M_us.
+     * M is linear in the packed upper triangle of P_{k+1} with constant coefficients
+     * C(r, c; a, b) = F(a,r) F(b,c) + [a != b] F(b,r) F(a,c), summed as four interleaved partial
+     * sums over the packed index m mod 4, combined (s0 + s1) + (s2 + s3) - the association of
+     * the kernel (bqp_ocp.hip factor(), one value per lane of a quad). */
     for (int k = N - 1; k >= 0; --k) {
         const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
-        /* g = Pn Bbar, G = Pn Abar;  input rows of M = Ht + F' Pn F, F = [Abar Bbar]:
-         * M_us(:, j) = Ht_us(:, j) + g' Abar(:, j),  Rhat = M_uu = Ht_uu + g' Bbar  (the kernel
-         * forms the same products in the same association, bqp_ocp.hip factor()) */
-        double g[MAXNS][MAXNU], G[MAXNS][MAXNS];
-        for (int a = 0; a < ns; ++a) {
-            for (int j = 0; j < ns; ++j) {
-                double acc = 0;
-                for (int b = 0; b < ns; ++b) acc += Pn[a * ns + b] * P->Abar[b][j];
-                G[a][j] = acc;
+        double Mss[MAXNS][MAXNS], Msu[MAXNS][MAXNU], Muu[MAXNU * MAXNU];
+        for (int r = 0; r < nv; ++r)
+            for (int c = r; c < nv; ++c) {
+                if (r >= ns && c < ns) continue;
+                double sp[4] = {0.0, 0.0, 0.0, 0.0};
+                int m = 0;
+                for (int a = 0; a < ns; ++a)
+                    for (int b = a; b < ns; ++b, ++m) {
+                        double cf = fab(P, a, r) * fab(P, b, c);
+                        if (a != b) cf = fma(fab(P, b, r), fab(P, a, c), cf);
+                        sp[m & 3] = fma(cf, Pn[a * ns + b], sp[m & 3]);
+                    }
+                const double v = HT(k, r, c) + ((sp[0] + sp[1]) + (sp[2] + sp[3]));
+                if (c < ns) Mss[r][c] = v;
+                else if (r < ns) Msu[r][c - ns] = v;
+                else { Muu[(r - ns) * nu + (c - ns)] = v; Muu[(c - ns) * nu + (r - ns)] = v; }
             }
-            for (int x = 0; x < nu; ++x) {
-                double acc = 0;
-                for (int b = 0; b < ns; ++b) acc += Pn[a * ns + b] * P->Bbar[b][x];
-                g[a][x] = acc;
-            }
-        }
-        double Mu[MAXNU][MAXNV];
-        for (int x = 0; x < nu; ++x) {
-            for (int j = 0; j < ns; ++j) {
-                double acc = HT(k, ns + x, j);
-                for (int a = 0; a < ns; ++a) acc += g[a][x] * P->Abar[a][j];
-                Mu[x][j] = acc;
-            }
-            for (int y = 0; y < nu; ++y) {
-                double acc = HT(k, ns + x, ns + y);
-                for (int a = 0; a < ns; ++a) acc += g[a][x] * P->Bbar[a][y];
-                Mu[x][ns + y] = acc;
-            }
-        }
-        double Ruu[MAXNU * MAXNU];
-        double* Lk = W->Rinv + (size_t)k * nu * nu;    /* factor of Rhat_k (spd_fac) */
-        for (int a = 0; a < nu; ++a)
-            for (int b = 0; b < nu; ++b) Ruu[a * nu + b] = Mu[a][ns + b];
-        if (spd_fac(nu, Ruu, Lk)) return -1;
+        double* Lk = W->Rinv + (size_t)k * nu * nu;    /* factor of M_uu (spd_fac) */
+        if (spd_fac(nu, Muu, Lk)) return -1;
         double* Kk = W->Ktab + (size_t)k * nu * ns;
+        double Y[MAXNS][MAXNU];                        /* M_uu^{-1} M_u j */
         for (int j = 0; j < ns; ++j) {
             double col[MAXNU];
-            for (int b = 0; b < nu; ++b) col[b] = -Mu[b][j];
+            for (int x = 0; x < nu; ++x) col[x] = Msu[j][x];
             spd_solve(nu, Lk, col);
-            for (int a = 0; a < nu; ++a) Kk[a * ns + j] = col[a];
+            for (int x = 0; x < nu; ++x) { Y[j][x] = col[x]; Kk[x * ns + j] = -col[x]; }
         }
-        /* Joseph form: P_k = [I;K]' Ht [I;K] + Phi' Pn Phi,  Phi = Abar + Bbar K, with
-         * Pn Phi(:, j) = G(:, j) + g K(:, j) */
-        double Phi[MAXNS][MAXNS], T[MAXNS][MAXNS];
-        for (int a = 0; a < ns; ++a)
-            for (int j = 0; j < ns; ++j) {
-                double v = P->Abar[a][j], t = G[a][j];
-                for (int x = 0; x < nu; ++x) {
-                    v += P->Bbar[a][x] * Kk[x * ns + j];
-                    t += g[a][x] * Kk[x * ns + j];
-                }
-                Phi[a][j] = v;
-                T[a][j] = t;
-            }
         double* Pk = W->Ptab + (size_t)k * ns * ns;
-        double* Phk = W->Phit + (size_t)k * ns * ns;   /* closed loop Phi_k, row-major */
-        for (int a = 0; a < ns; ++a)
-            for (int j = 0; j < ns; ++j) Phk[a * ns + j] = Phi[a][j];
         for (int i = 0; i < ns; ++i)
             for (int j = i; j < ns; ++j) {
-                double v = HT(k, i, j);
-                for (int x = 0; x < nu; ++x) {
-                    v += Kk[x * ns + i] * HT(k, ns + x, j) + HT(k, i, ns + x) * Kk[x * ns + j];
-                    for (int y = 0; y < nu; ++y) v += Kk[x * ns + i] * HT(k, ns + x, ns + y) * Kk[y * ns + j];
+                double v;
+                if (nu == 1) {
+                    v = fma(-(Msu[i][0] * Lk[0]), Msu[j][0], Mss[i][j]);
+                } else {
+                    double acc = Msu[i][0] * Y[j][0];
+                    for (int x = 1; x < nu; ++x) acc = fma(Msu[i][x], Y[j][x], acc);
+                    v = Mss[i][j] - acc;
                 }
-                double acc = 0;
-                for (int a = 0; a < ns; ++a) acc += Phi[a][i] * T[a][j];
-                v += acc;
                 Pk[i * ns + j] = v;
                 Pk[j * ns + i] = v;
+            }
+        /* closed loop Phi_k = Abar + Bbar K_k (row-major), used by the sweeps */
+        double* Phk = W->Phit + (size_t)k * ns * ns;
+        for (int a = 0; a < ns; ++a)
+            for (int j = 0; j < ns; ++j) {
+                double v = P->Abar[a][j];
+                for (int x = 0; x < nu; ++x) v += P->Bbar[a][x] * Kk[x * ns + j];
+                Phk[a * ns + j] = v;
             }
     }
 #undef HT

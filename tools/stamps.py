@@ -25,7 +25,9 @@ st = np.zeros((B, 32))
 _lib.check(lib.bqp_debug_stamps(h.value, 20, 6, 616, _lib.ptr(st)), 'stamps')
 # STAMP(id) closes phase id; the phase names follow the barrier schedule of bqp_ocp.hip
 stage = ['wait B0 + residual combine', 'combine', 'wait B1', 'decide + factor', 'wait B2',
-         'solve pred', 'wait B3,B4', 'solve corr', 'wait B5,B6', 'update + partials']
+         'solve pred (post-fwd)', 'wait B3,B4', 'solve corr (post-fwd)', 'wait B5,B6', 'update + partials',
+         'solves: rhs + pre-pass', 'solves: backward sweep', 'solves: post-backward',
+         'solves: theta + forward sweep', 'solves: post-forward']
 row = ['wait B0', 'row residuals', 'rhs pred', 'wait B1,B2', 'wait B3',
        'ratio/comp/sigma/rhs corr', 'wait B4,B5', 'ratio corr + apply', 'wait B6 + lam side']
 ms, _ = h.kernel_ms()

@@ -112,8 +112,14 @@ __device__ __forceinline__ void chol_solve_small(const real* L, real (&b)[N]) {
 // Packed upper-triangular storage of the symmetric NS x NS Riccati matrices P_k: entry (i, j),
 // i <= j, at pk_idx(i, j); each stage slot is padded to an even number of doubles so that a
 // slot starts 16-byte aligned and is read back with ds_read_b128.
+// The stride is also chosen against LDS bank conflicts: lane k reads stage k's slot in the
+// solve pre-pass and the dual update, and ds_read_b64 banks are (a/4) mod 64 over 32-lane
+// halves, so a slot of 16 doubles (32 dwords) puts every lane on two banks (16-way); an even
+// stride that is 2 mod 4 doubles costs 2-way at most.
 __host__ __device__ constexpr int pk_len(int NS) { return NS * (NS + 1) / 2; }
-__host__ __device__ constexpr int pk_stride(int NS) { return (pk_len(NS) + 1) & ~1; }
+__host__ __device__ constexpr int pk_stride(int NS) {
+    return (((pk_len(NS) + 1) & ~1) % 4 == 0) ? ((pk_len(NS) + 1) & ~1) + 2 : ((pk_len(NS) + 1) & ~1);
+}
 __host__ __device__ constexpr int pk_idx(int NS, int i, int j) {
     return i <= j ? i * NS - i * (i - 1) / 2 + (j - i) : j * NS - j * (j - 1) / 2 + (i - j);
 }
@@ -131,7 +137,7 @@ enum : int {
 
 // Per-instance LDS layout (in doubles), sized from N at run time.
 struct QpLds {
-    int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, qu, fv, dsv, duv, dsc, duc, Dx, FD,
+    int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, bw, qu, fv, dsv, duv, dsc, duc, Dx, FD,
         blam, ebox, bnd, gpp, gpe, prp, hp, xch, total;
     __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad) {
         const int NS = NX + NP, NV = NS + NU, NB = NX + NU;
@@ -149,7 +155,8 @@ struct QpLds {
         o.ru = c;     c += (N + 1) * NU;             // stationarity residual (u part)
         o.re = c;     c += (N + 1) * NS;             // dynamics residual
         o.pv = c;     c += (N + 1) * NS;             // p_k of the backward sweep
-        o.wv = c;     c += (N + 1) * NS;             // P_{k+1} re_k
+        o.wv = c;     c += (N + 1) * NS;             // cw_k = Phi_k' P_{k+1} re_k (prep_iter)
+        o.bw = c;     c += (N + 1) * NU;             // Bbar' P_{k+1} re_k
         o.qu = c;     c += (N + 1) * NU;             // u right-hand side
         o.fv = c;     c += (N + 1) * NS;             // forward-sweep drift f_k
         o.dsv = c;    c += (N + 1) * NS;             // predictor direction (s)
@@ -584,6 +591,51 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         return ok;
     };
 
+    // ======================= once per factorisation ========================================
+    // The dynamics residual re_k is the same for the predictor and the corrector solve, so the
+    // part of the solves that depends on it alone is formed once: with w_k = P_{k+1} re_k,
+    //   cw_k = Phi_k' w_k (Phi_k = Abar + Bbar K_k; the pre-pass adds it to qt_k),
+    //   bw_k = Bbar' w_k (the post-backward pass adds it to Bbar' p_{k+1}).
+    auto prep_iter = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k < N) {
+                const real* Pn = W + L.P + (k + 1) * PST;
+                const real* Kk = W + L.K + k * NU * NS;
+                real rek[NS], wk[NS];
+#pragma unroll
+                for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    real v = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NS; ++c) v += Pn[pk_idx(NS, i, c)] * rek[c];
+                    wk[i] = v;
+                }
+#pragma unroll
+                for (int x = 0; x < NU; ++x) {
+                    real v = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NS; ++c) v += Bbar(c, x) * wk[c];
+                    W[L.bw + k * NU + x] = v;
+                }
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    real v = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NS; ++c) {
+                        real ph = Abar(c, i);
+#pragma unroll
+                        for (int x = 0; x < NU; ++x) ph += Bbar(c, x) * Kk[x * NS + i];
+                        v += ph * wk[c];
+                    }
+                    W[L.wv + k * NS + i] = v;
+                }
+            }
+        }
+    };
+
     // ======================= Newton solve ==================================================
     // right-hand side q = r_v + C'((lam o ri - rc)/t): the row wave supplies the box terms
     // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
@@ -632,46 +684,21 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                 }
             }
         }
-        // pre-pass: wv_k = P_{k+1} re_k, qt_k = qs_k + K_k' qu_k, qh_k = qt_k + Phi_k' wv_k ;
-        // p_N = qs_N.  qh carries everything of the backward recursion that does not depend on
-        // p_{k+1}, so the sequential sweep is one NS x NS mat-vec per stage.
+        // pre-pass: qh_k = qt_k + cw_k with qt_k = qs_k + K_k' qu_k (cw_k = Phi_k' P_{k+1} re_k
+        // is the right-hand-side-independent part, formed once per factorisation by
+        // prep_iter); p_N = qs_N.  qh carries everything of the backward recursion that does
+        // not depend on p_{k+1}, so the sequential sweep is one NS x NS mat-vec per stage.
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
-                const real* Pn = W + L.P + (k + 1) * PST;
                 const real* Kk = W + L.K + k * NU * NS;
-                real rek[NS], wk[NS], qtk[NS], Kl[NU][NS];
-#pragma unroll
-                for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
-#pragma unroll
-                for (int x = 0; x < NU; ++x)
-#pragma unroll
-                    for (int c = 0; c < NS; ++c) Kl[x][c] = Kk[x * NS + c];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    real v = 0.0;
-#pragma unroll
-                    for (int c = 0; c < NS; ++c) v += Pn[pk_idx(NS, i, c)] * rek[c];
-                    wk[i] = v;
-                    W[L.wv + k * NS + i] = v;
                     real qq = qs[j][i];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) qq += Kl[x][i] * qu[j][x];
-                    qtk[i] = qq;
-                }
-                // Phi_k = Abar + Bbar K_k, column i formed as in the factorisation
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    real v = qtk[i];
-#pragma unroll
-                    for (int c = 0; c < NS; ++c) {
-                        real ph = Abar(c, i);
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) ph += Bbar(c, x) * Kl[x][i];
-                        v += ph * wk[c];
-                    }
-                    W[L.qt_xpi + k * NS + i] = v;
+                    for (int x = 0; x < NU; ++x) qq += Kk[x * NS + i] * qu[j][x];
+                    W[L.qt_xpi + k * NS + i] = qq + W[L.wv + k * NS + i];
                 }
 #pragma unroll
                 for (int x = 0; x < NU; ++x) W[L.qu + k * NU + x] = qu[j][x];
@@ -721,17 +748,17 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
         wave_sync();
         STAMP(11);
-        // post-backward: kff_k = -Rhat^{-1}(qu_k + Bbar'(p_{k+1} + w_k)); f_k = Bbar kff_k + re_k
+        // post-backward: kff_k = -Rhat^{-1}((qu_k + bw_k) + Bbar' p_{k+1}); f_k = Bbar kff_k + re_k
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
                 real y[NS], r[NU];
 #pragma unroll
-                for (int i = 0; i < NS; ++i) y[i] = W[L.pv + (k + 1) * NS + i] + W[L.wv + k * NS + i];
+                for (int i = 0; i < NS; ++i) y[i] = W[L.pv + (k + 1) * NS + i];
 #pragma unroll
                 for (int x = 0; x < NU; ++x) {
-                    real v = qu[j][x];
+                    real v = qu[j][x] + W[L.bw + k * NU + x];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) v += Bbar(c, x) * y[c];
                     r[x] = -v;
@@ -859,6 +886,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     combine();
     int flag = 0;
     if (!factor()) flag = -8;
+    prep_iter();
     BARRIER();                                            // I1: predictor rhs of the start
     solve(L.dsv, L.duv);
     update_stage(1.0, L.dsv, L.duv);
@@ -903,6 +931,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             if (it == max_iter) stop = true;
         }
         if (!stop && !factor()) { flag = -8; stop = true; }
+        if (!stop) prep_iter();
         STAMP(3);
         if (lane == 0) X[X_STOP] = stop ? 1.0 : 0.0;
         BARRIER();                                        // B2: predictor rhs ready; stop flag
@@ -1230,8 +1259,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     };
 
     // ---- row passes along the direction (ids, idu): dt = -ri - C dv, dlam = (-rc - lam dt)/t.
-    //      mode 0: ratio max(-dt/t, -dlam/lam); 1: sum (t+al dt)(lam+al dlam) and store the
-    //      polytope predictor products; 2: apply t += al dt, lam += al dlam ----
+    //      mode 0: ratio max(-dt/t, -dlam/lam); 2: apply t += al dt, lam += al dlam (the
+    //      starting point; the iterations use pred_pass / box_apply / poly_apply_lam) ----
     auto row_pass = [&](int mode, bool corr, real smu, real al, int ids, int idu) __attribute__((always_inline)) -> real {
         real acc = 0.0;
 #pragma unroll
@@ -1245,8 +1274,6 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             if (mode == 0) {
                 acc = fmax(acc, -dt * frcp(tx[b]));
                 acc = fmax(acc, -dl * frcp(lx[b]));
-            } else if (mode == 1) {
-                acc += (tx[b] + al * dt) * (lx[b] + al * dl);
             } else {
                 // residual of the stepped iterate: r + al (+-dv + dt) = (1 - al) r
                 acc = fmax(acc, fabs((1.0 - al) * box_res(b)));
@@ -1269,9 +1296,6 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             if (mode == 0) {
                 acc = fmax(acc, -dt * frcp(tp[q]));
                 acc = fmax(acc, -dl * frcp(lp[q]));
-            } else if (mode == 1) {
-                acc += (tp[q] + al * dt) * (lp[q] + al * dl);
-                W[L.prp + r] = dt * dl;
             } else {
                 // the polytope residual Fp v + t - hp of the stepped iterate, by the linear
                 // update r + al (Fp dv + dt): the next iteration needs no residual pass (and
@@ -1282,17 +1306,16 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 lp[q] += al * dl;
             }
         }
-        if (mode == 1) return wsum(acc);
         return wmax(acc);   // mode 0: max ratio; mode 2: max |row residual| after the step
     };
 
-    // ---- predictor pass 2 fused with the corrector right-hand side: the complementarity sum
-    //      (t + al dt)(lam + al dlam) along the predictor direction, the stored products
-    //      dt dlam, and the corrector terms WITHOUT their sigma mu part,
-    //      e0 = (lam ri - t lam - dt dlam)/t (box slots in place, polytope rows as Fp'e0), plus
-    //      Fp'(1/t): e = e0 + sigma mu / t once sigma is known (rhs_corr_finish) ----
-    auto comp_rhs0 = [&](real al, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) -> real {
-        real acc = 0.0;
+    // ---- predictor pass: the ratio test, the complementarity sum and the corrector terms in ONE pass over the
+    //      rows.  Along the affine direction t dlam + lam dt = -t lam, so the complementarity
+    //      after any step a is  sum (t + a dt)(lam + a dlam) = S0 (1 - a) + a^2 S2  with
+    //      S0 = sum t lam (X_CS) and S2 = sum dt dlam: the sum no longer needs the step length,
+    //      and the pass returns the lane partials of max(-dt/t, -dlam/lam) and S2 ----
+    auto pred_pass = [&](real& rmx, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) -> real {
+        real rm = 0.0, s2 = 0.0;
 #pragma unroll
         for (int b = 0; b < BPL; ++b) {
             ROW_FENCE(b);
@@ -1304,8 +1327,11 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 const real rc = t * l;
                 const real dt = box_dir(b, L.dsv, L.duv);
                 const real dl = (-rc - l * dt) * it;
-                acc += (t + al * dt) * (l + al * dl);
-                e0 = (l * box_res(b) - (rc + dt * dl)) * it;
+                rm = fmax(rm, -dt * it);
+                rm = fmax(rm, -dl * frcp(l));
+                const real pr = dt * dl;
+                s2 += pr;
+                e0 = (l * box_res(b) - (rc + pr)) * it;
             }
             W[L.ebox + brow(b)] = e0;
         }
@@ -1329,15 +1355,130 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             const real rc = t * l;
             const real dt = -rp[q] - fd;
             const real dl = (-rc - l * dt) * it;
-            acc += (t + al * dt) * (l + al * dl);
+            rm = fmax(rm, -dt * it);
+            rm = fmax(rm, -dl * frcp(l));
             const real pr = dt * dl;
+            s2 += pr;
             W[L.prp + r] = pr;
             const real e0 = (l * rp[q] - (rc + pr)) * it;
 #pragma unroll
             for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }
         }
-        return acc;                                   // lane partial; reduced with gpe0, gpi
+        rmx = rm;
+        return s2;
     };
+
+    // ---- corrector step, box rows (before B6, while the stage vector in LDS is still the
+    //      current iterate's): t += a dt, lam += a dlam; returns max |(1 - a) r| ----
+    auto box_apply = [&](real smu, real al) __attribute__((always_inline)) -> real {
+        real fe = 0.0;
+#pragma unroll
+        for (int b = 0; b < BPL; ++b) {
+            ROW_FENCE(b);
+            if (!bpres(b)) continue;
+            const real pr = box_pred_prod(b);
+            const real rc = rcv(tx[b], lx[b], pr, true, smu);
+            const real dt = box_dir(b, L.dsc, L.duc);
+            const real dl = (-rc - lx[b] * dt) * frcp(tx[b]);
+            fe = fmax(fe, fabs((1.0 - al) * box_res(b)));
+            tx[b] += al * dt;
+            lx[b] += al * dl;
+        }
+        return fe;
+    };
+
+    // ---- corrector step of the polytope rows fused with the multiplier-side tables of the
+    //      new iterate (after B6, alongside the stage wave's update; every row reads its Fp
+    //      entries once for both): residual by the linear update r + a (Fp dv + dt), t, lam,
+    //      then Fp'lam, F'DF, sum t.lam exactly as lam_side; feb = the box rows' residual norm ----
+    auto poly_apply_lam = [&](real smu, real al, real feb) __attribute__((always_inline)) {
+        real cs = 0.0;
+#pragma unroll
+        for (int pv = 0; pv < BPL / 2; ++pv) {
+            ROW_FENCE(pv);
+            real d = 0.0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int b = 2 * pv + h;
+                if (bpres(b)) {
+                    d += lx[b] * frcp(tx[b]);
+                    cs += tx[b] * lx[b];
+                }
+                if (binrange(b)) W[L.blam + brow(b)] = bpres(b) ? lx[b] : 0.0;
+            }
+            if (binrange(2 * pv)) {
+                const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
+                W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
+            }
+        }
+        real gpp[NV];
+        real fdt[NV * (NV + 1) / 2];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gpp[c] = 0.0;
+#pragma unroll
+        for (int c = 0; c < NV * (NV + 1) / 2; ++c) fdt[c] = 0.0;
+        real fe = feb;
+        real dvp[NV];
+        load_v(dvp, L.dsc, L.duc);
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            ROW_FENCE(q);
+            const int r = lane + WAVE * q;
+            if (r < mp) {
+                real f[NV];
+#pragma unroll
+                for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
+                real fd = 0.0;
+#pragma unroll
+                for (int c = 0; c < NV; ++c) fd += f[c] * dvp[c];
+                const real rc = rcv(tp[q], lp[q], W[L.prp + r], true, smu);
+                const real dt = -rp[q] - fd;
+                const real dl = (-rc - lp[q] * dt) * frcp(tp[q]);
+                rp[q] += al * (fd + dt);
+                fe = fmax(fe, fabs(rp[q]));
+                tp[q] += al * dt;
+                lp[q] += al * dl;
+#pragma unroll
+                for (int c = 0; c < NV; ++c) gpp[c] += f[c] * lp[q];
+                cs += tp[q] * lp[q];
+                const real d = lp[q] * frcp(tp[q]);
+                int idx = 0;
+#pragma unroll
+                for (int i2 = 0; i2 < NV; ++i2) {
+                    const real di = d * f[i2];
+#pragma unroll
+                    for (int j2 = i2; j2 < NV; ++j2) fdt[idx++] += di * f[j2];
+                }
+            }
+        }
+        fe = wmax(fe);
+        if (lane == 0) X[X_FEASB] = fe;                   // row residual norm of the new iterate
+        constexpr int NT = NV * (NV + 1) / 2;
+        real red[NV + NT + 1];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) red[c] = gpp[c];
+#pragma unroll
+        for (int c = 0; c < NT; ++c) red[NV + c] = fdt[c];
+        red[NV + NT] = cs;
+        const real tot = wsum_t(red, lane);
+        if (lane < NV) {
+            W[L.gpp + lane] = tot;
+        } else if (lane < NV + NT) {
+            const int idx = lane - NV;
+            int i2 = 0, st = 0;
+#pragma unroll
+            for (int r = 1; r < NV; ++r) {
+                const int sr = r * NV - r * (r - 1) / 2;
+                if (idx >= sr) { i2 = r; st = sr; }
+            }
+            const int j2 = i2 + (idx - st);
+            W[L.FD + i2 * NV + j2] = tot;
+            W[L.FD + j2 * NV + i2] = tot;
+        } else if (lane == NV + NT) {
+            X[X_CS] = tot;
+        }
+    };
+
     auto rhs_corr_finish = [&](real smu, real tot) __attribute__((always_inline)) {
 #pragma unroll
         for (int b = 0; b < BPL; ++b)
@@ -1412,18 +1553,19 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         if (X[X_STOP] != 0.0) break;
         BARRIER();                                        // B3: predictor direction in (dsv, duv)
         STAMP(4);
-        const real mu = X[X_CS] * minv;
-        const real rm_a = row_pass(0, false, 0.0, 0.0, L.dsv, L.duv);
+        const real cs0 = X[X_CS];
+        const real mu = cs0 * minv;
+        real gpe0[NV], gpi[NV], rmx;
+        const real s2p = pred_pass(rmx, gpe0, gpi);
+        const real rm_a = wmax(rmx);
         const real al_aff = rm_a > 1.0 ? 1.0 / rm_a : 1.0;
-        real gpe0[NV], gpi[NV];
-        const real accp = comp_rhs0(al_aff, gpe0, gpi);
-        // joint transposed reduction: [Fp'e0, Fp'(1/t)] interleaved, then the complementarity sum
+        // joint transposed reduction: [Fp'e0, Fp'(1/t)] interleaved, then S2
         real red[2 * NV + 1];
 #pragma unroll
         for (int c = 0; c < NV; ++c) { red[2 * c] = gpe0[c]; red[2 * c + 1] = gpi[c]; }
-        red[2 * NV] = accp;
+        red[2 * NV] = s2p;
         const real tot = wsum_t(red, lane);
-        const real mua = rl(tot, 2 * NV) * minv;
+        const real mua = (cs0 * (1.0 - al_aff) + al_aff * al_aff * rl(tot, 2 * NV)) * minv;
         real sg = mua / mu;
         sg = sg * sg * sg;
         const real smu = sg * mu;
@@ -1436,11 +1578,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         real al = (rm > 1.0 ? 1.0 / rm : 1.0) * a.tau;
         if (al > 1.0) al = 1.0;
         if (lane == 0) X[X_ALPHA] = al;
-        const real fe = row_pass(2, true, smu, al, L.dsc, L.duc);
-        if (lane == 0) X[X_FEASB] = fe;                   // row residual norm of the new iterate
+        const real feb = box_apply(smu, al);
         STAMP(7);
         BARRIER();                                        // B6
-        lam_side();
+        poly_apply_lam(smu, al, feb);
         STAMP(8);
     }
 

@@ -39,7 +39,7 @@ typedef struct {
     /* work */
     double *rs, *ru, *re, *rix, *riu, *rip;
     double *ds, *du, *dpi, *dtx, *dlx, *dtu, *dlu, *dtp, *dlp;
-    double *Ptab, *Ktab, *Rinv, *Phit, *p, *qs, *qu, *wv, *qt, *qh, *kff, *f;
+    double *Ptab, *Ktab, *Rinv, *Phit, *p, *qs, *qu, *wv, *cw, *qt, *qh, *kff, *f;
     double *Dx, *Du, *FD;
     double *itx, *ilx, *itu, *ilu, *itp, *ilp;   /* 1/t, 1/lam (once per iteration) */
     double P0inv[MAXNS * MAXNS];
@@ -337,6 +337,32 @@ static int factor(const prob_t* P, work_t* W) {
     return 0;
 }
 
+/* once per factorisation: the part of both solves that depends on the dynamics residual alone
+ * (the kernel's prep_iter): w_k = P_{k+1} re_k, cw_k = Phi_k' w_k, bw_k = Bbar' w_k */
+static void prep_iter(const prob_t* P, work_t* W) {
+    const int N = P->N, ns = P->ns, nu = P->nu;
+    for (int k = 0; k < N; ++k) {
+        const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
+        const double* Phk = W->Phit + (size_t)k * ns * ns;
+        double w[MAXNS];
+        for (int i = 0; i < ns; ++i) {
+            double v = 0;
+            for (int j = 0; j < ns; ++j) v += Pn[i * ns + j] * W->re[k * ns + j];
+            w[i] = v;
+        }
+        for (int a = 0; a < nu; ++a) {
+            double v = 0;
+            for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * w[j];
+            W->wv[k * nu + a] = v;
+        }
+        for (int i = 0; i < ns; ++i) {
+            double v = 0;
+            for (int j = 0; j < ns; ++j) v += Phk[j * ns + i] * w[j];
+            W->cw[k * ns + i] = v;
+        }
+    }
+}
+
 /* ---------------- solve ---------------- */
 /* rcx/rcu/rcp: complementarity right-hand side per row */
 static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const double* rcu,
@@ -373,27 +399,16 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
         if (P->kp < N)
             for (int i = 0; i < nu; ++i) W->qu[P->kp * nu + i] += gp[ns + i];
     }
-    /* pre-pass: wv_k = P_{k+1} re_k ; qt_k = qs_k + K_k' qu_k */
+    /* pre-pass: qt_k = qs_k + K_k' qu_k, qh_k = qt_k + cw_k (cw_k = Phi_k' P_{k+1} re_k, formed
+     * once per factorisation by prep_iter), then the backward sweep
+     * p_k = Phi_k' p_{k+1} + qh_k   (= Phi_k'(p_{k+1} + w_k) + qt_k) */
     for (int k = 0; k < N; ++k) {
-        const double* Pn = W->Ptab + (size_t)(k + 1) * ns * ns;
         const double* Kk = W->Ktab + (size_t)k * nu * ns;
         for (int i = 0; i < ns; ++i) {
-            double v = 0;
-            for (int j = 0; j < ns; ++j) v += Pn[i * ns + j] * W->re[k * ns + j];
-            W->wv[k * ns + i] = v;
             double q = W->qs[k * ns + i];
             for (int a = 0; a < nu; ++a) q += Kk[a * ns + i] * W->qu[k * nu + a];
             W->qt[k * ns + i] = q;
-        }
-    }
-    /* qh_k = qt_k + Phi_k' w_k (parallel over k), then the backward sweep
-     * p_k = Phi_k' p_{k+1} + qh_k   (= Phi_k'(p_{k+1} + w_k) + qt_k) */
-    for (int k = 0; k < N; ++k) {
-        const double* Phk = W->Phit + (size_t)k * ns * ns;
-        for (int i = 0; i < ns; ++i) {
-            double v = W->qt[k * ns + i];
-            for (int j = 0; j < ns; ++j) v += Phk[j * ns + i] * W->wv[k * ns + j];
-            W->qh[k * ns + i] = v;
+            W->qh[k * ns + i] = q + W->cw[k * ns + i];
         }
     }
     for (int i = 0; i < ns; ++i) W->p[N * ns + i] = W->qs[N * ns + i];
@@ -405,13 +420,13 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
             W->p[k * ns + i] = v;
         }
     }
-    /* post-backward: kff_k = -Rinv_k (qu_k + Bbar'(p_{k+1} + w_k)); f_k = Bbar kff_k + re_k */
+    /* post-backward: kff_k = -Rinv_k ((qu_k + bw_k) + Bbar' p_{k+1}); f_k = Bbar kff_k + re_k
+     * (wv holds bw_k = Bbar' P_{k+1} re_k, prep_iter) */
     for (int k = 0; k < N; ++k) {
-        double y[MAXNS], r[MAXNU];
-        for (int i = 0; i < ns; ++i) y[i] = W->p[(k + 1) * ns + i] + W->wv[k * ns + i];
+        double r[MAXNU];
         for (int a = 0; a < nu; ++a) {
-            double v = W->qu[k * nu + a];
-            for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * y[j];
+            double v = W->qu[k * nu + a] + W->wv[k * nu + a];
+            for (int j = 0; j < ns; ++j) v += P->Bbar[j][a] * W->p[(k + 1) * ns + j];
             r[a] = v;
         }
         for (int a = 0; a < nu; ++a) r[a] = -r[a];
@@ -523,22 +538,23 @@ static double max_step(const prob_t* P, work_t* W) {
     return rm > 1.0 ? 1.0 / rm : 1.0;
 }
 
-static double comp_after(const prob_t* P, work_t* W, double a) {
+static double comp_s2(const prob_t* P, work_t* W) {
+    /* sum dt dlam over the present rows */
     const int N = P->N, nx = P->nx, nu = P->nu;
     double s = 0;
     for (int k = 1; k <= N; ++k)
         for (int i = 0; i < nx; ++i) {
             int o = (k * nx + i) * 2;
-            if (isfinite(W->xub[k * nx + i])) s += (W->tx[o] + a * W->dtx[o]) * (W->lx[o] + a * W->dlx[o]);
-            if (isfinite(W->xlb[k * nx + i])) s += (W->tx[o + 1] + a * W->dtx[o + 1]) * (W->lx[o + 1] + a * W->dlx[o + 1]);
+            if (isfinite(W->xub[k * nx + i])) s += W->dtx[o] * W->dlx[o];
+            if (isfinite(W->xlb[k * nx + i])) s += W->dtx[o + 1] * W->dlx[o + 1];
         }
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int o = (k * nu + i) * 2;
-            if (isfinite(W->uub[k * nu + i])) s += (W->tu[o] + a * W->dtu[o]) * (W->lu[o] + a * W->dlu[o]);
-            if (isfinite(W->ulb[k * nu + i])) s += (W->tu[o + 1] + a * W->dtu[o + 1]) * (W->lu[o + 1] + a * W->dlu[o + 1]);
+            if (isfinite(W->uub[k * nu + i])) s += W->dtu[o] * W->dlu[o];
+            if (isfinite(W->ulb[k * nu + i])) s += W->dtu[o + 1] * W->dlu[o + 1];
         }
-    for (int r = 0; r < P->mp; ++r) s += (W->tp[r] + a * W->dtp[r]) * (W->lp[r] + a * W->dlp[r]);
+    for (int r = 0; r < P->mp; ++r) s += W->dtp[r] * W->dlp[r];
     return s;
 }
 
@@ -586,6 +602,7 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     for (int i = 0; i < nxr + nur + P->mp; ++i) rcx[i] = 1.0;
     residuals(P, W, &stat, &feas, &cs, &mc, &gs);
     if (factor(P, W)) { free(rcx); return -8; }
+    prep_iter(P, W);
     solve_kkt(P, W, rcx, rcu, rcp);
     for (int i = 0; i < (N + 1) * ns; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
     for (int i = 0; i < N * nu; ++i) W->u[i] += W->du[i];
@@ -667,12 +684,15 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         if (mu < mu_min) mu_min = mu;
         if (it == op->max_iter) break;
         if (factor(P, W)) { flag = -8; break; }
+        prep_iter(P, W);
         for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i];
         for (int i = 0; i < nur; ++i) rcu[i] = W->tu[i] * W->lu[i];
         for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r];
         solve_kkt(P, W, rcx, rcu, rcp);
         double a = max_step(P, W);
-        double mua = comp_after(P, W, a) / (mc > 0 ? mc : 1);
+        /* along the affine direction t dlam + lam dt = -t lam: the complementarity after the
+         * step is cs (1 - a) + a^2 sum dt dlam (the kernel's pred_pass) */
+        double mua = (cs * (1.0 - a) + a * a * comp_s2(P, W)) / (mc > 0 ? mc : 1);
         double sg = mua / mu;
         sg = sg * sg * sg;
         for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i] + W->dtx[i] * W->dlx[i] - sg * mu;
@@ -762,7 +782,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.Ptab = alloc0((size_t)(N + 1) * ns * ns); W.Ktab = alloc0((size_t)N * nu * ns);
         W.Phit = alloc0((size_t)N * ns * ns);
         W.Rinv = alloc0((size_t)N * nu * nu); W.p = alloc0((N + 1) * ns);
-        W.qs = alloc0((N + 1) * ns); W.qu = alloc0(N * nu); W.wv = alloc0(N * ns);
+        W.qs = alloc0((N + 1) * ns); W.qu = alloc0(N * nu); W.wv = alloc0(N * ns); W.cw = alloc0(N * ns);
         W.qt = alloc0(N * ns); W.qh = alloc0(N * ns); W.kff = alloc0(N * nu); W.f = alloc0(N * ns);
         W.Dx = alloc0((N + 1) * nx); W.Du = alloc0(N * nu); W.FD = alloc0(nv * nv);
         W.itx = alloc0((N + 1) * nx * 2); W.ilx = alloc0((N + 1) * nx * 2);
@@ -835,7 +855,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.lp); free(W.rs); free(W.ru); free(W.re); free(W.rix); free(W.riu); free(W.rip);
         free(W.ds); free(W.du); free(W.dpi); free(W.dtx); free(W.dlx); free(W.dtu); free(W.dlu);
         free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Phit); free(W.Ktab); free(W.Rinv); free(W.p);
-        free(W.qs); free(W.qu); free(W.wv); free(W.qt); free(W.qh); free(W.kff); free(W.f); free(W.Dx);
+        free(W.qs); free(W.qu); free(W.wv); free(W.cw); free(W.qt); free(W.qh); free(W.kff); free(W.f); free(W.Dx);
         free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
         free(W.ilp);
     }

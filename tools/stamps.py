@@ -29,7 +29,7 @@ stage = ['wait B0 + residual combine', 'combine', 'wait B1', 'decide + factor', 
          'solves: rhs + pre-pass', 'solves: backward sweep', 'solves: post-backward',
          'solves: theta + forward sweep', 'solves: post-forward']
 row = ['wait B0', 'row residuals', 'rhs pred', 'wait B1,B2', 'wait B3',
-       'ratio/comp/sigma/rhs corr', 'wait B4,B5', 'ratio corr + apply', 'wait B6 + lam side']
+       'pred pass/sigma/rhs corr', 'wait B4,B5', 'ratio corr + box apply', 'wait B6 + poly apply/lam side']
 ms, _ = h.kernel_ms()
 it = r.iterations.mean()
 print('batch %d kernel %.3f ms, mean iterations %.2f' % (B, ms, it))

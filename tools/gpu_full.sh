@@ -1,11 +1,11 @@
 #!/bin/bash
-# full GPU check of the tree: all gpu tests, smoke, stamps, C2 bench (with CPU leg), C3 / C5 lines
+# full GPU check of the tree: all gpu tests, smoke, C2 bench (with CPU leg), C3 / C4 / C5 lines
+# (phase stamps: tools/gpu_stamps_configs.sh, needs `make -C learning-based-mpc_amd stamps`)
 set -o pipefail
 OUT=gpurun_out/${1:-full}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 90 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-timeout -k 10 120 python tools/stamps.py 1024 > $OUT/stamps.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 50 --warmup 5 > $OUT/bench.log 2>&1 && \
 timeout -k 10 200 python bench.py --config C5 --steps 5 --warmup 1 --no-cpu > $OUT/c5.log 2>&1 && \
 timeout -k 10 200 python bench.py --config C5 --precision fp32 --steps 5 --warmup 1 --no-cpu > $OUT/c5_fp32.log 2>&1 && \

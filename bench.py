@@ -228,7 +228,7 @@ class GpuSolver:
         self.oo = torch.empty((B * C.sizeof(_lib.Output),), dtype=torch.uint8, device=dev)
         self.lib = bqp.load()
         self.h = bqp.Handle(local)
-        self.opt = _lib.options(precision=1 if precision == 'fp32' else 0)
+        self.opt = _lib.options(precision={'fp64': 0, 'fp32': 1, 'mixed': 2}[precision])
         self.stream = torch.cuda.current_stream(dev)
 
     def step(self, with_out=False):
@@ -299,7 +299,7 @@ def main():
     ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C3', 'C4', 'C5', 'CL'])
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32'],
+    ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32', 'mixed'],
                     help='structured solver arithmetic (C5 compares both)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
@@ -442,7 +442,7 @@ def main():
             'value': round(value, 1), 'unit': 'QP-steps/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
             'higher_is_better': True, 'scaling': wl['scaling'], 'vs_baseline': None,
-            'dtype': 'f32' if args.precision == 'fp32' else 'f64',
+            'dtype': {'fp64': 'f64', 'fp32': 'f32', 'mixed': 'f32+f64'}[args.precision],
             'data': wl['data'] + (' [CPU dry run: stub solver, gloo]' if args.dry_run else ''),
             'config': {'workload': wl['text'], 'batch_per_gpu': B, 'horizon': N,
                        'parallelism': 'dp%d' % world},

@@ -52,8 +52,12 @@ typedef struct {
     double tol_feas;   /* primal residual inf-norm / (1 + |bounds, rhs|_inf), default 1e-10 */
     double tol_comp;   /* average complementarity mu (absolute), default 1e-14 */
     double tau;        /* fraction-to-boundary, default 0.995 */
-    int precision;     /* 0 = fp64 (default); 1 = fp32 solver arithmetic/LDS state (structured API; inputs
-                          and outputs stay fp64; tolerances floored at 1e-5 / 1e-6 / 1e-9) */
+    int precision;     /* structured API: 0 = fp64 (default); 1 = fp32 solver arithmetic/LDS state
+                          (inputs and outputs stay fp64; tolerances floored at 1e-5 / 1e-6 / 1e-9);
+                          2 = mixed: an fp32 launch to those floored tolerances, then an fp64 launch
+                          that continues every instance from its fp32 iterate to the fp64
+                          tolerances (fp64 results; instances the fp32 phase ends with -2/-8
+                          restart in fp64) */
     int want_duals;    /* reserved (set 0): the structured API writes the multiplier outputs
                           whenever its `duals` argument is non-NULL */
 } bqp_options;

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -44,6 +45,7 @@ struct bqp_handle_s {
     DevBuf dwork;  // dense per-instance scratch
     DevBuf lwork;  // learning-based MPC (SQP) buffers
     DevBuf cwork;  // closed-loop simulation buffers
+    DevBuf hwork;  // mixed precision: fp32 -> fp64 handoff records
     int last_batch = 0;
 };
 
@@ -140,6 +142,7 @@ int bqp_destroy(bqp_handle h) {
         h->dwork.release();
         h->lwork.release();
         h->cwork.release();
+        h->hwork.release();
         if (h->ev0) hipEventDestroy(h->ev0);
         if (h->ev1) hipEventDestroy(h->ev1);
         if (h->stream) hipStreamDestroy(h->stream);
@@ -188,25 +191,44 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     hipStream_t st = (hipStream_t)stream;
     bqp_options o;
     resolve(opt, &o);
-    const bool f32 = o.precision == 1;     // fp32 instantiation (bqp_ocp_f32.hip), config C5
-    if (f32) {
-        // fp32 arithmetic cannot resolve the fp64 defaults: floor the stopping tolerances
-        o.tol_stat = std::max(o.tol_stat, 1e-5);
-        o.tol_feas = std::max(o.tol_feas, 1e-6);
-        o.tol_comp = std::max(o.tol_comp, 1e-9);
+    if (o.precision < 0 || o.precision > 2) return BQP_E_ARG;
+    const bool f32 = o.precision == 1;     // fp32 instantiation (bqp_ocp_f32.hip)
+    const bool mixed = o.precision == 2;   // fp32 phase, then fp64 from the fp32 iterate
+    bqp_options o32 = o;
+    // fp32 arithmetic cannot resolve the fp64 defaults: floor the stopping tolerances
+    o32.tol_stat = std::max(o.tol_stat, 1e-5);
+    o32.tol_feas = std::max(o.tol_feas, 1e-6);
+    o32.tol_comp = std::max(o.tol_comp, 1e-9);
+    if (mixed) {
+        // hand over once the fp32 iterate is feasible to 1e-6 and mu <= 1e-7: the fp64 launch then
+        // needs ~3 iterations and ends at the fp64 solve's KKT accuracy (duals within 5e-8 of
+        // lambda*); a later switch (mu 1e-9) saves 4 % more time but leaves the duals at 1.7e-7
+        // (tools/diag_mixed.py, profiles/r02_mx/diag_switch.log).  BQP_MIXED_MU overrides, for that sweep.
+        o32.tol_comp = std::max(o.tol_comp, 1e-7);
+        const char* e = getenv("BQP_MIXED_MU");
+        if (e) o32.tol_comp = atof(e);
     }
+    if (f32) o = o32;
     const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
     const int nv = nx + nu + np;
     const int mp = d->n_poly;
     const int hstride = nv * nv + 1;
     const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));   // = the kernel's RPL * 64
     const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;   // elements
-    const int per_wave = f32 ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad)
-                             : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
-    const size_t lds_budget = 160 * 1024 / (f32 ? sizeof(float) : sizeof(double));
-    int wpb = 4;   // instances per workgroup (two waves each)
-    while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
-    if ((size_t)shared_doubles + (size_t)per_wave > lds_budget) return BQP_E_UNSUPPORTED;
+    // instances per workgroup (two waves each) that fit the 160 KB of LDS
+    auto fit_wpb = [&](bool single, int& wpb) -> bool {
+        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad)
+                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
+        const size_t lds_budget = 160 * 1024 / (single ? sizeof(float) : sizeof(double));
+        // long horizons (N + 1 > 64, two stages per lane) are compiled for <= 256 threads per
+        // workgroup: one wave per SIMD, whose 512 registers hold the doubled stage state
+        wpb = (N + 1 > 64) ? 2 : 4;
+        while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
+        return (size_t)shared_doubles + (size_t)per_wave <= lds_budget;
+    };
+    int wpb = 1, wpb32 = 1;
+    if (!fit_wpb(f32, wpb)) return BQP_E_UNSUPPORTED;
+    if (mixed && !fit_wpb(true, wpb32)) return BQP_E_UNSUPPORTED;
     // workspace: H, Fp, stats
     const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * bqp::STATS_W;
 #ifdef BQP_STAMPS
@@ -240,13 +262,34 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     h->last_batch = batch;
 #endif
     HIP_TRY(hipEventRecord(h->ev0, st));
-    if (f32)
-        HIP_TRY(bqp::launch_ocp_f32(a, nx, nu, np, st));
-    else
+    if (mixed) {
+        // phase 1: fp32 to the floored tolerances, iterate to the handoff records
+        const int hf = bqp::ocp_hand_floats(N, nx, nu, np, mp);
+        if (hf <= 0) return BQP_E_UNSUPPORTED;
+        const size_t hrec = ((size_t)hf + 63) & ~(size_t)63;
+        HIP_TRY(h->hwork.reserve(sizeof(float) * hrec * batch + 2 * sizeof(int) * (size_t)batch));
+        float* hb = (float*)h->hwork.p;
+        int* hflag = (int*)(hb + hrec * batch);
+        int* hit = hflag + batch;
+        bqp::OcpKernelArgs a1 = a;
+        a1.wpb = wpb32;
+        a1.max_iter = o32.max_iter; a1.tol_stat = o32.tol_stat; a1.tol_feas = o32.tol_feas;
+        a1.tol_comp = o32.tol_comp;
+        a1.exitflag = hflag;
+        a1.hand_out = hb; a1.hand_it = hit; a1.hand_stride = (int64_t)hrec;
+        a1.pi_out = a1.lamx_out = a1.lamu_out = a1.lamp_out = nullptr;
+        HIP_TRY(bqp::launch_ocp_f32(a1, nx, nu, np, st));
+        // phase 2: fp64 from the handed-over iterates
+        a.hand_in = hb; a.hand_flag = hflag; a.hand_it = hit; a.hand_stride = (int64_t)hrec;
         HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
+    } else if (f32) {
+        HIP_TRY(bqp::launch_ocp_f32(a, nx, nu, np, st));
+    } else {
+        HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
+    }
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->timed = true;
-    h->launches = 1;
+    h->launches = mixed ? 2 : 1;
     if (out) HIP_TRY(bqp::launch_ocp_finalize(Sd, batch, out, st));
     return BQP_OK;
 }

@@ -27,10 +27,21 @@ struct OcpKernelArgs {
     double* stats;  // batch x STATS_W (see STATS_W)
     double *pi_out, *lamx_out, *lamu_out, *lamp_out;
     double* stamps;  // diagnostic build (BQP_STAMPS): batch x 16 phase cycle counts
+    // mixed precision (bqp_options.precision = 2): the fp32 launch ends each instance at its
+    // (floored) tolerances and writes its iterate (s, pi, u, row slacks and multipliers) to
+    // hand_out; the fp64 launch continues from hand_in the instances whose fp32 exit flag
+    // (hand_flag) is 1 or 0, and starts the others (-2, -8) from its own initial point
+    float* hand_out;
+    const float* hand_in;
+    const int* hand_flag;
+    int* hand_it;           // fp32-phase iterations (written by the fp32 launch, added by the fp64 one)
+    int64_t hand_stride;    // floats per instance (ocp_hand_floats)
 };
 
 bool ocp_supported(int nx, int nu, int np);
 int ocp_rpl_for(int mp);
+int ocp_bpl_for(int N, int nx, int nu);
+int ocp_hand_floats(int N, int nx, int nu, int np, int mp);
 int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad);
 hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 // fp32 instantiation (bqp_ocp_f32.hip): LDS element count per instance (floats) and launch

@@ -178,6 +178,27 @@ struct QpLds {
     }
 };
 
+// Mixed-precision handoff record of one instance (floats, OcpKernelArgs::hand_*): per stage
+// k = 0..N the vectors s_k, pi_k, u_k (u_N = 0), then from a 64-aligned offset the row wave's
+// box rows [t: BPL x 64 | lam: BPL x 64] and polytope rows [t: RPL x 64 | lam: RPL x 64],
+// slot-major so that a wave's store of one slot is one coalesced 256-byte line
+__host__ __device__ constexpr int hand_stage_w(int NS, int NU) { return 2 * NS + NU; }
+__host__ __device__ constexpr int hand_rows_off(int N, int NS, int NU) {
+    return ((N + 1) * hand_stage_w(NS, NU) + 63) & ~63;
+}
+// a warm (continued) instance of the fp64 launch: its fp32 phase ended with 1 or 0
+// (fp64 instantiation only; the fp32 one only writes handoff records)
+#ifdef BQP_F32
+#define BQP_HAND_IN 0
+#define BQP_HAND_OUT 1
+#else
+#define BQP_HAND_IN 1
+#define BQP_HAND_OUT 0
+#endif
+__device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
+    return BQP_HAND_IN && a.hand_in && (a.hand_flag[inst] == 1 || a.hand_flag[inst] == 0);
+}
+
 #ifdef BQP_STAMPS
 // diagnostic build only (see tools/stamps.py): cycles per phase and per wave role, summed over
 // the solve; slots 0..15 stage wave, 16..31 row wave
@@ -878,22 +899,47 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 
     // ======================= initial point ==================================================
     real feasA = 0, gsA = 0;
-    write_state();
-    stage_partials(feasA, gsA);
-    BARRIER();                                            // I0: row-side tables of t = lam = 1
-    const real minv = 1.0 / fmax(X[X_CNT], 1.0);
-    const real bscale = fmax(x0max, X[X_BSR]);
-    combine();
-    int flag = 0;
-    if (!factor()) flag = -8;
-    prep_iter();
-    BARRIER();                                            // I1: predictor rhs of the start
-    solve(L.dsv, L.duv);
-    update_stage(1.0, L.dsv, L.duv);
-    BARRIER();                                            // I2: row wave takes dt (old iterate), shifts
-    BARRIER();                                            // I3: row wave done with the old iterate
-    write_state();
-    stage_partials(feasA, gsA);
+    real minv, bscale;
+    int flag = 0, it0 = 0;
+    if (hand_warm(a, inst)) {
+        // continue the fp32 phase's iterate (mixed precision); x_0 stays the exact fp64 state
+        const float* hb = a.hand_in + (int64_t)inst * a.hand_stride;
+        constexpr int SW = hand_stage_w(NS, NU);
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                s[j][i] = (k == 0 && i < NX) ? s[j][i] : (real)hb[k * SW + i];
+                pi[j][i] = (real)hb[k * SW + NS + i];
+            }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) u[j][i] = (k < N) ? (real)hb[k * SW + 2 * NS + i] : 0.0;
+        }
+        write_state();
+        stage_partials(feasA, gsA);
+        BARRIER();                                        // W0: row wave forms residuals + tables
+        minv = 1.0 / fmax(X[X_CNT], 1.0);
+        bscale = fmax(x0max, X[X_BSR]);
+        it0 = a.hand_it[inst];
+    } else {
+        write_state();
+        stage_partials(feasA, gsA);
+        BARRIER();                                        // I0: row-side tables of t = lam = 1
+        minv = 1.0 / fmax(X[X_CNT], 1.0);
+        bscale = fmax(x0max, X[X_BSR]);
+        combine();
+        if (!factor()) flag = -8;
+        prep_iter();
+        BARRIER();                                        // I1: predictor rhs of the start
+        solve(L.dsv, L.duv);
+        update_stage(1.0, L.dsv, L.duv);
+        BARRIER();                                        // I2: row wave takes dt (old iterate), shifts
+        BARRIER();                                        // I3: row wave done with the old iterate
+        write_state();
+        stage_partials(feasA, gsA);
+    }
 
     // ======================= main loop ======================================================
     int it = 0;
@@ -955,6 +1001,26 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     }
 
     // ======================= outputs =======================================================
+    if (BQP_HAND_OUT && a.hand_out) {
+        // fp32 phase of the mixed mode: hand the iterate to the fp64 launch
+        float* hb = a.hand_out + (int64_t)inst * a.hand_stride;
+        constexpr int SW = hand_stage_w(NS, NU);
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) { hb[k * SW + i] = (float)s[j][i]; hb[k * SW + NS + i] = (float)pi[j][i]; }
+#pragma unroll
+            for (int i = 0; i < NU; ++i) hb[k * SW + 2 * NS + i] = (k < N) ? (float)u[j][i] : 0.0f;
+        }
+        STAMP_STORE(0);
+        if (lane == 0) {
+            a.exitflag[inst] = flag;
+            a.hand_it[inst] = it;
+        }
+        return;
+    }
     real fv = 0.0;
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
@@ -998,7 +1064,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         a.exitflag[inst] = flag;
         if (a.stats) {
             double* so = a.stats + (int64_t)inst * STATS_W;
-            so[0] = (double)it; so[1] = stat; so[2] = feas; so[3] = mu; so[4] = feq; so[5] = fin;
+            so[0] = (double)(it + it0); so[1] = stat; so[2] = feas; so[3] = mu; so[4] = feq; so[5] = fin;
         }
     }
 }
@@ -1489,6 +1555,25 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     };
 
     // ======================= initial point ==================================================
+    constexpr int HR_T = 0, HR_L = BPL * WAVE, HP_T = 2 * BPL * WAVE, HP_L = (2 * BPL + RPL) * WAVE;
+    if (hand_warm(a, inst)) {
+        // continue the fp32 phase's iterate (mixed precision): slacks and multipliers as they
+        // were, the residuals and multiplier tables formed afresh in fp64
+        const float* hb = a.hand_in + (int64_t)inst * a.hand_stride + hand_rows_off(N, NS, NU);
+#pragma unroll
+        for (int b = 0; b < BPL; ++b) {
+            tx[b] = (real)hb[HR_T + b * WAVE + lane];
+            lx[b] = (real)hb[HR_L + b * WAVE + lane];
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            tp[q] = (real)hb[HP_T + q * WAVE + lane];
+            lp[q] = (real)hb[HP_L + q * WAVE + lane];
+        }
+        BARRIER();                                        // W0: the stage vectors are in LDS
+        row_residuals();
+        lam_side();
+    } else {
     lam_side();
     BARRIER();                                            // I0
     row_residuals();
@@ -1540,6 +1625,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     }
     lam_side();
     BARRIER();                                            // I3
+    }
 
     // ======================= main loop ======================================================
     for (;;) {
@@ -1586,6 +1672,22 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     }
 
     // ======================= outputs (multipliers) ==========================================
+    if (BQP_HAND_OUT && a.hand_out) {
+        // fp32 phase of the mixed mode: slacks and multipliers to the handoff record
+        float* hb = a.hand_out + (int64_t)inst * a.hand_stride + hand_rows_off(N, NS, NU);
+#pragma unroll
+        for (int b = 0; b < BPL; ++b) {
+            hb[HR_T + b * WAVE + lane] = (float)tx[b];
+            hb[HR_L + b * WAVE + lane] = (float)lx[b];
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            hb[HP_T + q * WAVE + lane] = (float)tp[q];
+            hb[HP_L + q * WAVE + lane] = (float)lp[q];
+        }
+        STAMP_STORE(16);
+        return;
+    }
 #pragma unroll
     for (int b = 0; b < BPL; ++b) {
         ROW_FENCE(b);
@@ -1613,7 +1715,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 // kernel: QPB instances per workgroup, waves [0, QPB) stage waves, [QPB, 2 QPB) row waves
 // ==========================================================================================
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
-__global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
+__global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernelArgs a) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -1645,14 +1747,19 @@ __global__ void __launch_bounds__(512) ocp_ipm_kernel(OcpKernelArgs a) {
 // ------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------------
-// LDS elements (of the instantiation's precision) per instance
-int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad) {
-#ifdef BQP_F32
-    return sp::QpLds::make(N, nx, nu, np, mpad).total;
+// The kernel instantiations are split over translation units by model family so that the
+// build compiles them in parallel (Makefile: BQP_FAMILY=1 MG nx4/nu1/np1 with the dispatcher
+// and host helpers, BQP_FAMILY=2 DI nx2/nu2/np2); without BQP_FAMILY one unit holds all.
+#if !defined(BQP_FAMILY)
+#define BQP_FAM_MG 1
+#define BQP_FAM_DI 1
+#elif BQP_FAMILY == 1
+#define BQP_FAM_MG 1
+#define BQP_FAM_DI 0
 #else
-    return dp::QpLds::make(N, nx, nu, np, mpad).total;
+#define BQP_FAM_MG 0
+#define BQP_FAM_DI 1
 #endif
-}
 
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipStream_t st) {
@@ -1693,6 +1800,27 @@ static hipError_t launch_spl(const OcpKernelArgs& a, int spl, int rpl, int block
     return hipErrorInvalidValue;
 }
 
+hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st);
+hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st);
+
+#if BQP_FAM_MG
+hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st) {
+#ifdef BQP_ISA_ONLY_MG10
+    // codegen inspection build (make isa): the MG N<64, 616-row instance only
+    if (spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st);
+    return hipErrorInvalidValue;
+#else
+    return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);
+#endif
+}
+#endif
+#if BQP_FAM_DI && !defined(BQP_ISA_ONLY_MG10)
+hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st) {
+    return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st);
+}
+#endif
+
+#if BQP_FAM_MG
 #ifndef BQP_F32
 bool ocp_supported(int nx, int nu, int np) {
     return (nx == 4 && nu == 1 && np == 1) || (nx == 2 && nu == 2 && np == 2);
@@ -1706,7 +1834,28 @@ int ocp_rpl_for(int mp) {
     return -1;
 }
 
+// box rows per lane of the instantiation launch_spl selects (-1: outside the compiled set)
+int ocp_bpl_for(int N, int nx, int nu) {
+    const int nbr = (N + 1) * 2 * (nx + nu);
+    if (N + 1 <= WAVE) return nbr <= 4 * WAVE ? 4 : (nbr <= 10 * WAVE ? 10 : -1);
+    return nbr <= 16 * WAVE ? 16 : (nbr <= 20 * WAVE ? 20 : -1);
+}
+
+int ocp_hand_floats(int N, int nx, int nu, int np, int mp) {
+    const int bpl = ocp_bpl_for(N, nx, nu), rpl = ocp_rpl_for(mp > 1 ? mp : 1);
+    if (bpl < 0 || rpl < 0) return -1;
+    return dp::hand_rows_off(N, nx + np, nu) + 2 * (bpl + rpl) * WAVE;
+}
 #endif
+
+// LDS elements (of the instantiation's precision) per instance
+int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad) {
+#ifdef BQP_F32
+    return sp::QpLds::make(N, nx, nu, np, mpad).total;
+#else
+    return dp::QpLds::make(N, nx, nu, np, mpad).total;
+#endif
+}
 
 hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st) {
     const int spl = (a.N + 1 <= 64) ? 1 : 2;
@@ -1714,15 +1863,12 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
     const size_t lds = sizeof(real) * ((size_t)a.shared_doubles +
                                        (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad));
-#ifdef BQP_ISA_ONLY_MG10
-    // codegen inspection build (make isa): the MG N<64, 616-row instance only
-    if (nx == 4 && nu == 1 && np == 1 && spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st);
-    return hipErrorInvalidValue;
-#else
-    if (nx == 4 && nu == 1 && np == 1) return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);
-    if (nx == 2 && nu == 2 && np == 2) return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st);
-    return hipErrorInvalidValue;
+    if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st);
+#ifndef BQP_ISA_ONLY_MG10
+    if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st);
 #endif
+    return hipErrorInvalidValue;
 }
+#endif
 
 }  // namespace bqp

@@ -55,10 +55,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const int m = (A && !mxIsEmpty(A)) ? (int)mxGetM(A) : 0;
     int me0 = (Aeq && !mxIsEmpty(Aeq)) ? (int)mxGetM(Aeq) : 0;
 
-    if (!g_handle) {
-        if (bqp_create(&g_handle, -1) != BQP_OK) mexErrMsgIdAndTxt("bqp:gpu", "no gfx950 device");
-        mexAtExit(cleanup);
-    }
+    if (!mxIsEmpty(H) && mxGetNumberOfElements(H) % ((size_t)n * n) != 0)
+        mexErrMsgIdAndTxt("bqp:dims", "H must be n x n (x batch) with n = rows of f = %d", n);
+    if (m && mxGetN(A) % (size_t)n != 0)
+        mexErrMsgIdAndTxt("bqp:dims", "A must have n = %d columns (x batch)", n);
+    const int64_t sH = stride_of(H, (size_t)n * n, batch), sA = stride_of(A, (size_t)m * n, batch),
+                  sb = stride_of(b, m, batch);
     /* fixed variables (lb == ub) -> equality rows (same pattern for every instance) */
     const double* lbp = (lb && !mxIsEmpty(lb)) ? mxGetDoubles(lb) : NULL;
     const double* ubp = (ub && !mxIsEmpty(ub)) ? mxGetDoubles(ub) : NULL;
@@ -104,12 +106,17 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
             U2[(size_t)i * n + fix[r]] = INFINITY;
         }
     }
+    /* arguments are validated above: only now take the device (first call) */
+    if (!g_handle) {
+        if (bqp_create(&g_handle, -1) != BQP_OK) mexErrMsgIdAndTxt("bqp:gpu", "no gfx950 device");
+        mexAtExit(cleanup);
+    }
     bqp_dims d = {n, m, me};
     bqp_strides st;
-    st.sH = stride_of(H, (size_t)n * n, batch);
+    st.sH = sH;
     st.sf = n;
-    st.sA = stride_of(A, (size_t)m * n, batch);
-    st.sb = stride_of(b, m, batch);
+    st.sA = sA;
+    st.sb = sb;
     st.sAeq = (int64_t)me * n;
     st.sbeq = me;
     st.slb = n;

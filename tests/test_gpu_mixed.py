@@ -1,0 +1,115 @@
+"""Mixed precision (bqp_options.precision = 2, config C5 "fp32 vs fp64 mixed precision"): an fp32
+launch runs each instance to the floored fp32 tolerances and hands its iterate (stage vectors,
+dynamics multipliers, row slacks and multipliers) to an fp64 launch that continues the same
+Mehrotra iteration to the fp64 tolerances.  The results are held to the fp64 bar: the north-star
+tolerance 1e-8 against the exact optimum z* of the fixtures, and the fp64 solve's exit flags."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+TOL_Z = 1e-8          # |z - z*|_inf / max(1, |z*|_inf), as the fp64 tests (test_gpu_ocp.py)
+
+
+@pytest.fixture(scope='module')
+def handle():
+    import bqp
+    return bqp.Handle(0)
+
+
+def _tracking(mg, ts, N):
+    import bqp
+    return bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                            mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                            ts[0], ts[1], mg['x_wp'], mg['u_wp'], N=N)
+
+
+def test_mixed_f2_n100(mg, term_set, handle):
+    """C5 problem (MG DMS tracking LMPC, N=100, 616-row terminal set): first move and theta
+    within 1e-8 of z*, every instance converged, fewer fp64 iterations than the fp64 solve."""
+    g = golden('dms_DSS_tLMPC.npz')
+    tl = _tracking(mg, term_set, 100)
+    X = g['x'][g['idx']]
+    r64 = tl.solve(X, handle=handle)
+    rmx = tl.solve(X, handle=handle, precision=2)
+    assert (rmx.exitflag == 1).all(), rmx.exitflag
+    err = np.abs(rmx.u0[:, 0] - g['u_star'])
+    print('mixed N=100: first-move error max %.2e median %.2e; iterations (fp32 + fp64) %.1f, '
+          'fp64 alone %.1f; |u_mixed - u_fp64| max %.2e'
+          % (err.max(), np.median(err), rmx.iterations.mean(), r64.iterations.mean(),
+             np.abs(rmx.u - r64.u).max()))
+    assert err.max() < TOL_Z * max(1.0, np.abs(g['u_star']).max())
+    # whole horizon: the late DMS states are weakly determined (running weight delta = 0.01), so
+    # two solves stopping at the same tolerances agree there to 2e-7, as fp64 does with z*
+    # (tests/test_gpu_ocp.py)
+    assert np.abs(rmx.u - r64.u).max() < 2e-7
+    assert np.abs(rmx.theta - r64.theta).max() < 2e-7
+    # the continued fp64 iterate meets the fp64 stopping rule (tolerances of include/bqp.h)
+    assert rmx.mu.max() <= 1e-14
+
+
+def test_mixed_f1_n20(mg, term_set, handle):
+    """C2 problem through the mixed mode: whole decision vector within 1e-8 of z*."""
+    import bqp
+    g = golden('lmpc_N20.npz')
+    lm = bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                  mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                  term_set[0], term_set[1], N=20)
+    r = lm.solve(g['dx'][g['idx']], handle=handle, precision=2)
+    assert (r.exitflag == 1).all()
+    zs = g['z_star']
+    err = np.abs(r.opt_var - zs).max() / max(1.0, np.abs(zs).max())
+    print('mixed N=20: |z - z*| %.2e, iterations %.1f' % (err, r.iterations.mean()))
+    assert err < TOL_Z, err
+
+
+def test_mixed_duals_kkt(mg, term_set, handle):
+    """multipliers of the continued solve on the reference's F2 rows (tests/dual_map.py): the
+    full dense KKT conditions, and lambda* of the oracle's exact active-set solve where it is
+    unique - the bars of the fp64 dual test (tests/test_gpu_duals.py)"""
+    import dual_map as dm
+    from oracle import dense_qp, qp_forms
+    g = golden('dms_DSS_tLMPC.npz')
+    N = int(g['N'])
+    tl = _tracking(mg, term_set, N)
+    X = g['x'][g['idx'][:8]]
+    r = tl.solve(X, handle=handle, precision=2, want_duals=True)
+    assert (r.exitflag == 1).all()
+    for i in range(len(X)):
+        qp = qp_forms.dms_dense(mg, N, X[i], *term_set)
+        lin, y = dm.f2_duals(N, r.lam_x[i], r.lam_u[i], r.lam_p[i], r.pi[i])
+        st, comp, lmin, viol = dm.f2_kkt(qp, r.y_OL[i], lin, y, 4)
+        assert st < 1e-8 and comp < 1e-9 and lmin > -1e-12 and viol < 1e-9, (i, st, comp, lmin, viol)
+        zs, fv, ls, info = dense_qp.solve(qp)
+        if dm.licq(qp['A'], lin, ls['ineqlin']):
+            sc = max(1.0, np.abs(ls['ineqlin']).max(), np.abs(ls['eqlin']).max())
+            assert np.abs(lin - ls['ineqlin']).max() / sc < 1e-7
+            assert np.abs(y - ls['eqlin'][:4 * N]).max() / sc < 1e-7
+
+
+def test_mixed_status_cold_restart(mg, term_set, handle):
+    """perturbed models (config C4 generator): instances the fp32 phase ends as infeasible or
+    failed restart in fp64 from the fp64 initial point, so the exit flags are the fp64 solve's
+    and the converged first moves agree"""
+    import bqp
+    d = golden('mg_design.npz')
+    rng = np.random.default_rng(4)
+    n = 512
+    E = rng.standard_normal((n, 4, 4))
+    e = rng.standard_normal((n, 4, 1))
+    A = d['A'] + 0.01 * E * np.abs(d['A'])
+    Bm = d['B'].reshape(4, 1) + 0.01 * e * np.abs(d['B'].reshape(4, 1))
+    dx = golden('lmpc_N20.npz')['dx'][:n]
+    lm = bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                  mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                  term_set[0], term_set[1], N=20)
+    r64 = lm.solve(dx, A=A, B=Bm, handle=handle)
+    rmx = lm.solve(dx, A=A, B=Bm, handle=handle, precision=2)
+    print('mixed C4 sample: flags fp64 %s, mixed %s' % (np.unique(r64.exitflag, return_counts=True),
+                                                       np.unique(rmx.exitflag, return_counts=True)))
+    assert (r64.exitflag == -2).any()
+    assert np.array_equal(r64.exitflag, rmx.exitflag)
+    ok = r64.exitflag == 1
+    assert np.abs(rmx.du0[ok] - r64.du0[ok]).max() < 1e-8

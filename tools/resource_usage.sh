@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-instantiation VGPRs / scratch bytes per lane of a HIP source: tools/resource_usage.sh [file.hip]
 F=${1:-learning-based-mpc_amd/csrc/bqp_ocp.hip}
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-result -Wno-unused-value -x hip -c "$F" -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | \
+/opt/rocm/bin/hipcc $EXTRA -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-result -Wno-unused-value -x hip -c "$F" -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | \
   python3 -c "
 import re,sys
 cur=None; v={}

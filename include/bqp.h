@@ -259,6 +259,39 @@ int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
                                const bqp_closed_loop* cl, const double* x_init, double* X,
                                double* U, int* exitflag, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * LBMPC closed loop with the learned model's data window:
+ * matlab/LBMPC/examples/DMS_LBMPC_casadi.m:163-218.  Per step: the structured solve at the
+ * measured state, the plant step, then the data acquisition of the reference -
+ *   X = [dx1; dx2; du], Y = (x+ - x_eq) - (A dx + B du)          (:202-206, deviation coords)
+ *   window <- get_data(X, Y, q, it, window)                     (utilities/get_data.m)
+ * and the logged learned prediction xl = x_eq + A dx + B du + g(X, Y, v) with the window before
+ * the update (:199, casadiL2NW.m).  In that script the learned states enter only equality rows
+ * that no cost term or inequality reads, so the per-step OCP is the QP the caller poses in
+ * `data` (its own form: F_x_d and the terminal set on x_1, polytope at stage 1); the window
+ * drives xl.  A, B of the window update are data->A / data->B.  Same loop and outputs as
+ * bqp_closed_loop_ocp, plus: */
+typedef struct {
+    int q;               /* points in the data window (get_data.m's q) */
+    int mask;            /* 1: 8 x q window with validity row v, only the first (zero) point valid
+                            at the start (DMS_LBMPC_casadi.m:160-161); 0: every point counts (the
+                            7-row window of hybrid_LBMPC_casadi.m:160) */
+    double bandwidth, lambda;  /* NW kernel; <= 0 selects the reference's 0.5, 1e-3 */
+    double* XL;          /* out: batch*(steps+1)*nx learned predictions xl (XL[:,0] = x_init) */
+    double* window;      /* out, may be NULL: batch*q*8 final windows, [X; Y; v] per point, ring
+                            order (iteration it's sample in point it mod q) */
+} bqp_learning;
+
+int bqp_closed_loop_lbmpc(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* data,
+                          const bqp_options* opt, const bqp_closed_loop* cl,
+                          const bqp_learning* lw, const double* x_init, double* X, double* U,
+                          int* exitflag);
+int bqp_closed_loop_lbmpc_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
+                                 const bqp_ocp_data* data, const bqp_options* opt,
+                                 const bqp_closed_loop* cl, const bqp_learning* lw,
+                                 const double* x_init, double* X, double* U, int* exitflag,
+                                 void* stream);
+
 /* Timing of the most recent solve on this handle: kernel time measured with hipEvents on the
  * launch stream (ms), and the number of kernel launches it covered. */
 int bqp_last_kernel_ms(bqp_handle h, double* ms, int* launches);

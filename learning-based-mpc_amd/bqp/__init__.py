@@ -6,7 +6,7 @@ this package only marshals arrays across the C ABI.
 """
 from ._lib import BqpError, Handle, load, options  # noqa: F401
 from .ocp import OcpProblem, solve_ocp  # noqa: F401
-from .mpc import LMPC, TrackingLMPC, TrackingMPC  # noqa: F401
+from .mpc import LMPC, TrackingLBMPC, TrackingLMPC, TrackingMPC  # noqa: F401
 from .quadprog import quadprog  # noqa: F401
 from .lbmpc import LBMPC, HybridLBMPC, nw_oracle  # noqa: F401
 from .loop import closed_loop  # noqa: F401

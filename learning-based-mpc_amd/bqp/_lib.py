@@ -66,7 +66,8 @@ EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version',
            'bqp_solve_ocp_batched', 'bqp_solve_ocp_batched_device', 'bqp_quadprog_batched',
            'bqp_quadprog_batched_device', 'bqp_last_kernel_ms', 'bqp_nw_oracle',
            'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device',
-           'bqp_closed_loop_ocp', 'bqp_closed_loop_ocp_device']
+           'bqp_closed_loop_ocp', 'bqp_closed_loop_ocp_device', 'bqp_closed_loop_lbmpc',
+           'bqp_closed_loop_lbmpc_device']
 
 _lib = None
 
@@ -116,6 +117,13 @@ def load():
     lib.bqp_closed_loop_ocp_device.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int,
                                                C.POINTER(OcpData), C.POINTER(Options), C.c_void_p,
                                                _PD, _PD, _PD, _PI, C.c_void_p]
+    lib.bqp_closed_loop_lbmpc.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int,
+                                          C.POINTER(OcpData), C.POINTER(Options), C.c_void_p,
+                                          C.c_void_p, _PD, _PD, _PD, _PI]
+    lib.bqp_closed_loop_lbmpc_device.argtypes = [C.c_void_p, C.POINTER(OcpDims), C.c_int,
+                                                 C.POINTER(OcpData), C.POINTER(Options),
+                                                 C.c_void_p, C.c_void_p, _PD, _PD, _PD, _PI,
+                                                 C.c_void_p]
     _lib = lib
     return lib
 

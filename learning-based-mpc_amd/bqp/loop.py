@@ -21,10 +21,21 @@ class ClosedLoop(C.Structure):
                 ('x_eq', _lib._PD), ('u_eq', _lib._PD)]
 
 
-def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, **opts):
-    """mpc: a TrackingLMPC (deviation coordinates around mpc.x_eq, mpc.u_eq); x_init (batch, n)
-    absolute initial states.  Returns X (batch, steps+1, n), U (batch, steps, m) absolute, and
-    the per-step exit flags (batch, steps)."""
+class Learning(C.Structure):
+    _fields_ = [('q', C.c_int), ('mask', C.c_int), ('bandwidth', C.c_double),
+                ('lambda_', C.c_double), ('XL', _lib._PD), ('window', _lib._PD)]
+
+
+def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, **opts):
+    """mpc: a TrackingLMPC / TrackingLBMPC (deviation coordinates around mpc.x_eq, mpc.u_eq);
+    x_init (batch, n) absolute initial states.  Returns X (batch, steps+1, n), U (batch, steps,
+    m) absolute, and the per-step exit flags (batch, steps).
+
+    learning=dict(q=100, mask=1[, bandwidth, lambda_]) also keeps the learned model's data window
+    per instance (bqp_closed_loop_lbmpc: LBMPC_casadi.m:193-198 / DMS_LBMPC_casadi.m:198-207)
+    and returns XL (batch, steps+1, n), the learned one-step predictions, and window
+    (batch, q, 8), the final windows [X; Y; v] per point in ring order (iteration it's sample
+    in point it mod q)."""
     lib = _lib.load()
     h = handle or _default_handle()
     x_init = np.ascontiguousarray(np.atleast_2d(x_init), dtype=np.float64)
@@ -37,7 +48,19 @@ def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, **opts):
     X = np.zeros((b, steps + 1, prob.nx)); U = np.zeros((b, steps, prob.nu))
     flags = np.zeros((b, steps), np.int32)
     o = _lib.options(**opts)
-    rc = lib.bqp_closed_loop_ocp(h.value, C.byref(dims), b, C.byref(data), C.byref(o), C.byref(cl),
-                                 _lib.ptr(x_init), _lib.ptr(X), _lib.ptr(U), _lib.iptr(flags))
-    _lib.check(rc, 'bqp_closed_loop_ocp')
-    return OcpResult(X=X, U=U, exitflag=flags)
+    if learning is None:
+        rc = lib.bqp_closed_loop_ocp(h.value, C.byref(dims), b, C.byref(data), C.byref(o),
+                                     C.byref(cl), _lib.ptr(x_init), _lib.ptr(X), _lib.ptr(U),
+                                     _lib.iptr(flags))
+        _lib.check(rc, 'bqp_closed_loop_ocp')
+        return OcpResult(X=X, U=U, exitflag=flags)
+    q = int(learning.get('q', 100))
+    XL = np.zeros_like(X)
+    win = np.zeros((b, q, 8))
+    lw = Learning(q, int(learning.get('mask', 1)), float(learning.get('bandwidth', 0.0)),
+                  float(learning.get('lambda_', 0.0)), _lib.ptr(XL), _lib.ptr(win))
+    rc = lib.bqp_closed_loop_lbmpc(h.value, C.byref(dims), b, C.byref(data), C.byref(o),
+                                   C.byref(cl), C.byref(lw), _lib.ptr(x_init), _lib.ptr(X),
+                                   _lib.ptr(U), _lib.iptr(flags))
+    _lib.check(rc, 'bqp_closed_loop_lbmpc')
+    return OcpResult(X=X, U=U, exitflag=flags, XL=XL, window=win)

@@ -146,6 +146,30 @@ class TrackingLMPC:
         return r
 
 
+class TrackingLBMPC(TrackingLMPC):
+    """CasADi LBMPC (examples/LBMPC_casadi.m:240-304; the nominal part of DMS_LBMPC_casadi.m):
+    the DMS tracking cost of TrackingLMPC (delta-weighted running cost, terminal P and T) with
+    the LBMPC constraint sets of getCONSPOLY.m - boxes F_x on x_1..x_N and F_u on every input,
+    and at k = 1 the tightened state set F_x_d x_1 <= h_x_d and the robust terminal set
+    F_w_N [x_1; theta] <= h_w_N (:285-289) - on the nominal model (the learned dynamics are
+    commented out of the constraints there, :292).  The polytope block is [F_x_d; F_w_N] at
+    stage 1.  closed_loop(..., learning=dict(q=100)) adds the script's data window
+    (update_data.m)."""
+
+    def __init__(self, A, B, Q, R, P, T, LAMBDA, PSI, F_x, h_x, F_u, h_u, F_w_N, h_w_N, F_x_d,
+                 h_x_d, x_eq, u_eq, N, delta=0.01):
+        super().__init__(A, B, Q, R, P, T, LAMBDA, PSI, F_x, h_x, F_u, h_u, F_w_N, h_w_N, x_eq,
+                         u_eq, N, delta)
+        pr = self.prob
+        n, m, p = self.n, self.m, self.p
+        Fd = np.zeros((np.shape(F_x_d)[0], n + m + p))
+        Fd[:, :n] = np.asarray(F_x_d, float)
+        Fp = np.vstack([Fd, _poly(F_w_N, n, m, p)])
+        hp = np.concatenate([np.asarray(h_x_d, float).ravel(), np.asarray(h_w_N, float).ravel()])
+        self.prob = OcpProblem(pr.A, pr.B, pr.W, N, p, xlb=pr.xlb, xub=pr.xub, ulb=pr.ulb,
+                               uub=pr.uub, Fp=Fp, hp=hp, poly_stage=1)
+
+
 class TrackingMPC:
     """trackingMPC/RunExample.m (double integrator): costFunction.m + constraintsFunction.m.
     The constant rows on x_0 (constraintsFunction.m:291, k=1) do not involve the decision and

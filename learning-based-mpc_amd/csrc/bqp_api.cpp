@@ -282,6 +282,12 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         // phase 2: fp64 from the handed-over iterates
         a.hand_in = hb; a.hand_flag = hflag; a.hand_it = hit; a.hand_stride = (int64_t)hrec;
         HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
+        // phase 3: a continuation that did not converge (-8 / -2 / 0: marginal instances, e.g.
+        // nearly infeasible perturbed models) is solved again from the fp64 initial point, so
+        // the mixed mode reports the fp64 solve's status there; the others leave at once
+        bqp::OcpKernelArgs a3 = a;
+        a3.hand_in = nullptr; a3.hand_it = nullptr; a3.redo_flag = hflag;
+        HIP_TRY(bqp::launch_ocp(a3, nx, nu, np, st));
     } else if (f32) {
         HIP_TRY(bqp::launch_ocp_f32(a, nx, nu, np, st));
     } else {
@@ -289,7 +295,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     }
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->timed = true;
-    h->launches = mixed ? 2 : 1;
+    h->launches = mixed ? 3 : 1;
     if (out) HIP_TRY(bqp::launch_ocp_finalize(Sd, batch, out, st));
     return BQP_OK;
 }
@@ -688,28 +694,35 @@ int bqp_lbmpc_solve_batched(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
 // ------------------------------------------------------------------------------------------
 // closed-loop simulation: batched structured solve + true-plant step, per time step
 // ------------------------------------------------------------------------------------------
-int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
-                               const bqp_ocp_data* D, const bqp_options* opt,
-                               const bqp_closed_loop* cl, const double* x_init, double* X,
-                               double* U, int* exitflag, void* stream) {
+static int closed_loop_impl(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
+                            const bqp_options* opt, const bqp_closed_loop* cl,
+                            const bqp_learning* lw, const double* x_init, double* X, double* U,
+                            int* exitflag, void* stream) {
     if (!h || !cl || !x_init || !X || !U) return BQP_E_ARG;
     int rc = ocp_check(d, batch, D);
     if (rc) return rc;
     if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
         return BQP_E_ARG;
     if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;   // the MG plant
+    if (lw && (lw->q < 1 || lw->q > (1 << 20) || !lw->XL)) return BQP_E_ARG;
     DevScope ds(h->device);
     hipStream_t st = (hipStream_t)stream;
     const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
     const size_t B = batch;
-    const size_t nd = B * nx + B * (N + 1) * nx + B * N * nu + B * np;
+    const size_t nwin = lw ? B * (size_t)lw->q * 8 : 0;
+    const size_t nd = B * nx + B * (N + 1) * nx + B * N * nu + B * np + nwin;
     HIP_TRY(h->cwork.reserve(sizeof(double) * nd + sizeof(int) * B));
     double* s = (double*)h->cwork.p;
     double* xo = s + B * nx;
     double* uo = xo + B * (N + 1) * nx;
     double* th = uo + B * N * nu;
-    int* fl = (int*)(th + B * np);
+    double* win = th + B * np;
+    int* fl = (int*)(win + nwin);
+    if (lw && lw->window) win = lw->window;   // the caller's buffer (device) keeps the final window
     HIP_TRY(bqp::launch_closed_loop_init(batch, nx, cl->steps, x_init, cl->x_eq, s, X, st));
+    const double bw = (lw && lw->bandwidth > 0) ? lw->bandwidth : 0.5;
+    const double lam = (lw && lw->lambda > 0) ? lw->lambda : 1e-3;
+    if (lw) HIP_TRY(bqp::launch_lbmpc_window_init(batch, cl->steps, lw->q, lw->mask, x_init, win, lw->XL, st));
     bqp_ocp_data Dm = *D;
     Dm.x0 = s;
     Dm.sx0 = nx;
@@ -722,6 +735,9 @@ int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         if (rc) { hipEventDestroy(e0); return rc; }
         HIP_TRY(bqp::launch_mg_plant(batch, N, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
                                      s, X, U, exitflag, st));
+        if (lw)
+            HIP_TRY(bqp::launch_lbmpc_window(batch, cl->steps, t, lw->q, bw, lam, D->A, D->sA, D->B,
+                                             D->sB, cl->x_eq, cl->u_eq, X, U, win, lw->XL, st));
     }
     // timing of the whole loop (solves + plant steps) on this stream
     HIP_TRY(hipEventRecord(h->ev1, st));
@@ -729,14 +745,32 @@ int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     std::swap(h->ev0, e0);
     hipEventDestroy(e0);
     h->timed = true;
-    h->launches = 3 * cl->steps;
+    h->launches = (lw ? 4 : 3) * cl->steps;
     return BQP_OK;
 }
 
-int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
-                        const bqp_options* opt, const bqp_closed_loop* cl, const double* x_init,
-                        double* X, double* U, int* exitflag) {
+int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
+                               const bqp_ocp_data* D, const bqp_options* opt,
+                               const bqp_closed_loop* cl, const double* x_init, double* X,
+                               double* U, int* exitflag, void* stream) {
+    return closed_loop_impl(h, d, batch, D, opt, cl, nullptr, x_init, X, U, exitflag, stream);
+}
+
+int bqp_closed_loop_lbmpc_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
+                                 const bqp_ocp_data* D, const bqp_options* opt,
+                                 const bqp_closed_loop* cl, const bqp_learning* lw,
+                                 const double* x_init, double* X, double* U, int* exitflag,
+                                 void* stream) {
+    if (!lw) return BQP_E_ARG;
+    return closed_loop_impl(h, d, batch, D, opt, cl, lw, x_init, X, U, exitflag, stream);
+}
+
+static int closed_loop_host(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
+                            const bqp_options* opt, const bqp_closed_loop* cl,
+                            const bqp_learning* lw, const double* x_init, double* X, double* U,
+                            int* exitflag) {
     if (!h || !cl || !x_init || !X || !U) return BQP_E_ARG;
+    if (lw && (lw->q < 1 || lw->q > (1 << 20) || !lw->XL)) return BQP_E_ARG;
     int rc = ocp_check(d, batch, D);
     if (rc) return rc;
     // validate the loop description before sizing the staging buffers from it
@@ -765,7 +799,8 @@ int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bq
     };
     const int nin = sizeof(in) / sizeof(in[0]);
     const size_t nX = (size_t)batch * (cl->steps + 1) * nx, nU = (size_t)batch * cl->steps * nu;
-    size_t tot = nX + nU;
+    const size_t nW = lw ? (size_t)batch * lw->q * 8 : 0;
+    size_t tot = nX + nU + (lw ? nX + nW : 0);
     for (int i = 0; i < nin; ++i) tot += (in[i].src ? in[i].n : 0);
     HIP_TRY(h->stage.reserve(sizeof(double) * tot + sizeof(int) * (size_t)batch * cl->steps));
     double* cur = (double*)h->stage.p;
@@ -777,6 +812,9 @@ int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bq
     }
     double* Xd = cur; cur += nX;
     double* Ud = cur; cur += nU;
+    double* XLd = nullptr;
+    double* Wd = nullptr;
+    if (lw) { XLd = cur; cur += nX; Wd = cur; cur += nW; }
     int* Fd = (int*)cur;
     bqp_ocp_data Dd = *D;
     Dd.A = in[0].dst; Dd.B = in[1].dst; Dd.c = in[2].dst; Dd.W = in[3].dst; Dd.w = in[4].dst;
@@ -785,14 +823,34 @@ int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bq
     Dd.x0 = in[11].dst;   // placeholder (the loop feeds the measured states)
     bqp_closed_loop cd = *cl;
     cd.x_eq = in[12].dst; cd.u_eq = in[13].dst;
-    rc = bqp_closed_loop_ocp_device(h, d, batch, &Dd, opt, &cd, in[11].dst, Xd, Ud,
-                                    exitflag ? Fd : nullptr, h->stream);
+    bqp_learning ld;
+    if (lw) { ld = *lw; ld.XL = XLd; ld.window = Wd; }
+    rc = closed_loop_impl(h, d, batch, &Dd, opt, &cd, lw ? &ld : nullptr, in[11].dst, Xd, Ud,
+                          exitflag ? Fd : nullptr, h->stream);
     if (rc) return rc;
+    if (lw) {
+        HIP_TRY(hipMemcpyAsync(lw->XL, XLd, sizeof(double) * nX, hipMemcpyDeviceToHost, h->stream));
+        if (lw->window) HIP_TRY(hipMemcpyAsync(lw->window, Wd, sizeof(double) * nW, hipMemcpyDeviceToHost, h->stream));
+    }
     HIP_TRY(hipMemcpyAsync(X, Xd, sizeof(double) * nX, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipMemcpyAsync(U, Ud, sizeof(double) * nU, hipMemcpyDeviceToHost, h->stream));
     if (exitflag) HIP_TRY(hipMemcpyAsync(exitflag, Fd, sizeof(int) * (size_t)batch * cl->steps, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return BQP_OK;
+}
+
+int bqp_closed_loop_ocp(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
+                        const bqp_options* opt, const bqp_closed_loop* cl, const double* x_init,
+                        double* X, double* U, int* exitflag) {
+    return closed_loop_host(h, d, batch, D, opt, cl, nullptr, x_init, X, U, exitflag);
+}
+
+int bqp_closed_loop_lbmpc(bqp_handle h, const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D,
+                          const bqp_options* opt, const bqp_closed_loop* cl,
+                          const bqp_learning* lw, const double* x_init, double* X, double* U,
+                          int* exitflag) {
+    if (!lw) return BQP_E_ARG;
+    return closed_loop_host(h, d, batch, D, opt, cl, lw, x_init, X, U, exitflag);
 }
 
 #ifdef BQP_STAMPS

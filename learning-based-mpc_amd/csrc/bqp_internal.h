@@ -36,6 +36,10 @@ struct OcpKernelArgs {
     const int* hand_flag;
     int* hand_it;           // fp32-phase iterations (written by the fp32 launch, added by the fp64 one)
     int64_t hand_stride;    // floats per instance (ocp_hand_floats)
+    // third launch of the mixed mode (cold fp64): only the instances whose warm continuation
+    // did not converge (exitflag != 1 with a warm hand_flag) are solved again from the fp64
+    // initial point; every other instance leaves at once
+    const int* redo_flag;
 };
 
 bool ocp_supported(int nx, int nu, int np);
@@ -101,5 +105,11 @@ hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* x
 hipError_t launch_mg_plant(int batch, int N, int steps, int t, double delta, const double* uo,
                            const int* fl, const double* xeq, const double* ueq, double* s,
                            double* X, double* U, int* flags, hipStream_t st);
+hipError_t launch_lbmpc_window_init(int batch, int steps, int q, int mask, const double* xinit,
+                                    double* win, double* XL, hipStream_t st);
+hipError_t launch_lbmpc_window(int batch, int steps, int t, int q, double bw, double lam,
+                               const double* A, int64_t sA, const double* B, int64_t sB,
+                               const double* xeq, const double* ueq, const double* X,
+                               const double* U, double* win, double* XL, hipStream_t st);
 
 }  // namespace bqp

@@ -1734,6 +1734,8 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     const int slot = rowwave ? wid - qpb : wid;
     const int inst = blockIdx.x * qpb + slot;
     if (inst >= a.batch) return;       // both waves of an empty slot leave together
+    if (a.redo_flag && !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
+        return;                        // mixed mode, cold retry launch: nothing to redo here
     const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad);
     real* W = lds + a.shared_doubles + slot * L.total;
     if (!rowwave)

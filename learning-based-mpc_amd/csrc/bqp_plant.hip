@@ -67,6 +67,101 @@ __global__ void mg_plant_kernel(int batch, int N, int steps, int t, double delta
     if (flags) flags[(int64_t)b * steps + t] = fl[b];
 }
 
+// ------------------------------------------------------------------------------------------
+// LBMPC data window (DMS_LBMPC_casadi.m:198-207, utilities/get_data.m, functions/casadiL2NW.m):
+// after the plant step t (iteration it = t + 1 of the reference loop) one wave per instance
+//   - forms the learned one-step prediction of the step, with the window BEFORE its update,
+//       xl = x_eq + A dx + B du + g(xi),  g = sum_i Y_i k_i / (lambda + sum_j k_j v_j),
+//       k_i = exp(-|X_i - xi|^2 / h^2),  xi = [dx1; dx2; du]   (casadiL2NW.m:14-28)
+//   - appends the sample X = [dx1; dx2; du], Y = (x+ - x_eq) - (A dx + B du) with v = 1.
+// The window is a ring of q points, 8 doubles each ([X; Y; v], the 8 x q layout of the reference
+// with its columns in ring order): iteration it writes point it mod q, which is exactly the
+// column get_data.m fills (it < q) or the oldest one it drops (it >= q).  The NW sum does not
+// depend on the column order.  lanes run over the points; the sums are wave reductions.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ void lbmpc_window_kernel(int batch, int steps, int t, int q, double hinv2, double lam,
+                                    const double* A, int64_t sA, const double* B, int64_t sB,
+                                    const double* xeq, const double* ueq, const double* X,
+                                    const double* U, double* win, double* XL) {
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b >= batch) return;
+    const double* xt = X + ((int64_t)b * (steps + 1) + t) * 4;
+    double dx[4], x1[4], nom[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { dx[i] = xt[i] - xeq[i]; x1[i] = xt[4 + i]; }
+    const double du = U[(int64_t)b * steps + t] - ueq[0];
+    const double* Ab = A + (int64_t)b * sA;
+    const double* Bb = B + (int64_t)b * sB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double v = Bb[i] * du;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v += Ab[j * 4 + i] * dx[j];   // column-major A
+        nom[i] = v;
+    }
+    const double xi0 = dx[0], xi1 = dx[1], xi2 = du;
+    double* w = win + (int64_t)b * q * 8;
+    double sy0 = 0, sy1 = 0, sy2 = 0, sy3 = 0, sk = 0;
+    for (int i = lane; i < q; i += 64) {
+        const double* pt = w + (int64_t)i * 8;
+        const double e0 = pt[0] - xi0, e1 = pt[1] - xi1, e2 = pt[2] - xi2;
+        const double k = exp(-(e0 * e0 + e1 * e1 + e2 * e2) * hinv2);
+        sy0 += pt[3] * k; sy1 += pt[4] * k; sy2 += pt[5] * k; sy3 += pt[6] * k;
+        sk += k * pt[7];
+    }
+    sy0 = wave_sum64(sy0); sy1 = wave_sum64(sy1); sy2 = wave_sum64(sy2); sy3 = wave_sum64(sy3);
+    sk = wave_sum64(sk);
+    if (lane == 0) {
+        const double den = lam + sk;
+        const double g[4] = {sy0 / den, sy1 / den, sy2 / den, sy3 / den};
+        double* xl = XL + ((int64_t)b * (steps + 1) + t + 1) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xl[i] = xeq[i] + nom[i] + g[i];
+        // get_data.m: the sample of iteration t + 1 into ring slot (t + 1) mod q
+        double* pt = w + (int64_t)((t + 1) % q) * 8;
+        pt[0] = xi0; pt[1] = xi1; pt[2] = xi2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pt[3 + i] = (x1[i] - xeq[i]) - nom[i];
+        pt[7] = 1.0;
+    }
+}
+
+// initial window: zeros; validity 1 on the first point only (DMS_LBMPC_casadi.m:160-161) or on
+// every point (mask = 0: the 7-row window of hybrid_LBMPC_casadi.m:160, no validity row);
+// XL[:, 0] = x_init
+__global__ void lbmpc_window_init_kernel(int batch, int steps, int q, int mask,
+                                         const double* xinit, double* win, double* XL) {
+    const int b = blockIdx.x;
+    if (b >= batch) return;
+    double* w = win + (int64_t)b * q * 8;
+    for (int i = threadIdx.x; i < q * 8; i += blockDim.x)
+        w[i] = ((i & 7) == 7 && (!mask || i == 7)) ? 1.0 : 0.0;
+    if (threadIdx.x < 4) XL[(int64_t)b * (steps + 1) * 4 + threadIdx.x] = xinit[(int64_t)b * 4 + threadIdx.x];
+}
+
+hipError_t launch_lbmpc_window_init(int batch, int steps, int q, int mask, const double* xinit,
+                                    double* win, double* XL, hipStream_t st) {
+    hipLaunchKernelGGL(lbmpc_window_init_kernel, dim3(batch), dim3(256), 0, st, batch, steps, q,
+                       mask, xinit, win, XL);
+    return hipGetLastError();
+}
+
+hipError_t launch_lbmpc_window(int batch, int steps, int t, int q, double bw, double lam,
+                               const double* A, int64_t sA, const double* B, int64_t sB,
+                               const double* xeq, const double* ueq, const double* X,
+                               const double* U, double* win, double* XL, hipStream_t st) {
+    hipLaunchKernelGGL(lbmpc_window_kernel, dim3((batch + 3) / 4), dim3(256), 0, st, batch, steps,
+                       t, q, 1.0 / (bw * bw), lam, A, sA, B, sB, xeq, ueq, X, U, win, XL);
+    return hipGetLastError();
+}
+
 hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* xinit,
                                    const double* xeq, double* s, double* X, hipStream_t st) {
     hipLaunchKernelGGL(closed_loop_init_kernel, dim3((batch + 255) / 256), dim3(256), 0, st, batch,

@@ -231,3 +231,48 @@ def f4_to_y(p, x0, z, x_eq, u_eq):
     """y_OL layout of hybrid_LBMPC_casadi.m (absolute [x_0..x_N; u; theta])."""
     x, u = rollout(p, x0, z, learned=False)
     return np.concatenate([(x + x_eq).ravel(), (u + u_eq).ravel(), _theta(p, z)])
+
+
+# ----------------------------------------------------------------------------------------
+# closed-loop data window (LBMPC_casadi.m:193-198 with utilities/update_data.m;
+# DMS_LBMPC_casadi.m:198-207 with utilities/get_data.m and functions/casadiL2NW.m)
+# ----------------------------------------------------------------------------------------
+def nw_masked(xi, data, h=0.5, lam=1e-3):
+    """casadiL2NW.m:14-28: g = sum_i Y_i k_i / (lambda + sum_j k_j v_j) over an 8 x q window
+    [X; Y; v], k_i = exp(-|X_i - xi|^2 / h^2)."""
+    d = data[:3] - np.asarray(xi, float)[:, None]
+    k = np.exp(-np.sum(d * d, axis=0) / h ** 2)
+    return data[3:7] @ k / (lam + k @ data[7])
+
+
+def window_replay(X, U, A, B, x_eq, u_eq, q, mask=True, h=0.5, lam=1e-3):
+    """Replays the data acquisition of the reference's LBMPC loop on a closed-loop record
+    (X (T+1, 4) and U (T,) absolute): per iteration it = 1..T the learned prediction
+    xl = x_eq + A dx + B du + g(xi) with the window before the update (DMS_LBMPC_casadi.m:199),
+    then X = [dx1; dx2; du], Y = (x+ - x_eq) - (A dx + B du) appended by get_data.m (a column
+    per iteration, the oldest dropped once the q columns are full).  The window starts as zeros
+    with only the first point valid (mask, :160-161), or with every point valid (7-row window
+    without validity row).  Returns XL (T+1, 4) with XL[0] = X[0], and the final 8 x q window in
+    the reference's column order."""
+    X = np.asarray(X, float); U = np.asarray(U, float).ravel()
+    A = np.asarray(A, float); B = np.asarray(B, float).reshape(4)
+    x_eq = np.asarray(x_eq, float); u_eq = float(np.ravel(u_eq)[0])
+    data = np.zeros((8, q))
+    if mask:
+        data[7, 0] = 1.0
+    else:
+        data[7, :] = 1.0
+    XL = [X[0].copy()]
+    for it in range(1, len(U) + 1):
+        t = it - 1
+        dx = X[t] - x_eq
+        du = U[t] - u_eq
+        nom = A @ dx + B * du
+        xi = np.array([dx[0], dx[1], du])
+        XL.append(x_eq + nom + nw_masked(xi, data, h, lam))
+        col = np.concatenate([xi, (X[t + 1] - x_eq) - nom, [1.0]])
+        if it < q:                                          # get_data.m:3-6
+            data[:, it] = col
+        else:                                               # get_data.m:7-9
+            data = np.hstack([data[:, 1:], col[:, None]])
+    return np.array(XL), data

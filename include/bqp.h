@@ -56,8 +56,9 @@ typedef struct {
                           (inputs and outputs stay fp64; tolerances floored at 1e-5 / 1e-6 / 1e-9);
                           2 = mixed: an fp32 launch to those floored tolerances, then an fp64 launch
                           that continues every instance from its fp32 iterate to the fp64
-                          tolerances (fp64 results; instances the fp32 phase ends with -2/-8
-                          restart in fp64) */
+                          tolerances (fp64 results; instances the fp32 phase ends with -2/-8,
+                          or whose continuation does not converge, restart in fp64); applies to
+                          long horizons (N >= 64), shorter ones are solved in fp64 */
     int want_duals;    /* reserved (set 0): the structured API writes the multiplier outputs
                           whenever its `duals` argument is non-NULL */
 } bqp_options;

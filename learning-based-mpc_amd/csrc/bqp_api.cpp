@@ -175,7 +175,8 @@ static int ocp_check(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D) {
     if (d->n_poly > 0 && (!D->Fp || !D->hp)) return BQP_E_ARG;
     if (!bqp::ocp_supported(d->nx, d->nu, d->np)) return BQP_E_UNSUPPORTED;
     if (d->N > 127 || bqp::ocp_rpl_for(std::max(d->n_poly, 1)) < 0) return BQP_E_UNSUPPORTED;
-    if (D->sW != 0 || D->sFp != 0) return BQP_E_UNSUPPORTED;  // shared stage costs / polytope
+    if (D->sW != 0) return BQP_E_UNSUPPORTED;                // shared stage costs
+    if (D->sFp != 0 && D->sFp < (int64_t)d->n_poly * (d->nx + d->nu + d->np)) return BQP_E_ARG;
     return BQP_OK;
 }
 
@@ -193,7 +194,9 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     resolve(opt, &o);
     if (o.precision < 0 || o.precision > 2) return BQP_E_ARG;
     const bool f32 = o.precision == 1;     // fp32 instantiation (bqp_ocp_f32.hip)
-    const bool mixed = o.precision == 2;   // fp32 phase, then fp64 from the fp32 iterate
+    // fp32 phase, then fp64 from the fp32 iterate; long horizons only (N + 1 > 64, the
+    // instantiations that carry the handoff): shorter ones are solved in fp64 alone
+    const bool mixed = o.precision == 2 && d->N + 1 > 64;
     bqp_options o32 = o;
     // fp32 arithmetic cannot resolve the fp64 defaults: floor the stopping tolerances
     o32.tol_stat = std::max(o.tol_stat, 1e-5);
@@ -214,11 +217,13 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     const int mp = d->n_poly;
     const int hstride = nv * nv + 1;
     const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));   // = the kernel's RPL * 64
-    const int shared_doubles = (((N + 1) * hstride + nv * mpad) + 1) & ~1;   // elements
+    // per-instance polytope (sFp != 0): each instance's LDS slot holds its own NV x mpad table
+    const bool fpi = mp > 0 && D->sFp != 0;
+    const int shared_doubles = (((N + 1) * hstride + (fpi ? 0 : nv * mpad)) + 1) & ~1;   // elements
     // instances per workgroup (two waves each) that fit the 160 KB of LDS
     auto fit_wpb = [&](bool single, int& wpb) -> bool {
-        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad)
-                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad);
+        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi)
+                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi);
         const size_t lds_budget = 160 * 1024 / (single ? sizeof(float) : sizeof(double));
         // long horizons (N + 1 > 64, two stages per lane) are compiled for <= 256 threads per
         // workgroup: one wave per SIMD, whose 512 registers hold the doubled stage state
@@ -252,6 +257,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     a.ulb = D->ulb; a.uub = D->uub; a.hp = mp > 0 ? D->hp : Hd; a.x0 = D->x0;
     a.sA = D->sA; a.sB = D->sB; a.sc = D->sc; a.sw = D->sw; a.sxb = D->sxb; a.sub = D->sub;
     a.shp = D->shp; a.sx0 = D->sx0;
+    if (fpi) { a.Fp_inst = D->Fp; a.sFp = D->sFp; }
     a.x = x; a.u = u; a.theta = theta; a.fval = fval; a.exitflag = exitflag; a.stats = Sd;
     if (duals) {
         a.pi_out = duals->pi; a.lamx_out = duals->lam_x; a.lamu_out = duals->lam_u;
@@ -791,7 +797,7 @@ static int closed_loop_host(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
         {D->xub, D->xub ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},
         {D->ulb, D->ulb ? span(batch, D->sub, (size_t)N * nu) : 0, nullptr},
         {D->uub, D->uub ? span(batch, D->sub, (size_t)N * nu) : 0, nullptr},
-        {D->Fp, mp > 0 ? (size_t)mp * nv : 0, nullptr},
+        {D->Fp, mp > 0 ? span(batch, D->sFp, (size_t)mp * nv) : 0, nullptr},
         {D->hp, mp > 0 ? span(batch, D->shp, mp) : 0, nullptr},
         {x_init, (size_t)batch * nx, nullptr},
         {cl->x_eq, (size_t)nx, nullptr},

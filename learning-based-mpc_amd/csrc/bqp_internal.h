@@ -40,16 +40,20 @@ struct OcpKernelArgs {
     // did not converge (exitflag != 1 with a warm hand_flag) are solved again from the fp64
     // initial point; every other instance leaves at once
     const int* redo_flag;
+    // per-instance polytope (bqp_ocp_data.sFp != 0): the caller's column-major n_poly x nv
+    // blocks, stride sFp; the shared Fp table is then unused
+    const double* Fp_inst;
+    int64_t sFp;
 };
 
 bool ocp_supported(int nx, int nu, int np);
 int ocp_rpl_for(int mp);
 int ocp_bpl_for(int N, int nx, int nu);
 int ocp_hand_floats(int N, int nx, int nu, int np, int mp);
-int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad);
+int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad, bool fpi);
 hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 // fp32 instantiation (bqp_ocp_f32.hip): LDS element count per instance (floats) and launch
-int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad);
+int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad, bool fpi);
 hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,

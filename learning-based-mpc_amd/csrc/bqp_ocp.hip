@@ -138,8 +138,9 @@ enum : int {
 // Per-instance LDS layout (in doubles), sized from N at run time.
 struct QpLds {
     int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, bw, qu, fv, dsv, duv, dsc, duc, Dx, FD,
-        blam, ebox, bnd, gpp, gpe, prp, hp, xch, total;
-    __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad) {
+        blam, ebox, bnd, gpp, gpe, prp, hp, xch, Fi, total;
+    // fpi: the instance carries its own polytope matrix (bqp_ocp_data.sFp != 0), NV x mpad
+    __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false) {
         const int NS = NX + NP, NV = NS + NU, NB = NX + NU;
         QpLds o;
         int c = 0;
@@ -173,6 +174,7 @@ struct QpLds {
         o.prp = c;    c += mpad;                     // predictor dt*dlam of the polytope rows
         o.hp = c;     c += mpad;                     // polytope right-hand side
         o.xch = c;    c += X_NXCH;
+        o.Fi = c;     c += fpi ? NV * mpad : 0;      // per-instance polytope (column-major)
         o.total = (c + 1) & ~1;
         return o;
     }
@@ -195,8 +197,13 @@ __host__ __device__ constexpr int hand_rows_off(int N, int NS, int NU) {
 #define BQP_HAND_IN 1
 #define BQP_HAND_OUT 0
 #endif
+// Only the long-horizon instantiations (two stages per lane, N + 1 > 64) carry the handoff
+// code: the mixed mode pays there (the fp32 launch fits twice the instances per CU); shorter
+// horizons run fp64 alone (bqp_api.cpp), and their kernels keep the register budget of the
+// plain solve.
+template <bool LONG>
 __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
-    return BQP_HAND_IN && a.hand_in && (a.hand_flag[inst] == 1 || a.hand_flag[inst] == 0);
+    return BQP_HAND_IN && LONG && a.hand_in && (a.hand_flag[inst] == 1 || a.hand_flag[inst] == 0);
 }
 
 #ifdef BQP_STAMPS
@@ -901,7 +908,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     real feasA = 0, gsA = 0;
     real minv, bscale;
     int flag = 0, it0 = 0;
-    if (hand_warm(a, inst)) {
+    if (hand_warm<SPL == 2>(a, inst)) {
         // continue the fp32 phase's iterate (mixed precision); x_0 stays the exact fp64 state
         const float* hb = a.hand_in + (int64_t)inst * a.hand_stride;
         constexpr int SW = hand_stage_w(NS, NU);
@@ -1001,7 +1008,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     }
 
     // ======================= outputs =======================================================
-    if (BQP_HAND_OUT && a.hand_out) {
+    if (BQP_HAND_OUT && SPL == 2 && a.hand_out) {
         // fp32 phase of the mixed mode: hand the iterate to the fp64 launch
         float* hb = a.hand_out + (int64_t)inst * a.hand_stride;
         constexpr int SW = hand_stage_w(NS, NU);
@@ -1556,7 +1563,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     // ======================= initial point ==================================================
     constexpr int HR_T = 0, HR_L = BPL * WAVE, HP_T = 2 * BPL * WAVE, HP_L = (2 * BPL + RPL) * WAVE;
-    if (hand_warm(a, inst)) {
+    if (hand_warm<(BPL >= 16)>(a, inst)) {
         // continue the fp32 phase's iterate (mixed precision): slacks and multipliers as they
         // were, the residuals and multiplier tables formed afresh in fp64
         const float* hb = a.hand_in + (int64_t)inst * a.hand_stride + hand_rows_off(N, NS, NU);
@@ -1672,7 +1679,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     }
 
     // ======================= outputs (multipliers) ==========================================
-    if (BQP_HAND_OUT && a.hand_out) {
+    if (BQP_HAND_OUT && BPL >= 16 && a.hand_out) {
         // fp32 phase of the mixed mode: slacks and multipliers to the handoff record
         float* hb = a.hand_out + (int64_t)inst * a.hand_stride + hand_rows_off(N, NS, NU);
 #pragma unroll
@@ -1726,18 +1733,38 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     const int qpb = a.wpb;
     // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
     real* Hs = lds;
+    const bool fpi = a.Fp_inst != nullptr;   // per-instance polytope: in the instance's LDS slot
     real* Fs = lds + (N + 1) * a.hstride;
     for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
-    for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
+    if (!fpi)
+        for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
     __syncthreads();
     const bool rowwave = wid >= qpb;
     const int slot = rowwave ? wid - qpb : wid;
     const int inst = blockIdx.x * qpb + slot;
     if (inst >= a.batch) return;       // both waves of an empty slot leave together
-    if (a.redo_flag && !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
+    if (SPL == 2 && a.redo_flag &&
+        !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
         return;                        // mixed mode, cold retry launch: nothing to redo here
-    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad);
+    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi);
     real* W = lds + a.shared_doubles + slot * L.total;
+    if (fpi && rowwave) {
+        // the instance's polytope, external column-major [x; u; theta] (n_poly rows) -> internal
+        // [x; theta; u] columns of mpad rows (the layout of the shared table, ocp_prep_kernel)
+        Fs = W + L.Fi;
+        const double* Fg = a.Fp_inst + (int64_t)inst * a.sFp;
+        constexpr int NS = NX + NP;
+        for (int r = lane; r < a.mpad; r += WAVE) {
+#pragma unroll
+            for (int c = 0; c < NV; ++c) {
+                const int e = c < NX ? c : (c < NS ? NX + NU + (c - NX) : NX + (c - NS));
+                real v = (r < a.mp) ? (real)Fg[(int64_t)e * a.mp + r] : real(0);
+                if (a.kp == N && c >= NS) v = 0;
+                Fs[c * a.mpad + r] = v;
+            }
+        }
+        wave_sync();
+    }
     if (!rowwave)
         stage_wave<NX, NU, NP, SPL>(a, W, L, Hs, lane, inst);
     else
@@ -1851,11 +1878,11 @@ int ocp_hand_floats(int N, int nx, int nu, int np, int mp) {
 #endif
 
 // LDS elements (of the instantiation's precision) per instance
-int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad) {
+int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad, bool fpi) {
 #ifdef BQP_F32
-    return sp::QpLds::make(N, nx, nu, np, mpad).total;
+    return sp::QpLds::make(N, nx, nu, np, mpad, fpi).total;
 #else
-    return dp::QpLds::make(N, nx, nu, np, mpad).total;
+    return dp::QpLds::make(N, nx, nu, np, mpad, fpi).total;
 #endif
 }
 
@@ -1864,7 +1891,8 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
     const int rpl = ocp_rpl_for(a.mp);
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
     const size_t lds = sizeof(real) * ((size_t)a.shared_doubles +
-                                       (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad));
+                                       (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad,
+                                                                                      a.Fp_inst != nullptr));
     if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st);
 #ifndef BQP_ISA_ONLY_MG10
     if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st);

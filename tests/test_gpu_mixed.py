@@ -51,7 +51,8 @@ def test_mixed_f2_n100(mg, term_set, handle):
 
 
 def test_mixed_f1_n20(mg, term_set, handle):
-    """C2 problem through the mixed mode: whole decision vector within 1e-8 of z*."""
+    """C2 problem through the mixed mode: short horizons (N < 64) are solved in fp64 alone
+    (include/bqp.h), so the result is the fp64 solve's, within 1e-8 of z*."""
     import bqp
     g = golden('lmpc_N20.npz')
     lm = bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
@@ -63,6 +64,8 @@ def test_mixed_f1_n20(mg, term_set, handle):
     err = np.abs(r.opt_var - zs).max() / max(1.0, np.abs(zs).max())
     print('mixed N=20: |z - z*| %.2e, iterations %.1f' % (err, r.iterations.mean()))
     assert err < TOL_Z, err
+    r64 = lm.solve(g['dx'][g['idx']], handle=handle)
+    assert np.array_equal(r.u, r64.u)
 
 
 def test_mixed_duals_kkt(mg, term_set, handle):
@@ -104,7 +107,7 @@ def test_mixed_status_cold_restart(mg, term_set, handle):
     dx = golden('lmpc_N20.npz')['dx'][:n]
     lm = bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
                   mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
-                  term_set[0], term_set[1], N=20)
+                  term_set[0], term_set[1], N=80)
     r64 = lm.solve(dx, A=A, B=Bm, handle=handle)
     rmx = lm.solve(dx, A=A, B=Bm, handle=handle, precision=2)
     print('mixed C4 sample: flags fp64 %s, mixed %s' % (np.unique(r64.exitflag, return_counts=True),

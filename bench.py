@@ -296,7 +296,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C3', 'C4', 'C5', 'CL'])
+    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C2D', 'C3', 'C4', 'C5', 'CL'])
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32', 'mixed'],
@@ -304,7 +304,7 @@ def main():
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
     args = ap.parse_args()
-    if args.config in ('C1', 'CL', 'C2H'):
+    if args.config in ('C1', 'CL', 'C2H', 'C2D'):
         return bench_aux(args)
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         return launch_ranks(args)
@@ -492,6 +492,87 @@ def bench_aux(args):
                             'parallelism': 'dp1'},
                     roofline=None, kernel_ms=round(h.kernel_ms()[0], 4), cpu_baseline=None,
                     check=dict(converged_frac=float((r.exitflag == 1).mean())))
+    elif args.config == 'C2D':
+        # the C2 problem in fmincon's own form F1 (21 variables, 806 rows) through the dense
+        # quadprog entry point on device buffers: H and A shared, f and b per instance; the
+        # K = H + A'DA factorisation runs on the fp64 matrix cores (dense_wave_kernel<2>)
+        from bqp import _lib
+        from bqp.condense import Condensed
+        wl = workload('C2', args.batch, 0, 1)
+        cd = Condensed(wl['prob'])
+        B = wl['X'].shape[0]
+        f, b = cd.rhs(wl['X'])
+        n, m = cd.n, cd.m
+
+        def dt(a_):
+            return torch.from_numpy(np.ascontiguousarray(a_, dtype=np.float64)).to(dev)
+        dH, dA, df, db = dt(cd.H.T), dt(cd.A.T), dt(f), dt(b)      # column-major H, A
+        ox = torch.empty((B, n), dtype=torch.float64, device=dev)
+        ofv = torch.empty((B,), dtype=torch.float64, device=dev)
+        oe = torch.empty((B,), dtype=torch.int32, device=dev)
+        lam = torch.empty((B, m), dtype=torch.float64, device=dev)
+        lib = bqp.load()
+        dims = _lib.Dims(n, m, 0)
+        strides = _lib.Strides(0, n, 0, m, 0, 0, 0, 0)
+        opt = _lib.options()
+        P = _lib.dptr
+        stream = torch.cuda.current_stream(dev)
+
+        def step():
+            rc = lib.bqp_quadprog_batched_device(
+                h.value, C.byref(dims), B, C.byref(strides), P(dH), P(df), P(dA), P(db), None, None,
+                None, None, C.byref(opt), P(ox), P(ofv),
+                C.cast(C.c_void_p(oe.data_ptr()), C.POINTER(C.c_int)), P(lam), None, None, None,
+                None, C.c_void_p(stream.cuda_stream))
+            _lib.check(rc, 'bqp_quadprog_batched_device')
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = _t.perf_counter()
+        kms = []
+        for _ in range(args.steps):
+            step()
+            kms.append(h.kernel_ms()[0])
+        torch.cuda.synchronize()
+        el = _t.perf_counter() - t0
+        Z = ox.cpu().numpy()
+        u, th, x = cd.recover(Z, wl['X'])
+        g2 = np.load(os.path.join(GOLD, 'lmpc_N20.npz'))
+        du_star = g2['du_star']
+        sel = np.flatnonzero(np.isin(wl['gidx'], g2['idx']))
+        pos = {int(v): i for i, v in enumerate(g2['idx'])}
+        err = max(abs(u[i, 0, 0] - du_star[pos[int(wl['gidx'][i])]]) for i in sel) if len(sel) else None
+        kms_mean = float(np.mean(kms))
+        flops_iter = m * n * n + n ** 3 / 3.0 + 8.0 * m * n          # A'DA (MFMA), Cholesky, mat-vecs
+        its = None
+        try:
+            out = (_lib.Output * B)()
+            rc = lib.bqp_quadprog_batched(h.value, C.byref(dims), B, C.byref(strides),
+                                          _lib.ptr(np.ascontiguousarray(cd.H.T)), _lib.ptr(f),
+                                          _lib.ptr(np.ascontiguousarray(cd.A.T)), _lib.ptr(b),
+                                          None, None, None, None, None, C.byref(opt),
+                                          _lib.ptr(np.zeros((B, n))), None,
+                                          _lib.iptr(np.zeros(B, np.int32)), None, None, None, None,
+                                          out)
+            its = float(np.mean([o.iterations for o in out])) if rc == 0 else None
+        except Exception:
+            its = None
+        ach = B * (its or 0) * flops_iter / (kms_mean * 1e-3) / 1e12
+        line = dict(metric='dense quadprog QP-steps/s (F1, N=20: 21 vars, 806 rows)',
+                    value=round(B * args.steps / el, 1), unit='QP-steps/s', n_gpus=1, steps=args.steps,
+                    warmup=args.warmup, ms_per_step=round(1e3 * el / args.steps, 4),
+                    higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
+                    data=wl['data'],
+                    config={'workload': 'C2 problem in quadprog form F1 (bqp.condense), batch %d' % B,
+                            'batch_per_gpu': B, 'horizon': 20, 'parallelism': 'dp1'},
+                    roofline=dict(bound='fp64_mfma', achieved=round(ach, 4), peak=78.6,
+                                  unit='TFLOP/s', frac=round(ach / 78.6, 5), kernel_ms=round(kms_mean, 4),
+                                  note='per-iteration flops m n^2 + n^3/3 + 8 m n x the kernel\'s own mean '
+                                       'iteration count (no CPU K_ref for this form)'),
+                    cpu_baseline=None,
+                    check=dict(converged_frac=float((oe.cpu().numpy() == 1).mean()),
+                               iterations_mean=its,
+                               max_abs_du0_vs_exact=None if err is None else float(err)))
     elif args.config == 'C1':
         g = np.load(os.path.join(GOLD, 'lbmpc_instance.npz'))
         td = np.load(os.path.join(GOLD, 'train_data.npz'))['data'][:, :100]

@@ -533,20 +533,54 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 #define SW_A_LDS_MAX 4096             // A (m x n) staged in LDS when it has at most this many entries
 
 __host__ __device__ inline int small_lds_doubles(int n, int m) {
-    return n * n + 4 * n + 12 * n + 7 * m + (m * n <= SW_A_LDS_MAX ? m * n : 0);
+    // K, H, f, lb, ub, z, q, dz, rd, 6 x 2n bound-row vectors, 7 m-vectors, b, A (if small)
+    return 2 * n * n + 8 * n + 12 * n + 8 * m + (m * n <= SW_A_LDS_MAX ? m * n : 0);
 }
 
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// A'v for the n <= 16 NT columns of A (column-major m x n): every lane accumulates its rows
+// r = lane, lane + 64, ... for all columns at once, then one transposed wave sum (wsum_t) leaves
+// column c's total in lane c (& 31).  No serial m-long chain on the n column lanes.
+template <int NT>
+__device__ __forceinline__ double atv(const double* A, const double* v, int m, int n, int lane) {
+    constexpr int NM = 16 * NT;
+    double acc[NM];
+#pragma unroll
+    for (int c = 0; c < NM; ++c) acc[c] = 0.0;
+    for (int r = lane; r < m; r += 64) {
+        const double vr = v[r];
+#pragma unroll
+        for (int c = 0; c < NM; ++c)
+            if (c < n) acc[c] = fma(A[(int64_t)c * m + r], vr, acc[c]);
+    }
+    return wsum_t(acc, lane);
+}
+
+// small dense QPs (n <= 32, no equality rows): one wave per instance, vectors, H and K in LDS.
+// K = H + A'DA on the matrix cores: v_mfma_f64_16x16x4_f64 tiles of A'(D A) over 4 rows of A per
+// instruction (lane l supplies A[r0 + l/16][16 I + l%16] as the A operand and d_r times the same
+// entry of column tile J as the B operand), one 16 x 16 tile for n <= 16, three for n <= 32
+// (the lower block triangle).  The A'v products are transposed wave sums, the Cholesky and its
+// triangular solves column-oriented with readlane broadcasts.  Same Mehrotra rules and start
+// as dense_ipm_kernel; used for the LBMPC SQP sub-problems (n = N*nu + np = 11 at config C1) and
+// small quadprog calls (F1 at N = 20: n = 21, m = 806).
+template <int NT>
 __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
     if (inst >= a.batch) return;
     const int n = a.n, m = a.m, lane = threadIdx.x;
     extern __shared__ double sm[];
     double* K = sm;                       // n x n column-major; lower Cholesky factor in place
-    double* z = K + n * n;
+    double* Hs = K + n * n;               // H (n x n column-major)
+    double* fs = Hs + n * n;
+    double* z = fs + n;
     double* q = z + n;
     double* dz = q + n;
     double* rd = dz + n;
-    double* tB = rd + n;                  // bound rows: [upper 0..n-1, lower n..2n-1]
+    double* ubs = rd + n;
+    double* lbs = ubs + n;
+    double* tB = lbs + n;                 // bound rows: [upper 0..n-1, lower n..2n-1]
     double* lB = tB + 2 * n;
     double* riB = lB + 2 * n;
     double* rcB = riB + 2 * n;
@@ -559,136 +593,229 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     double* dtA = rcA + m;
     double* dlA = dtA + m;
     double* DA = dlA + m;
+    double* bs = DA + m;
     const double* H = a.H + (int64_t)inst * a.sH;
     const double* f = a.f + (int64_t)inst * a.sf;
     const double* A = a.A ? a.A + (int64_t)inst * a.sA : nullptr;
     const double* b = a.b ? a.b + (int64_t)inst * a.sb : nullptr;
     const double* lb = a.lb ? a.lb + (int64_t)inst * a.slb : nullptr;
     const double* ub = a.ub ? a.ub + (int64_t)inst * a.sub : nullptr;
-    if (A && m * n <= SW_A_LDS_MAX) {             // the rows are re-read ~6x per IPM iteration
-        double* As = DA + m;
+    // stage the instance's data: H, f, b, bounds (read every iteration); A when it is small
+    for (int i = lane; i < n * n; i += 64) Hs[i] = H[i];
+    for (int r = lane; r < m; r += 64) bs[r] = b[r];
+    if (lane < n) {
+        fs[lane] = f[lane];
+        ubs[lane] = ub ? ub[lane] : INFINITY;
+        lbs[lane] = lb ? lb[lane] : -INFINITY;
+    }
+    if (A && m * n <= SW_A_LDS_MAX) {
+        double* As = bs + m;
         for (int i = lane; i < m * n; i += 64) As[i] = A[i];
-        wave_sync();
         A = As;
     }
-    auto up_present = [&](int j) -> bool { return ub && isfinite(ub[j]); };
-    auto lo_present = [&](int j) -> bool { return lb && isfinite(lb[j]); };
-    double cnt = 0.0;
-    for (int j = lane; j < n; j += 64) cnt += (up_present(j) ? 1.0 : 0.0) + (lo_present(j) ? 1.0 : 0.0);
-    const double minv = 1.0 / fmax(wsum(cnt) + (double)m, 1.0);
+    wave_sync();
+    // lane j < n owns variable j and both its bound rows
+    const bool upj = lane < n && isfinite(ubs[lane]);
+    const bool loj = lane < n && isfinite(lbs[lane]);
+    const double ubj = upj ? ubs[lane] : 0.0, lbj = loj ? lbs[lane] : 0.0;
+    const double minv = 1.0 / fmax(wsum((upj ? 1.0 : 0.0) + (loj ? 1.0 : 0.0)) + (double)m, 1.0);
 
-    auto residuals = [&](double& stat, double& fin, double& csum, double& gscale, double& zmax) {
+    auto residuals = [&](double& stat, double& fin, double& csum, double& gscale, double& zmax) __attribute__((always_inline)) {
         double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0;
+        double zc[16 * NT];
+#pragma unroll
+        for (int c = 0; c < 16 * NT; ++c) zc[c] = c < n ? z[c] : 0.0;
         for (int r = lane; r < m; r += 64) {
-            double v = tA[r] - b[r];
-            for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
+            double v = tA[r] - bs[r];
+#pragma unroll
+            for (int c = 0; c < 16 * NT; ++c)
+                if (c < n) v = fma(A[(int64_t)c * m + r], zc[c], v);   // independent loads, one chain
             riA[r] = v;
             fe = fmax(fe, fabs(v));
-            cs += tA[r] * lA[r];
+            cs = fma(tA[r], lA[r], cs);
         }
-        for (int j = lane; j < n; j += 64) {
-            double v = f[j];
-            for (int i = 0; i < n; ++i) v += H[(int64_t)j * n + i] * z[i];
-            gs = fmax(gs, fabs(v));
-            for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * lA[r];
+        const double atl = atv<NT>(A, lA, m, n, lane);       // (A' lam)_lane
+        if (lane < n) {
+            const int j = lane;
+            double v = fs[j];
+#pragma unroll
+            for (int i = 0; i < 16 * NT; ++i)
+                if (i < n) v = fma(Hs[j * n + i], zc[i], v);
+            gs = fabs(v);
+            v += atl;
             riB[j] = 0.0; riB[n + j] = 0.0;
-            if (up_present(j)) { v += lB[j]; riB[j] = z[j] + tB[j] - ub[j]; cs += tB[j] * lB[j]; }
-            if (lo_present(j)) { v -= lB[n + j]; riB[n + j] = -z[j] + tB[n + j] + lb[j]; cs += tB[n + j] * lB[n + j]; }
+            if (upj) { v += lB[j]; riB[j] = z[j] + tB[j] - ubj; cs += tB[j] * lB[j]; }
+            if (loj) { v -= lB[n + j]; riB[n + j] = -z[j] + tB[n + j] + lbj; cs += tB[n + j] * lB[n + j]; }
             fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
             rd[j] = v;
-            st = fmax(st, fabs(v));
-            zm = fmax(zm, fabs(z[j]));
+            st = fabs(v);
+            zm = fabs(z[j]);
         }
         stat = wmax(st); fin = wmax(fe); csum = wsum(cs); gscale = wmax(gs); zmax = wmax(zm);
         wave_sync();
     };
 
-    // in-place lower Cholesky of K (lane r owns row r).  fl >= 0: pivots floored at fl (static
-    // pivoting); fl < 0: false at the first non-positive pivot (the convexity test)
-    auto chol = [&](double fl) -> bool {
+    // Cholesky in registers: lane r < n holds row r of the lower factor (Lr[c], c <= r), its
+    // reciprocal pivot (dinv) and, after the factorisation, column r of it (Lc[i] = L(i, r),
+    // i > r, for the backward substitution).  Right-looking over the columns j: the pivot comes
+    // from lane j by readlane, the scaled column entries L(c, j) from lane c - no LDS and no
+    // barrier on the sequential chain.  fl >= 0: pivots floored at fl (static pivoting);
+    // fl < 0: false at the first non-positive pivot (the convexity test).
+    constexpr int NM = 16 * NT;
+    double Lr[NM], Lc[NM], dinv = 0.0;
+    auto load_rows = [&]() __attribute__((always_inline)) {                          // rows of the lower triangle of K (LDS)
+#pragma unroll
+        for (int c = 0; c < NM; ++c) Lr[c] = (c < n && c <= lane && lane < n) ? K[(int64_t)c * n + lane] : 0.0;
+    };
+    auto chol = [&](double fl) __attribute__((always_inline)) -> bool {
         bool ok = true;
-        for (int j = 0; j < n; ++j) {
-            double d = K[(int64_t)j * n + j];
-            if (fl >= 0.0 && !(d > fl)) d = fl;
-            if (!(d > 0.0)) { ok = false; break; }
-            const double ljj = sqrt(d);
-            const double il = 1.0 / ljj;
-            if (lane > j && lane < n) K[(int64_t)j * n + lane] *= il;
-            if (lane == j) K[(int64_t)j * n + j] = ljj;
-            wave_sync();
-            if (lane > j && lane < n) {
-                const double lrj = K[(int64_t)j * n + lane];
-                for (int c = j + 1; c <= lane; ++c) K[(int64_t)c * n + lane] -= lrj * K[(int64_t)j * n + c];
+#pragma unroll
+        for (int jj = 0; jj < NM; ++jj) {
+            if (jj < n && ok) {
+                double d = rl(Lr[jj], jj);
+                if (fl >= 0.0 && !(d > fl)) d = fl;
+                if (!(d > 0.0)) {
+                    ok = false;
+                } else {
+                    const double ljj = sqrt(d);
+                    const double il = 1.0 / ljj;
+                    if (lane > jj) Lr[jj] *= il;
+                    if (lane == jj) { Lr[jj] = ljj; dinv = il; }
+#pragma unroll
+                    for (int c = jj + 1; c < NM; ++c) {
+                        if (c < n) {
+                            const double lcj = rl(Lr[jj], c);
+                            if (lane >= c) Lr[c] = fma(-Lr[jj], lcj, Lr[c]);
+                        }
+                    }
+                }
             }
+        }
+        if (ok) {
+            // transpose through LDS (K is free now): lane c gets L(i, c) for i > c
+            if (lane < n) {
+#pragma unroll
+                for (int c = 0; c < NM; ++c) if (c < n && c <= lane) K[(int64_t)lane * n + c] = Lr[c];
+            }
+            wave_sync();
+#pragma unroll
+            for (int ii = 0; ii < NM; ++ii) Lc[ii] = (ii < n && lane < ii) ? K[(int64_t)ii * n + lane] : 0.0;
             wave_sync();
         }
         return ok;
     };
-    // K = H + A'DA + bound diagonal, factored with the static pivot floor
-    auto factor = [&]() -> bool {
+    // K = H + A'DA + bound diagonal on the matrix cores, factored with the static pivot floor
+    auto factor = [&]() __attribute__((always_inline)) -> bool {
         for (int r = lane; r < m; r += 64) DA[r] = lA[r] / tA[r];
         wave_sync();
-        const int ne = n * (n + 1) / 2;
-        double dmx = 0.0;
-        for (int e2 = lane; e2 < ne; e2 += 64) {
-            int j = (int)((sqrt(8.0 * e2 + 1.0) - 1.0) / 2.0);
-            while (j * (j + 1) / 2 > e2) --j;
-            while ((j + 1) * (j + 2) / 2 <= e2) ++j;
-            const int i = e2 - j * (j + 1) / 2;          // i <= j
-            double v = H[(int64_t)j * n + i];
-            for (int r = 0; r < m; ++r) v += A[(int64_t)i * m + r] * DA[r] * A[(int64_t)j * m + r];
-            if (i == j) {
-                if (up_present(j)) v += lB[j] / tB[j];
-                if (lo_present(j)) v += lB[n + j] / tB[n + j];
-                dmx = fmax(dmx, fabs(v));
+        constexpr int NTL = NT * (NT + 1) / 2;     // lower block triangle: (0,0), (1,0), (1,1)
+        dbl4 acc[NTL];
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+        const int c16 = lane & 15, k4 = lane >> 4;
+        constexpr int KU = 4;                      // k-steps per trip: the loads of 4 steps in flight
+        for (int r0 = 0; r0 < m; r0 += 4 * KU) {
+            double av[KU][NT], dv[KU];
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int r = r0 + 4 * u + k4;
+                const bool rv = r < m;
+                dv[u] = rv ? DA[r] : 0.0;
+#pragma unroll
+                for (int I = 0; I < NT; ++I) {
+                    const int c = 16 * I + c16;
+                    av[u][I] = (rv && c < n) ? A[(int64_t)c * m + r] : 0.0;
+                }
             }
-            K[(int64_t)i * n + j] = v;                   // lower: row j, column i
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                int t = 0;
+#pragma unroll
+                for (int I = 0; I < NT; ++I)
+#pragma unroll
+                    for (int J = 0; J <= I; ++J, ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u][I], dv[u] * av[u][J], acc[t], 0, 0, 0);
+            }
         }
+        // tile (I, J), lane l, register e: K(16 I + l/16 + 4 e, 16 J + l%16)
+        double dmx = 0.0;
+        int t = 0;
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J, ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = 16 * I + k4 + 4 * e, col = 16 * J + c16;
+                    if (row < n && col < n && row >= col) {
+                        double v = acc[t][e] + Hs[col * n + row];
+                        if (row == col) {
+                            if (isfinite(ubs[row])) v += lB[row] / tB[row];
+                            if (isfinite(lbs[row])) v += lB[n + row] / tB[n + row];
+                            dmx = fmax(dmx, fabs(v));
+                        }
+                        K[(int64_t)col * n + row] = v;        // lower: row, column col
+                    }
+                }
         const double kfl = DQ_PIV_FLOOR * fmax(wmax(dmx), 1e-300);
         wave_sync();
+        load_rows();
         return chol(kfl);
     };
 
-    // x = -(L L')^{-1} q with lane i holding entry i (n <= 32): column-oriented substitution,
-    // the solved entry broadcast by readlane
-    auto chol_neg_solve = [&](double* x) {
+    // x = -(L L')^{-1} q with lane i holding entry i (n <= 32): column-oriented substitution on
+    // the register factor, the solved entry broadcast by readlane
+    auto chol_neg_solve = [&](double* x) __attribute__((always_inline)) {
         double v = (lane < n) ? -q[lane] : 0.0;
-        for (int i = 0; i < n; ++i) {                     // L y = -q
-            const double yi = rl(v, i) / K[(int64_t)i * n + i];
-            if (lane == i) v = yi;
-            else if (lane > i && lane < n) v -= K[(int64_t)i * n + lane] * yi;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {                    // L y = -q
+            if (i < n) {
+                const double yi = rl(v, i) * rl(dinv, i);
+                if (lane == i) v = yi;
+                else if (lane > i) v = fma(-Lr[i], yi, v);
+            }
         }
-        for (int i = n - 1; i >= 0; --i) {                // L' x = y
-            const double xi = rl(v, i) / K[(int64_t)i * n + i];
-            if (lane == i) v = xi;
-            else if (lane < i) v -= K[(int64_t)lane * n + i] * xi;
+#pragma unroll
+        for (int i = NM - 1; i >= 0; --i) {               // L' x = y
+            if (i < n) {
+                const double xi = rl(v, i) * rl(dinv, i);
+                if (lane == i) v = xi;
+                else if (lane < i) v = fma(-Lc[i], xi, v);
+            }
         }
         if (lane < n) x[lane] = v;
         wave_sync();
     };
 
-    auto solve = [&]() {
+    auto solve = [&]() __attribute__((always_inline)) {
         for (int r = lane; r < m; r += 64) dlA[r] = (lA[r] * riA[r] - rcA[r]) / tA[r];
         wave_sync();
-        for (int j = lane; j < n; j += 64) {
-            double v = rd[j];
-            for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * dlA[r];
-            if (up_present(j)) v += (lB[j] * riB[j] - rcB[j]) / tB[j];
-            if (lo_present(j)) v -= (lB[n + j] * riB[n + j] - rcB[n + j]) / tB[n + j];
+        const double atd = atv<NT>(A, dlA, m, n, lane);
+        if (lane < n) {
+            const int j = lane;
+            double v = rd[j] + atd;
+            if (upj) v += (lB[j] * riB[j] - rcB[j]) / tB[j];
+            if (loj) v -= (lB[n + j] * riB[n + j] - rcB[n + j]) / tB[n + j];
             q[j] = v;
         }
         wave_sync();
         chol_neg_solve(dz);
+        double dzc[NM];
+#pragma unroll
+        for (int c = 0; c < NM; ++c) dzc[c] = c < n ? dz[c] : 0.0;
         for (int r = lane; r < m; r += 64) {
             double v = 0.0;
-            for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * dz[j];
+#pragma unroll
+            for (int c = 0; c < NM; ++c)
+                if (c < n) v = fma(A[(int64_t)c * m + r], dzc[c], v);
             dtA[r] = -riA[r] - v;
             dlA[r] = (-rcA[r] - lA[r] * dtA[r]) / tA[r];
         }
-        for (int j = lane; j < n; j += 64) {
+        if (lane < n) {
+            const int j = lane;
             dtB[j] = dlB[j] = dtB[n + j] = dlB[n + j] = 0.0;
-            if (up_present(j)) { dtB[j] = -riB[j] - dz[j]; dlB[j] = (-rcB[j] - lB[j] * dtB[j]) / tB[j]; }
-            if (lo_present(j)) { dtB[n + j] = -riB[n + j] + dz[j]; dlB[n + j] = (-rcB[n + j] - lB[n + j] * dtB[n + j]) / tB[n + j]; }
+            if (upj) { dtB[j] = -riB[j] - dz[j]; dlB[j] = (-rcB[j] - lB[j] * dtB[j]) / tB[j]; }
+            if (loj) { dtB[n + j] = -riB[n + j] + dz[j]; dlB[n + j] = (-rcB[n + j] - lB[n + j] * dtB[n + j]) / tB[n + j]; }
         }
         wave_sync();
     };
@@ -696,9 +823,10 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         double al = 1.0;
 #define DW_RATIO(v, dv) if ((dv) < 0.0) al = fmin(al, -(v) / (dv));
         for (int r = lane; r < m; r += 64) { DW_RATIO(tA[r], dtA[r]); DW_RATIO(lA[r], dlA[r]); }
-        for (int j = lane; j < n; j += 64) {
-            if (up_present(j)) { DW_RATIO(tB[j], dtB[j]); DW_RATIO(lB[j], dlB[j]); }
-            if (lo_present(j)) { DW_RATIO(tB[n + j], dtB[n + j]); DW_RATIO(lB[n + j], dlB[n + j]); }
+        if (lane < n) {
+            const int j = lane;
+            if (upj) { DW_RATIO(tB[j], dtB[j]); DW_RATIO(lB[j], dlB[j]); }
+            if (loj) { DW_RATIO(tB[n + j], dtB[n + j]); DW_RATIO(lB[n + j], dlB[n + j]); }
         }
 #undef DW_RATIO
         return wmin(al);
@@ -706,44 +834,42 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     auto comp_after = [&](double al) -> double {
         double c = 0.0;
         for (int r = lane; r < m; r += 64) c += (tA[r] + al * dtA[r]) * (lA[r] + al * dlA[r]);
-        for (int j = lane; j < n; j += 64) {
-            if (up_present(j)) c += (tB[j] + al * dtB[j]) * (lB[j] + al * dlB[j]);
-            if (lo_present(j)) c += (tB[n + j] + al * dtB[n + j]) * (lB[n + j] + al * dlB[n + j]);
+        if (lane < n) {
+            const int j = lane;
+            if (upj) c += (tB[j] + al * dtB[j]) * (lB[j] + al * dlB[j]);
+            if (loj) c += (tB[n + j] + al * dtB[n + j]) * (lB[n + j] + al * dlB[n + j]);
         }
         return wsum(c);
     };
 
     // initial point (as dense_ipm_kernel)
-    for (int j = lane; j < n; j += 64) {
+    if (lane < n) {
+        const int j = lane;
         z[j] = 0.0;
         tB[j] = tB[n + j] = 1.0;
-        lB[j] = up_present(j) ? 1.0 : 0.0;
-        lB[n + j] = lo_present(j) ? 1.0 : 0.0;
-        rcB[j] = up_present(j) ? 1.0 : 0.0;
-        rcB[n + j] = lo_present(j) ? 1.0 : 0.0;
+        lB[j] = upj ? 1.0 : 0.0;
+        lB[n + j] = loj ? 1.0 : 0.0;
+        rcB[j] = upj ? 1.0 : 0.0;
+        rcB[n + j] = loj ? 1.0 : 0.0;
     }
     for (int r = lane; r < m; r += 64) { tA[r] = 1.0; lA[r] = 1.0; rcA[r] = 1.0; }
     wave_sync();
     double bsl = 0.0;
-    for (int r = lane; r < m; r += 64) bsl = fmax(bsl, fabs(b[r]));
-    for (int j = lane; j < n; j += 64) {
-        if (up_present(j)) bsl = fmax(bsl, fabs(ub[j]));
-        if (lo_present(j)) bsl = fmax(bsl, fabs(lb[j]));
-    }
+    for (int r = lane; r < m; r += 64) bsl = fmax(bsl, fabs(bs[r]));
+    if (upj) bsl = fmax(bsl, fabs(ubj));
+    if (loj) bsl = fmax(bsl, fabs(lbj));
     const double bscale = wmax(bsl);
-    double fmx = 0.0;
-    for (int j = lane; j < n; j += 64) fmx = fmax(fmx, fabs(f[j]));
-    const double zbig = DQ_Z_BIG * (1.0 + bscale + wmax(fmx));
+    const double zbig = DQ_Z_BIG * (1.0 + bscale + wmax(lane < n ? fabs(fs[lane]) : 0.0));
     int flag = 0;
     {
         // convexity test: Cholesky of H + CONVEX_EPS max(1, max H_ii) I without pivot floor
-        double hd = 0.0;
-        for (int j = lane; j < n; j += 64) hd = fmax(hd, fabs(H[(int64_t)j * n + j]));
-        const double sh = DQ_CONVEX_EPS * fmax(1.0, wmax(hd));
+        const double sh = DQ_CONVEX_EPS * fmax(1.0, wmax(lane < n ? fabs(Hs[lane * n + lane]) : 0.0));
         for (int e2 = lane; e2 < n * n; e2 += 64) {
             const int i = e2 % n, j = e2 / n;
-            K[e2] = H[e2] + (i == j ? sh : 0.0);
+            K[e2] = Hs[e2] + (i == j ? sh : 0.0);
         }
+        wave_sync();
+        load_rows();
         wave_sync();
         if (!chol(-1.0)) flag = -6;
     }
@@ -754,21 +880,20 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     if (flag == 0) {
         solve();
         double tmin = INFINITY, tmax = -INFINITY;
-        for (int j = lane; j < n; j += 64) z[j] += dz[j];
+        if (lane < n) z[lane] += dz[lane];
         for (int r = lane; r < m; r += 64) { const double t = 1.0 + dtA[r]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
-        for (int j = lane; j < n; j += 64) {
-            if (up_present(j)) { const double t = 1.0 + dtB[j]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
-            if (lo_present(j)) { const double t = 1.0 + dtB[n + j]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
-        }
+        if (upj) { const double t = 1.0 + dtB[lane]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+        if (loj) { const double t = 1.0 + dtB[n + lane]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
         tmin = wmin(tmin);
         tmax = wmax(tmax);
         const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
         const double shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
         for (int r = lane; r < m; r += 64) { const double t = 1.0 + dtA[r]; tA[r] = t + shp; lA[r] = -t + shd; }
-        for (int j = lane; j < n; j += 64) {
+        if (lane < n) {
+            const int j = lane;
             const double tu = 1.0 + dtB[j], tl = 1.0 + dtB[n + j];
-            tB[j] = up_present(j) ? tu + shp : 1.0; lB[j] = up_present(j) ? -tu + shd : 0.0;
-            tB[n + j] = lo_present(j) ? tl + shp : 1.0; lB[n + j] = lo_present(j) ? -tl + shd : 0.0;
+            tB[j] = upj ? tu + shp : 1.0; lB[j] = upj ? -tu + shd : 0.0;
+            tB[n + j] = loj ? tl + shp : 1.0; lB[n + j] = loj ? -tl + shd : 0.0;
         }
         wave_sync();
     }
@@ -788,7 +913,7 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }
             for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r];
-            for (int j = lane; j < 2 * n; j += 64) rcB[j] = tB[j] * lB[j];
+            if (lane < n) { rcB[lane] = tB[lane] * lB[lane]; rcB[n + lane] = tB[n + lane] * lB[n + lane]; }
             wave_sync();
             solve();
             double al = max_step();
@@ -797,30 +922,33 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             sg = sg * sg * sg;
             const double smu = sg * mu;
             for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r] + dtA[r] * dlA[r] - smu;
-            for (int j = lane; j < n; j += 64) {
-                rcB[j] = up_present(j) ? tB[j] * lB[j] + dtB[j] * dlB[j] - smu : 0.0;
-                rcB[n + j] = lo_present(j) ? tB[n + j] * lB[n + j] + dtB[n + j] * dlB[n + j] - smu : 0.0;
+            if (lane < n) {
+                const int j = lane;
+                rcB[j] = upj ? tB[j] * lB[j] + dtB[j] * dlB[j] - smu : 0.0;
+                rcB[n + j] = loj ? tB[n + j] * lB[n + j] + dtB[n + j] * dlB[n + j] - smu : 0.0;
             }
             wave_sync();
             solve();
             al = fmin(1.0, max_step() * a.tau);
-            for (int j = lane; j < n; j += 64) {
+            if (lane < n) {
+                const int j = lane;
                 z[j] += al * dz[j];
-                if (up_present(j)) { tB[j] += al * dtB[j]; lB[j] += al * dlB[j]; }
-                if (lo_present(j)) { tB[n + j] += al * dtB[n + j]; lB[n + j] += al * dlB[n + j]; }
+                if (upj) { tB[j] += al * dtB[j]; lB[j] += al * dlB[j]; }
+                if (loj) { tB[n + j] += al * dtB[n + j]; lB[n + j] += al * dlB[n + j]; }
             }
             for (int r = lane; r < m; r += 64) { tA[r] += al * dtA[r]; lA[r] += al * dlA[r]; }
             wave_sync();
         }
     }
     double fv = 0.0;
-    for (int j = lane; j < n; j += 64) {
+    if (lane < n) {
+        const int j = lane;
         double hz = 0.0;
-        for (int i = 0; i < n; ++i) hz += H[(int64_t)j * n + i] * z[i];
-        fv += z[j] * (0.5 * hz + f[j]);
+        for (int i = 0; i < n; ++i) hz += Hs[j * n + i] * z[i];
+        fv = z[j] * (0.5 * hz + fs[j]);
         a.x[(int64_t)inst * n + j] = z[j];
-        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = (lo_present(j) && flag != -6) ? lB[n + j] : 0.0;
-        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = (up_present(j) && flag != -6) ? lB[j] : 0.0;
+        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = (loj && flag != -6) ? lB[n + j] : 0.0;
+        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = (upj && flag != -6) ? lB[j] : 0.0;
     }
     for (int r = lane; r < m; r += 64)
         if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = flag != -6 ? lA[r] : 0.0;
@@ -836,8 +964,11 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
 hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
     if (a.n > 256 || a.me > 256) return hipErrorInvalidValue;
     if (a.me == 0 && a.n <= SW_NMAX && small_lds_doubles(a.n, a.m) <= SW_LDS_MAX) {
-        hipLaunchKernelGGL(dense_wave_kernel, dim3(a.batch), dim3(64),
-                           sizeof(double) * small_lds_doubles(a.n, a.m), st, a);
+        const size_t lds = sizeof(double) * small_lds_doubles(a.n, a.m);
+        if (a.n <= 16)
+            hipLaunchKernelGGL(dense_wave_kernel<1>, dim3(a.batch), dim3(64), lds, st, a);
+        else
+            hipLaunchKernelGGL(dense_wave_kernel<2>, dim3(a.batch), dim3(64), lds, st, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(dense_ipm_kernel, dim3(a.batch), dim3(DT), 0, st, a);

@@ -1732,6 +1732,16 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     const int wid = threadIdx.x >> 6;
     const int qpb = a.wpb;
     // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
+    if constexpr (SPL == 2) {
+        // mixed mode, cold retry launch: a workgroup none of whose instances needs the retry
+        // leaves before staging the shared tables
+        if (a.redo_flag) {
+            const int i0 = blockIdx.x * a.wpb + ((threadIdx.x >> 6) % a.wpb);
+            const bool need = i0 < a.batch && a.exitflag[i0] != 1 &&
+                              (a.redo_flag[i0] == 1 || a.redo_flag[i0] == 0);
+            if (!__syncthreads_or(need)) return;
+        }
+    }
     real* Hs = lds;
     const bool fpi = a.Fp_inst != nullptr;   // per-instance polytope: in the instance's LDS slot
     real* Fs = lds + (N + 1) * a.hstride;

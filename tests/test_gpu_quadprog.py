@@ -72,3 +72,25 @@ def test_box_bounds_and_infeasible_free(handle):
         z, fv, _, _ = dense_qp.solve(qp_forms.dense_qp(H[i], f[i], A[i], b[i], lb=lb, ub=ub))
         assert np.abs(x[i] - z).max() < 1e-8
         assert abs(fval[i] - fv) < 1e-8 * max(1, abs(fv))
+
+
+def test_condensed_c2_batch_on_matrix_cores(mg, term_set, handle):
+    """the C2 states through bqp.condense + bqp.quadprog (H, A shared; f, b per instance): the
+    n = 21 instances run dense_wave_kernel<2> (MFMA factorisation); first moves within 1e-8 of
+    z*, multipliers satisfy quadprog's stationarity"""
+    import bqp
+    from bqp.condense import Condensed
+    g = golden('lmpc_N20.npz')
+    lm = bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                  mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                  term_set[0], term_set[1], N=20)
+    cd = Condensed(lm.prob)
+    X0 = g['dx'][g['idx']]
+    f, b = cd.rhs(X0)
+    x, fval, flag, out, lam = bqp.quadprog(cd.H, f, cd.A, b, handle=handle)
+    assert (flag == 1).all()
+    u, th, xs = cd.recover(x, X0)
+    assert np.abs(u[:, 0, 0] - g['du_star']).max() < 1e-8
+    for i in range(len(X0)):
+        r = cd.H @ x[i] + f[i] + cd.A.T @ lam['ineqlin'][i]
+        assert np.abs(r).max() < 1e-6 * (1 + np.abs(f[i]).max())

@@ -46,6 +46,7 @@ struct bqp_handle_s {
     DevBuf lwork;  // learning-based MPC (SQP) buffers
     DevBuf cwork;  // closed-loop simulation buffers
     DevBuf hwork;  // mixed precision: fp32 -> fp64 handoff records
+    DevBuf pwork;  // long-horizon layout: global Riccati tables
     int last_batch = 0;
 };
 
@@ -143,6 +144,7 @@ int bqp_destroy(bqp_handle h) {
         h->lwork.release();
         h->cwork.release();
         h->hwork.release();
+        h->pwork.release();
         if (h->ev0) hipEventDestroy(h->ev0);
         if (h->ev1) hipEventDestroy(h->ev1);
         if (h->stream) hipStreamDestroy(h->stream);
@@ -203,11 +205,12 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     o32.tol_feas = std::max(o.tol_feas, 1e-6);
     o32.tol_comp = std::max(o.tol_comp, 1e-9);
     if (mixed) {
-        // hand over once the fp32 iterate is feasible to 1e-6 and mu <= 1e-7: the fp64 launch then
-        // needs ~3 iterations and ends at the fp64 solve's KKT accuracy (duals within 5e-8 of
-        // lambda*); a later switch (mu 1e-9) saves 4 % more time but leaves the duals at 1.7e-7
-        // (tools/diag_mixed.py, profiles/r02_mx/diag_switch.log).  BQP_MIXED_MU overrides, for that sweep.
-        o32.tol_comp = std::max(o.tol_comp, 1e-7);
+        // hand over once the fp32 iterate is feasible to 1e-6 and mu <= 1e-6: the fp64 launch then
+        // needs ~4 iterations and ends at the fp64 solve's KKT accuracy (duals within ~3e-8 of
+        // lambda*); later switches (mu 1e-7 .. 1e-9) save 3-7 % of the time but leave the duals
+        // of some instances at 1e-7 .. 2e-7 (tools/diag_mixed.py, profiles/r02_mx/diag_switch.log).
+        // BQP_MIXED_MU overrides, for that sweep.
+        o32.tol_comp = std::max(o.tol_comp, 1e-6);
         const char* e = getenv("BQP_MIXED_MU");
         if (e) o32.tol_comp = atof(e);
     }
@@ -219,11 +222,34 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));   // = the kernel's RPL * 64
     // per-instance polytope (sFp != 0): each instance's LDS slot holds its own NV x mpad table
     const bool fpi = mp > 0 && D->sFp != 0;
-    const int shared_doubles = (((N + 1) * hstride + (fpi ? 0 : nv * mpad)) + 1) & ~1;   // elements
+    // long horizons (two stages per lane): H read from global, Riccati tables in global scratch,
+    // polytope rhs / box bounds in the shared tables when the batch shares them (QpLds lng)
+    // (fp64 instantiation only; the fp32 one keeps the plain layout)
+    struct Shared { bool lng, hpsh, bndsh; int sh_F, sh_hp, sh_bnd, doubles; };
+    auto shared_layout = [&](bool single) {
+        Shared o;
+        o.lng = !single && N + 1 > 64;
+        o.hpsh = o.lng && mp > 0 && D->shp == 0;
+        o.bndsh = o.lng && D->sxb == 0 && D->sub == 0;
+        const int nbr = (N + 1) * 2 * (nx + nu);
+        int sh = o.lng ? 0 : (N + 1) * hstride;
+        o.sh_F = sh;
+        sh += fpi ? 0 : nv * mpad;
+        o.sh_hp = o.hpsh ? sh : -1;
+        sh += o.hpsh ? mpad : 0;
+        o.sh_bnd = o.bndsh ? sh : -1;
+        sh += o.bndsh ? nbr : 0;
+        o.doubles = (sh + 1) & ~1;   // elements
+        return o;
+    };
+    const Shared L64 = shared_layout(f32), L32 = shared_layout(true);
+    const bool lng = L64.lng;
     // instances per workgroup (two waves each) that fit the 160 KB of LDS
     auto fit_wpb = [&](bool single, int& wpb) -> bool {
-        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi)
-                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi);
+        const Shared& S = single ? L32 : L64;
+        const int shared_doubles = S.doubles;
+        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi, false, false, false)
+                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi, S.lng, S.hpsh, S.bndsh);
         const size_t lds_budget = 160 * 1024 / (single ? sizeof(float) : sizeof(double));
         // long horizons (N + 1 > 64, two stages per lane) are compiled for <= 256 threads per
         // workgroup: one wave per SIMD, whose 512 registers hold the doubled stage state
@@ -244,12 +270,19 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     double* Hd = (double*)h->work.p;
     double* Fd = Hd + nH;
     double* Sd = Fd + nF;
+    void* Pg = nullptr;
+    if (lng) {   // global Riccati tables of the long-horizon layout
+        HIP_TRY(h->pwork.reserve(sizeof(double) * (size_t)batch * (N + 1) * bqp::ocp_pstride(nx + np)));
+        Pg = h->pwork.p;
+    }
     HIP_TRY(bqp::launch_ocp_prep(D->W, mp > 0 ? D->Fp : D->W, nx, nu, np, N, mp, d->poly_stage,
                                  hstride, mpad, Hd, Fd, st));
     bqp::OcpKernelArgs a;
     memset(&a, 0, sizeof(a));
     a.N = N; a.mp = mp; a.kp = d->poly_stage; a.batch = batch; a.wpb = wpb;
-    a.hstride = hstride; a.mpad = mpad; a.shared_doubles = shared_doubles;
+    const Shared& LS = f32 ? L32 : L64;
+    a.hstride = hstride; a.mpad = mpad; a.shared_doubles = LS.doubles;
+    a.Pg = Pg; a.sh_F = LS.sh_F; a.sh_hp = LS.sh_hp; a.sh_bnd = LS.sh_bnd;
     a.max_iter = o.max_iter; a.tol_stat = o.tol_stat; a.tol_feas = o.tol_feas;
     a.tol_comp = o.tol_comp; a.tau = o.tau;
     a.H = Hd; a.Fp = Fd;
@@ -279,6 +312,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         int* hit = hflag + batch;
         bqp::OcpKernelArgs a1 = a;
         a1.wpb = wpb32;
+        a1.shared_doubles = L32.doubles; a1.sh_F = L32.sh_F; a1.sh_hp = L32.sh_hp; a1.sh_bnd = L32.sh_bnd;
         a1.max_iter = o32.max_iter; a1.tol_stat = o32.tol_stat; a1.tol_feas = o32.tol_feas;
         a1.tol_comp = o32.tol_comp;
         a1.exitflag = hflag;

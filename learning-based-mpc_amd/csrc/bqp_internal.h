@@ -44,16 +44,25 @@ struct OcpKernelArgs {
     // blocks, stride sFp; the shared Fp table is then unused
     const double* Fp_inst;
     int64_t sFp;
+    // long-horizon layout (two stages per lane, N + 1 > 64; QpLds lng): Riccati tables in global
+    // scratch (batch x (N+1) x ocp_pstride elements of the instantiation's precision) and the
+    // shared-LDS offsets of the polytope matrix, polytope rhs and box bounds (-1: not shared).
+    // The stage-cost table H is then read from global (L2) instead of LDS.
+    void* Pg;
+    int sh_F, sh_hp, sh_bnd;
 };
 
 bool ocp_supported(int nx, int nu, int np);
 int ocp_rpl_for(int mp);
 int ocp_bpl_for(int N, int nx, int nu);
 int ocp_hand_floats(int N, int nx, int nu, int np, int mp);
-int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad, bool fpi);
+int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad, bool fpi, bool lng, bool hpsh,
+                         bool bndsh);
+int ocp_pstride(int ns);
 hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 // fp32 instantiation (bqp_ocp_f32.hip): LDS element count per instance (floats) and launch
-int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad, bool fpi);
+int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad, bool fpi, bool lng,
+                             bool hpsh, bool bndsh);
 hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,

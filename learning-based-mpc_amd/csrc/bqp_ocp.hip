@@ -51,6 +51,13 @@ namespace dp {
 #define BQP_CAT(a, b) BQP_CAT2(a, b)
 
 #define WAVE 64
+// the long-horizon LDS layout (QpLds lng) is used by the fp64 instantiation only: the fp32 one
+// already fits two long-horizon instances per workgroup in the plain layout
+#ifdef BQP_F32
+#define BQP_LNG_OK 0
+#else
+#define BQP_LNG_OK 1
+#endif
 #ifdef BQP_F32
 #define PIV_FLOOR 1e-7
 #else
@@ -139,12 +146,19 @@ enum : int {
 struct QpLds {
     int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, bw, qu, fv, dsv, duv, dsc, duc, Dx, FD,
         blam, ebox, bnd, gpp, gpe, prp, hp, xch, Fi, total;
-    // fpi: the instance carries its own polytope matrix (bqp_ocp_data.sFp != 0), NV x mpad
-    __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false) {
+    // fpi: the instance carries its own polytope matrix (bqp_ocp_data.sFp != 0), NV x mpad.
+    // lng: long-horizon layout (N + 1 > 64, two instances per workgroup at fp64 N = 100): the
+    // Riccati P_k live in global scratch (an LDS ring of two stages feeds the recursion), the
+    // forward drift f_k shares the qhat_k slot, box multipliers and right-hand-side terms are
+    // stored per box variable ([upper] - [lower]), the predictor products dt*dlam of the
+    // polytope rows stay in the row wave's registers, and the polytope right-hand side and box
+    // bounds sit in the shared tables when the batch shares them (hpsh, bndsh).
+    __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false,
+                                          bool lng = false, bool hpsh = false, bool bndsh = false) {
         const int NS = NX + NP, NV = NS + NU, NB = NX + NU;
         QpLds o;
         int c = 0;
-        o.P = c;      c += (N + 1) * pk_stride(NS);  // Riccati P_k (packed)
+        o.P = c;      c += (lng ? 2 : N + 1) * pk_stride(NS);  // Riccati P_k (packed; lng: ring)
         o.K = c;      c += N * NU * NS;              // feedback K_k (row-major NU x NS)
         o.Lr = c;     c += N * NU * NU;              // factor of Rhat_k (nu = 1: its reciprocal)
         o.L0 = c;     c += NP * NP;                  // factor of P_0[theta, theta]
@@ -159,20 +173,24 @@ struct QpLds {
         o.wv = c;     c += (N + 1) * NS;             // cw_k = Phi_k' P_{k+1} re_k (prep_iter)
         o.bw = c;     c += (N + 1) * NU;             // Bbar' P_{k+1} re_k
         o.qu = c;     c += (N + 1) * NU;             // u right-hand side
-        o.fv = c;     c += (N + 1) * NS;             // forward-sweep drift f_k
+        if (lng) {
+            o.fv = o.qt_xpi;                         // f_k written after the backward sweep
+        } else {
+            o.fv = c; c += (N + 1) * NS;             // forward-sweep drift f_k
+        }
         o.dsv = c;    c += (N + 1) * NS;             // predictor direction (s)
         o.duv = c;    c += (N + 1) * NU;             //                     (u)
         o.dsc = c;    c += (N + 1) * NS;             // corrector direction (s)
         o.duc = c;    c += (N + 1) * NU;             //                     (u)
         o.Dx = c;     c += (N + 1) * NV;             // box diagonal of stage k (internal order, theta 0)
         o.FD = c;     c += NV * NV;                  // polytope F'DF
-        o.blam = c;   c += (N + 1) * NB * 2;         // box multipliers [upper, lower] (0 if absent)
-        o.ebox = c;   c += (N + 1) * NB * 2;         // box right-hand-side terms [upper, lower]
-        o.bnd = c;    c += (N + 1) * NB * 2;         // box bounds [upper, lower]
+        o.blam = c;   c += (N + 1) * NB * (lng ? 1 : 2);   // box multipliers [upper, lower] (0 if absent)
+        o.ebox = c;   c += (N + 1) * NB * (lng ? 1 : 2);   // box right-hand-side terms [upper, lower]
+        o.bnd = c;    c += bndsh ? 0 : (N + 1) * NB * 2;   // box bounds [upper, lower]
         o.gpp = c;    c += NV;                       // Fp' lam
         o.gpe = c;    c += NV;                       // Fp' e
-        o.prp = c;    c += mpad;                     // predictor dt*dlam of the polytope rows
-        o.hp = c;     c += mpad;                     // polytope right-hand side
+        o.prp = c;    c += lng ? 0 : mpad;           // predictor dt*dlam of the polytope rows
+        o.hp = c;     c += hpsh ? 0 : mpad;          // polytope right-hand side
         o.xch = c;    c += X_NXCH;
         o.Fi = c;     c += fpi ? NV * mpad : 0;      // per-instance polytope (column-major)
         o.total = (c + 1) & ~1;
@@ -254,6 +272,13 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     const int N = a.N, kp = a.kp, hstride = a.hstride;
     real* X = W + L.xch;
     STAMP_DECL;
+    constexpr bool LNG = BQP_LNG_OK && SPL == 2;     // long-horizon layout (QpLds lng)
+    // stage cost of stage k: the shared LDS table, or (long horizons) the prepared table in
+    // global memory (L2-resident, read-only); a stage pointer per use, as the address
+    // arithmetic of the short-horizon kernels is register-critical
+#define BQP_HK(k) const real* Hk = Hs + (k) * hstride; const double* Hkg = a.H + (int64_t)(k) * hstride
+#define BQP_HV(idx) (LNG ? (real)Hkg[idx] : Hk[idx])
+    real* Pgl = LNG ? (real*)a.Pg + (int64_t)inst * (N + 1) * pk_stride(NS) : nullptr;
 
     // ---------------- per-instance model -> LDS (Abar row-major, Bbar) ---------------------
     {
@@ -323,7 +348,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k > N) continue;
-            const real* Hk = Hs + k * hstride;
+            BQP_HK(k);
             real v[NV];
 #pragma unroll
             for (int i = 0; i < NS; ++i) v[i] = s[j][i];
@@ -334,7 +359,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             for (int i = 0; i < NV; ++i) {
                 real acc = gterm(k, i);
 #pragma unroll
-                for (int c = 0; c < NV; ++c) acc += Hk[i * NV + c] * v[c];
+                for (int c = 0; c < NV; ++c) acc += BQP_HV(i * NV + c) * v[c];
                 gv[i] = acc;
                 gs = fmax(gs, fabs(acc));
             }
@@ -393,13 +418,21 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             for (int i = 0; i < NU; ++i) ru[i] = W[L.ru + k * NU + i];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                r[i] += W[L.blam + (k * NB + i) * 2];
-                r[i] -= W[L.blam + (k * NB + i) * 2 + 1];
+                if constexpr (LNG) {
+                    r[i] += W[L.blam + k * NB + i];
+                } else {
+                    r[i] += W[L.blam + (k * NB + i) * 2];
+                    r[i] -= W[L.blam + (k * NB + i) * 2 + 1];
+                }
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
-                ru[i] += W[L.blam + (k * NB + NX + i) * 2];
-                ru[i] -= W[L.blam + (k * NB + NX + i) * 2 + 1];
+                if constexpr (LNG) {
+                    ru[i] += W[L.blam + k * NB + NX + i];
+                } else {
+                    ru[i] += W[L.blam + (k * NB + NX + i) * 2];
+                    ru[i] -= W[L.blam + (k * NB + NX + i) * 2 + 1];
+                }
             }
             if (k == kp) {
 #pragma unroll
@@ -490,10 +523,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // operands are prefetched one stage ahead and combined as (H + D) + FD
     struct HRaw { real h[VPL], d[VPL]; };
     auto load_h = [&](int k, HRaw& o) __attribute__((always_inline)) {
-        const real* Hk = Hs + k * hstride;
+        BQP_HK(k);
 #pragma unroll
         for (int t = 0; t < VPL; ++t) {
-            o.h[t] = Hk[vr[t] * NV + vc[t]];
+            o.h[t] = BQP_HV(vr[t] * NV + vc[t]);
             o.d[t] = W[L.Dx + k * NV + vr[t]];
         }
     };
@@ -505,7 +538,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     real pu[PST];
     auto read_p = [&](int k) __attribute__((always_inline)) {
         wave_sync();
-        const real2* src = reinterpret_cast<const real2*>(W + L.P + k * PST);
+        const real2* src = reinterpret_cast<const real2*>(W + L.P + (LNG ? (k & 1) : k) * PST);
 #pragma unroll
         for (int q = 0; q < PST / 2; ++q) {
             const real2 t2 = src[q];
@@ -520,13 +553,15 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             // P_N = Ht_N(s, s)
             load_h(N, raw);
             const real v0 = ht(N, raw, 0);
-            if (fquad && fql == 0) W[L.P + N * PST + fq] = v0;
+            if (fquad && fql == 0) {
+                W[L.P + (LNG ? (N & 1) : N) * PST + fq] = v0;
+                if constexpr (LNG) Pgl[N * PST + fq] = v0;
+            }
         }
         read_p(N);
         bool ok = true;
-        load_h(N - 1, raw);
-        for (int k = N - 1; k >= 0; --k) {
-            if (k > 0) load_h(k - 1, nxt);
+        // one stage of the recursion: P_k from P_{k+1} (in pu) and the stage's raw operands
+        auto fstage = [&](int k, const HRaw& raw) __attribute__((always_inline)) {
             real mv[VPL];
 #pragma unroll
             for (int t = 0; t < VPL; ++t) {
@@ -584,7 +619,8 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                 for (int x = 0; x < NU; ++x) Kc[x] = -y[x];
             }
             if (fquad && fql == 0) {
-                W[L.P + k * PST + fq] = pv;
+                W[L.P + (LNG ? (k & 1) : k) * PST + fq] = pv;
+                if constexpr (LNG) Pgl[k * PST + fq] = pv;   // the whole table for the solves
                 if (ie == je) {
 #pragma unroll
                     for (int x = 0; x < NU; ++x) W[L.K + k * NU * NS + x * NS + je] = Kc[x];
@@ -595,7 +631,30 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                 }
             }
             read_p(k);
-            raw = nxt;
+        };
+        if constexpr (LNG) {
+            // long horizons read H from global (L2): its operands are fetched two stages
+            // ahead, three register sets in rotation
+            HRaw r0, r1, r2;
+            load_h(N - 1, r0);
+            if (N >= 2) load_h(N - 2, r1);
+            for (int k = N - 1; k >= 0; k -= 3) {
+                if (k >= 2) load_h(k - 2, r2);
+                fstage(k, r0);
+                if (k < 1) break;
+                if (k >= 3) load_h(k - 3, r0);
+                fstage(k - 1, r1);
+                if (k < 2) break;
+                if (k >= 4) load_h(k - 4, r1);
+                fstage(k - 2, r2);
+            }
+        } else {
+            load_h(N - 1, raw);
+            for (int k = N - 1; k >= 0; --k) {
+                if (k > 0) load_h(k - 1, nxt);
+                fstage(k, raw);
+                raw = nxt;
+            }
         }
         // factor of the theta block of P_0 (np = 1: its reciprocal)
         real Pt[NP][NP], L0[NP][NP];
@@ -615,8 +674,22 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
                 for (int y = 0; y < NP; ++y) W[L.L0 + x * NP + y] = L0[x][y];
         }
+        // long horizons: the global P_k stores complete before the solves read them (the
+        // reads are agent-scope, past the L1)
+        if constexpr (LNG) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         wave_sync();
         return ok;
+    };
+    // packed P_k for the per-stage passes (prep_iter, update_stage): LDS or global scratch
+    auto load_pk = [&](int k, real* pk) __attribute__((always_inline)) {
+        if constexpr (LNG) {
+            const real* src = Pgl + k * PST;
+#pragma unroll
+            for (int e = 0; e < NPK; ++e) pk[e] = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+#pragma unroll
+            for (int e = 0; e < NPK; ++e) pk[e] = W[L.P + k * PST + e];
+        }
     };
 
     // ======================= once per factorisation ========================================
@@ -629,7 +702,9 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
             if (k < N) {
+                real Pn_[LNG ? PST : 1];
                 const real* Pn = W + L.P + (k + 1) * PST;
+                if constexpr (LNG) { load_pk(k + 1, Pn_); Pn = Pn_; }
                 const real* Kk = W + L.K + k * NU * NS;
                 real rek[NS], wk[NS];
 #pragma unroll
@@ -692,15 +767,23 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 real e = 0.0;
-                e += W[L.ebox + (kk * NB + i) * 2];
-                e -= W[L.ebox + (kk * NB + i) * 2 + 1];
+                if constexpr (LNG) {
+                    e += W[L.ebox + kk * NB + i];
+                } else {
+                    e += W[L.ebox + (kk * NB + i) * 2];
+                    e -= W[L.ebox + (kk * NB + i) * 2 + 1];
+                }
                 qs[j][i] += e;
             }
 #pragma unroll
             for (int i = 0; i < NU; ++i) {
                 real e = W[L.ru + kk * NU + i];
-                e += W[L.ebox + (kk * NB + NX + i) * 2];
-                e -= W[L.ebox + (kk * NB + NX + i) * 2 + 1];
+                if constexpr (LNG) {
+                    e += W[L.ebox + kk * NB + NX + i];
+                } else {
+                    e += W[L.ebox + (kk * NB + NX + i) * 2];
+                    e -= W[L.ebox + (kk * NB + NX + i) * 2 + 1];
+                }
                 qu[j][i] = e;
             }
             if (k == kp) {
@@ -886,7 +969,9 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
             for (int i = 0; i < NS; ++i) dsk[i] = W[ids + k * NS + i];
             if (k >= 1) {
+                real Pk_[LNG ? PST : 1];
                 const real* Pk = W + L.P + k * PST;
+                if constexpr (LNG) { load_pk(k, Pk_); Pk = Pk_; }
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     real v = W[L.pv + k * NS + i];
@@ -1045,7 +1130,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
             for (int i = 0; i < NP; ++i) a.theta[(int64_t)inst * NP + i] = s[j][NX + i];
         }
-        const real* Hk = Hs + k * hstride;
+        BQP_HK(k);
         real v[NV];
 #pragma unroll
         for (int i = 0; i < NS; ++i) v[i] = s[j][i];
@@ -1055,7 +1140,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         for (int i = 0; i < NV; ++i) {
             real hv = 0.0;
 #pragma unroll
-            for (int c = 0; c < NV; ++c) hv += Hk[i * NV + c] * v[c];
+            for (int c = 0; c < NV; ++c) hv += BQP_HV(i * NV + c) * v[c];
             fv += v[i] * (0.5 * hv + gterm(k, i));
         }
         if (a.pi_out && k >= 1) {
@@ -1076,12 +1161,15 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     }
 }
 
+#undef BQP_HK
+#undef BQP_HV
+
 // ==========================================================================================
 // row wave
 // ==========================================================================================
 template <int NX, int NU, int NP, int BPL, int RPL>
 __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
-                                         const real* Fs, int lane, int inst) {
+                                         const real* Fs, const real* Sh, int lane, int inst) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     constexpr int NB = NX + NU;          // box slots per stage: x then u, each [upper, lower]
@@ -1089,6 +1177,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     constexpr int mpad = RPL * WAVE;     // polytope table stride (host sets a.mpad to the same)
     real* X = W + L.xch;
     STAMP_DECL;
+    constexpr bool LNG = BQP_LNG_OK && BPL >= 16;    // long-horizon layout (QpLds lng)
+    const bool bndsh = LNG && a.sh_bnd >= 0;         // box bounds in the shared tables
+    const real* bndp = bndsh ? Sh + a.sh_bnd : W + L.bnd;
 
     // ---------------- box rows over all stages, spread over every lane of the wave: bounds to
     //                  LDS, presence mask.  Box variable vi = k NB + sl (stage k, slot sl: x then
@@ -1122,7 +1213,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 if (k < N && ub_) bd = ub_[(int64_t)inst * a.sub + (int64_t)k * NU + (sl - NX)];
             }
             if (isfinite(bd)) { bmsk |= 1u << b; bsl = fmax(bsl, fabs(bd)); }
-            W[L.bnd + r] = bd;
+            if (!bndsh) W[L.bnd + r] = bd;
         }
     }
     mcount += __builtin_popcount(bmsk);
@@ -1136,8 +1227,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     auto bcode = [&](int b) __attribute__((always_inline)) -> int { return (int)((bpk[b >> 1] >> (16 * (b & 1))) & 0xffffu); };
     auto binrange = [&](int b) __attribute__((always_inline)) -> bool { return (binr >> b) & 1u; };
     // polytope rows l, l+64, ...
-    real* hpi = W + L.hp;
-    {
+    const bool hpsh = LNG && a.sh_hp >= 0;           // polytope rhs in the shared tables
+    real* hpi = hpsh ? const_cast<real*>(Sh) + a.sh_hp : W + L.hp;
+    if (!hpsh) {
         const double* hg = a.hp + (int64_t)inst * a.shp;
         for (int r = lane; r < mp; r += WAVE) hpi[r] = hg[r];
     }
@@ -1167,6 +1259,11 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     // residuals are re-formed from the LDS stage vector and bounds when needed)
     real tx[BPL], lx[BPL];
     real tp[RPL], lp[RPL], rp[RPL];
+    real prr[LNG ? RPL : 1];             // long horizons: predictor dt*dlam of the polytope rows
+    auto prp_get = [&](int q, int r) __attribute__((always_inline)) -> real {
+        if constexpr (LNG) return prr[q];
+        else return W[L.prp + r];
+    };
 #pragma unroll
     for (int b = 0; b < BPL; ++b) { tx[b] = 1.0; lx[b] = 1.0; }
 #pragma unroll
@@ -1180,7 +1277,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         for (int pv = 0; pv < BPL / 2; ++pv) {
             ROW_FENCE(pv);
             // D of the variable: upper then lower row (both in this lane)
-            real d = 0.0;
+            real d = 0.0, blv = 0.0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int b = 2 * pv + h;
@@ -1188,7 +1285,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                     d += lx[b] * frcp(tx[b]);
                     cs += tx[b] * lx[b];
                 }
-                if (binrange(b)) W[L.blam + brow(b)] = bpres(b) ? lx[b] : 0.0;
+                if constexpr (LNG) {
+                    if (bpres(b)) blv += h ? -lx[b] : lx[b];
+                } else {
+                    if (binrange(b)) W[L.blam + brow(b)] = bpres(b) ? lx[b] : 0.0;
+                }
+            }
+            if constexpr (LNG) {
+                if (binrange(2 * pv)) W[L.blam + lane + WAVE * pv] = blv;   // [upper] - [lower]
             }
             if (binrange(2 * pv)) {
                 const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
@@ -1259,7 +1363,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     };
     auto box_res = [&](int b) __attribute__((always_inline)) -> real {
         const real v = bvar(b, L.xs, L.xu);
-        const real bd = W[L.bnd + brow(b)];
+        const real bd = bndp[brow(b)];
         return (bcode(b) & 1) == 0 ? v + tx[b] - bd : -v + tx[b] + bd;
     };
     // ---- row residuals of the current iterate (box: +-v + t -+ b; polytope: Fp v + t - hp) ----
@@ -1302,6 +1406,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     // ---- right-hand-side terms (lam o ri - rc)/t: box [upper, lower] per stage, Fp'e ----
     auto rhs_terms = [&](bool corr, real smu) __attribute__((always_inline)) {
+        real eacc = 0.0;
 #pragma unroll
         for (int b = 0; b < BPL; ++b) {
             ROW_FENCE(b);
@@ -1311,7 +1416,12 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 const real pr = corr ? box_pred_prod(b) : 0.0;
                 e = (lx[b] * box_res(b) - rcv(tx[b], lx[b], pr, corr, smu)) * frcp(tx[b]);
             }
-            W[L.ebox + brow(b)] = e;
+            if constexpr (LNG) {
+                if ((b & 1) == 0) eacc = e;
+                else W[L.ebox + lane + WAVE * (b >> 1)] = eacc - e;   // [upper] - [lower]
+            } else {
+                W[L.ebox + brow(b)] = e;
+            }
         }
         real gpe[NV];
 #pragma unroll
@@ -1321,7 +1431,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r < mp) {
-                const real pr = corr ? W[L.prp + r] : 0.0;
+                const real pr = corr ? prp_get(q, r) : 0.0;
                 const real e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * frcp(tp[q]);
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpe[c] += Fs[c * mpad + r] * e;
@@ -1361,7 +1471,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             ROW_FENCE(q);
             const int r = lane + WAVE * q;
             if (r >= mp) continue;
-            const real pr = corr ? W[L.prp + r] : 0.0;
+            const real pr = corr ? prp_get(q, r) : 0.0;
             const real rc = rcv(tp[q], lp[q], pr, corr, smu);
             const real fd = fdot(r, dvp);
             const real dt = -rp[q] - fd;
@@ -1388,7 +1498,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     //      S0 = sum t lam (X_CS) and S2 = sum dt dlam: the sum no longer needs the step length,
     //      and the pass returns the lane partials of max(-dt/t, -dlam/lam) and S2 ----
     auto pred_pass = [&](real& rmx, real (&gpe0)[NV], real (&gpi)[NV]) __attribute__((always_inline)) -> real {
-        real rm = 0.0, s2 = 0.0;
+        real rm = 0.0, s2 = 0.0, eacc = 0.0;
 #pragma unroll
         for (int b = 0; b < BPL; ++b) {
             ROW_FENCE(b);
@@ -1406,7 +1516,12 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 s2 += pr;
                 e0 = (l * box_res(b) - (rc + pr)) * it;
             }
-            W[L.ebox + brow(b)] = e0;
+            if constexpr (LNG) {
+                if ((b & 1) == 0) eacc = e0;
+                else W[L.ebox + lane + WAVE * (b >> 1)] = eacc - e0;
+            } else {
+                W[L.ebox + brow(b)] = e0;
+            }
         }
 #pragma unroll
         for (int c = 0; c < NV; ++c) { gpe0[c] = 0.0; gpi[c] = 0.0; }
@@ -1432,7 +1547,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             rm = fmax(rm, -dl * frcp(l));
             const real pr = dt * dl;
             s2 += pr;
-            W[L.prp + r] = pr;
+            if constexpr (LNG) prr[q] = pr;
+            else W[L.prp + r] = pr;
             const real e0 = (l * rp[q] - (rc + pr)) * it;
 #pragma unroll
             for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }
@@ -1469,7 +1585,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 #pragma unroll
         for (int pv = 0; pv < BPL / 2; ++pv) {
             ROW_FENCE(pv);
-            real d = 0.0;
+            real d = 0.0, blv = 0.0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int b = 2 * pv + h;
@@ -1477,7 +1593,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                     d += lx[b] * frcp(tx[b]);
                     cs += tx[b] * lx[b];
                 }
-                if (binrange(b)) W[L.blam + brow(b)] = bpres(b) ? lx[b] : 0.0;
+                if constexpr (LNG) {
+                    if (bpres(b)) blv += h ? -lx[b] : lx[b];
+                } else {
+                    if (binrange(b)) W[L.blam + brow(b)] = bpres(b) ? lx[b] : 0.0;
+                }
+            }
+            if constexpr (LNG) {
+                if (binrange(2 * pv)) W[L.blam + lane + WAVE * pv] = blv;   // [upper] - [lower]
             }
             if (binrange(2 * pv)) {
                 const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
@@ -1504,7 +1627,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 real fd = 0.0;
 #pragma unroll
                 for (int c = 0; c < NV; ++c) fd += f[c] * dvp[c];
-                const real rc = rcv(tp[q], lp[q], W[L.prp + r], true, smu);
+                const real rc = rcv(tp[q], lp[q], prp_get(q, r), true, smu);
                 const real dt = -rp[q] - fd;
                 const real dl = (-rc - lp[q] * dt) * frcp(tp[q]);
                 rp[q] += al * (fd + dt);
@@ -1553,9 +1676,19 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     };
 
     auto rhs_corr_finish = [&](real smu, real tot) __attribute__((always_inline)) {
+        if constexpr (LNG) {
 #pragma unroll
-        for (int b = 0; b < BPL; ++b)
-            if (bpres(b)) W[L.ebox + brow(b)] += smu * frcp(tx[b]);
+            for (int pv = 0; pv < BPL / 2; ++pv) {
+                real add = 0.0;
+                if (bpres(2 * pv)) add += smu * frcp(tx[2 * pv]);
+                if (bpres(2 * pv + 1)) add -= smu * frcp(tx[2 * pv + 1]);
+                if (binrange(2 * pv)) W[L.ebox + lane + WAVE * pv] += add;
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < BPL; ++b)
+                if (bpres(b)) W[L.ebox + brow(b)] += smu * frcp(tx[b]);
+        }
         // tot (from the joint reduction): lane 2c = Fp'e0 (c), lane 2c+1 = Fp'(1/t) (c)
         const real other = dpp_mov<0xB1, 0xf>(real(0), tot);
         if (lane < 2 * NV && (lane & 1) == 0) W[L.gpe + lane / 2] = tot + smu * other;
@@ -1742,12 +1875,33 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
             if (!__syncthreads_or(need)) return;
         }
     }
-    real* Hs = lds;
+    constexpr bool LNG = BQP_LNG_OK && SPL == 2;  // long-horizon layout (QpLds lng)
     const bool fpi = a.Fp_inst != nullptr;   // per-instance polytope: in the instance's LDS slot
-    real* Fs = lds + (N + 1) * a.hstride;
-    for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
+    // shared tables: H (short horizons; long ones read it from global), Fp, and for long horizons
+    // the polytope rhs and box bounds when the batch shares them
+    real* Hs = lds;
+    real* Fs = lds + a.sh_F;
+    if (!LNG)
+        for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
     if (!fpi)
         for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
+    if (LNG && a.sh_hp >= 0)
+        for (int r = threadIdx.x; r < a.mp; r += blockDim.x) lds[a.sh_hp + r] = a.hp[r];
+    if (LNG && a.sh_bnd >= 0) {
+        constexpr int NB = NX + NU;
+        for (int r = threadIdx.x; r < (N + 1) * NB * 2; r += blockDim.x) {
+            const int vi = r >> 1, h = r & 1, k = vi / NB, sl = vi - k * NB;
+            double bd = h ? -INFINITY : INFINITY;
+            if (sl < NX) {
+                const double* xb = h ? a.xlb : a.xub;
+                if (k > 0 && xb) bd = xb[(int64_t)k * NX + sl];
+            } else {
+                const double* ub_ = h ? a.ulb : a.uub;
+                if (k < N && ub_) bd = ub_[(int64_t)k * NU + (sl - NX)];
+            }
+            lds[a.sh_bnd + r] = (real)bd;
+        }
+    }
     __syncthreads();
     const bool rowwave = wid >= qpb;
     const int slot = rowwave ? wid - qpb : wid;
@@ -1756,7 +1910,8 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     if (SPL == 2 && a.redo_flag &&
         !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
         return;                        // mixed mode, cold retry launch: nothing to redo here
-    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi);
+    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, LNG && a.sh_hp >= 0,
+                                LNG && a.sh_bnd >= 0);
     real* W = lds + a.shared_doubles + slot * L.total;
     if (fpi && rowwave) {
         // the instance's polytope, external column-major [x; u; theta] (n_poly rows) -> internal
@@ -1778,7 +1933,7 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     if (!rowwave)
         stage_wave<NX, NU, NP, SPL>(a, W, L, Hs, lane, inst);
     else
-        row_wave<NX, NU, NP, BPL, RPL>(a, W, L, Fs, lane, inst);
+        row_wave<NX, NU, NP, BPL, RPL>(a, W, L, Fs, lds, lane, inst);
 }
 
 }  // namespace dp / sp
@@ -1880,6 +2035,8 @@ int ocp_bpl_for(int N, int nx, int nu) {
     return nbr <= 16 * WAVE ? 16 : (nbr <= 20 * WAVE ? 20 : -1);
 }
 
+int ocp_pstride(int ns) { return dp::pk_stride(ns); }
+
 int ocp_hand_floats(int N, int nx, int nu, int np, int mp) {
     const int bpl = ocp_bpl_for(N, nx, nu), rpl = ocp_rpl_for(mp > 1 ? mp : 1);
     if (bpl < 0 || rpl < 0) return -1;
@@ -1888,11 +2045,12 @@ int ocp_hand_floats(int N, int nx, int nu, int np, int mp) {
 #endif
 
 // LDS elements (of the instantiation's precision) per instance
-int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad, bool fpi) {
+int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad, bool fpi,
+                                          bool lng, bool hpsh, bool bndsh) {
 #ifdef BQP_F32
-    return sp::QpLds::make(N, nx, nu, np, mpad, fpi).total;
+    return sp::QpLds::make(N, nx, nu, np, mpad, fpi, lng, hpsh, bndsh).total;
 #else
-    return dp::QpLds::make(N, nx, nu, np, mpad, fpi).total;
+    return dp::QpLds::make(N, nx, nu, np, mpad, fpi, lng, hpsh, bndsh).total;
 #endif
 }
 
@@ -1902,7 +2060,9 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
     const size_t lds = sizeof(real) * ((size_t)a.shared_doubles +
                                        (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad,
-                                                                                      a.Fp_inst != nullptr));
+                                                                                      a.Fp_inst != nullptr, BQP_LNG_OK && spl == 2,
+                                                                                      BQP_LNG_OK && spl == 2 && a.sh_hp >= 0,
+                                                                                      BQP_LNG_OK && spl == 2 && a.sh_bnd >= 0));
     if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st);
 #ifndef BQP_ISA_ONLY_MG10
     if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st);

@@ -181,10 +181,11 @@ def test_large_batch_properties(mg, term_set, handle):
 
 
 def test_long_horizon_box_layouts(mg, term_set, handle):
-    """Horizons past one stage per lane: N=80 (16 box rows per lane, two stages per stage-wave
-    lane) fp64 iterates vs the C restatement; N=120 (20 box rows per lane) exceeds the fp64 LDS
-    budget of one instance (clean BQP_E_UNSUPPORTED) and runs in the fp32 instantiation, checked
-    against the fp64 C restatement to the fp32 accuracy of tests/test_gpu_fp32.py."""
+    """Horizons past one stage per lane (the long-horizon LDS layout: Riccati tables in global
+    scratch, shared bounds / polytope rhs): N=80 (16 box rows per lane, two stages per
+    stage-wave lane) and N=120 (20 box rows per lane; fits one fp64 instance since that layout)
+    fp64 iterates vs the C restatement; N=120 in the fp32 instantiation to the fp32 accuracy of
+    tests/test_gpu_fp32.py; N=127 (the longest compiled horizon) in the mixed mode."""
     import bqp
     from bqp._lib import BqpError
     from oracle import cpu_ref, qp_forms
@@ -201,10 +202,18 @@ def test_long_horizon_box_layouts(mg, term_set, handle):
     assert np.abs(r.x - c['x']).max() < TOL_ITER
     assert np.abs(r.u - c['u']).max() < TOL_ITER
     t120 = tl(120)
-    with pytest.raises(BqpError, match='unsupported'):
-        t120.solve(X, handle=handle)
-    r32 = t120.solve(X, handle=handle, precision=1)
+    r = t120.solve(X, handle=handle)
     c = cpu_ref.solve(qp_forms.dms_ocp(mg, 120, *term_set), X - mg['x_wp'].ravel())
+    assert (r.exitflag == 1).all() and (c['exitflag'] == 1).all()
+    assert np.abs(r.x - c['x']).max() < TOL_ITER
+    assert np.abs(r.u - c['u']).max() < TOL_ITER
+    r32 = t120.solve(X, handle=handle, precision=1)
     ok = r32.exitflag == 1
     assert ok.mean() >= 0.75
     assert np.abs(r32.u[ok, 0] - c['u'][ok, 0]).max() < 1e-4
+    rm = tl(127).solve(X, handle=handle, precision=2)
+    c = cpu_ref.solve(qp_forms.dms_ocp(mg, 127, *term_set), X - mg['x_wp'].ravel())
+    assert (rm.exitflag == 1).all()
+    assert np.abs(rm.u[:, 0] - c['u'][:, 0]).max() < 1e-8
+    with pytest.raises(BqpError, match='unsupported'):
+        tl(128).solve(X, handle=handle)

@@ -1,4 +1,4 @@
-"""Per-launch HBM bytes of the solve kernel from rocprofv3 PMC passes (tools/gpu_session.sh).
+"""Per-launch HBM bytes of the solve kernel from rocprofv3 PMC passes (tools/gpu_prof.sh).
 
     python tools/pmc_summary.py gpurun_out/TAG profiles/rNN_TAG [--kernel ocp_ipm_kernel]
 

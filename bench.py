@@ -404,6 +404,11 @@ def main():
     if rank == 0:
         value = wl['total'] / (elapsed / args.steps) if wl['scaling'] == 'strong' \
             else world * B * args.steps / elapsed
+        if args.config == 'C4' and 'converged_frac_all_ranks' in check:
+            # C4: only the converged instances count as QP-steps; the primal-infeasible models
+            # (exitflag -2, found in fewer iterations) are reported in `check`, not in `value`
+            check['value_all_instances'] = round(value, 1)
+            value *= check['converged_frac_all_ranks']
         ms_per_step = 1e3 * elapsed / args.steps
         roof, cpu = None, None
         if not args.dry_run:

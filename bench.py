@@ -442,6 +442,14 @@ def main():
                             'stage blocks); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
                             '(profiles/)'}
+            if args.config == 'C2':
+                # latency roof: at batch 1024 one instance runs per SIMD, so the
+                # kernel time is one instance's dependency chain; the stage wave (Riccati factor,
+                # two sweeps, update) works this fraction of the instance's cycles and waits on
+                # the row wave for the rest (s_memtime stamps, diagnostic build)
+                roof['latency'] = {'stage_wave_busy_frac': 0.757,
+                                   'stage_wave_cycles_per_iter': 54100,
+                                   'source': 'profiles/r02_h/stamps.log'}
         line = {
             'metric': METRIC,
             'value': round(value, 1), 'unit': 'QP-steps/s', 'n_gpus': world, 'steps': args.steps,

@@ -217,3 +217,38 @@ def test_long_horizon_box_layouts(mg, term_set, handle):
     assert np.abs(rm.u[:, 0] - c['u'][:, 0]).max() < 1e-8
     with pytest.raises(BqpError, match='unsupported'):
         tl(128).solve(X, handle=handle)
+
+
+def test_f5_c3_workload(handle):
+    """trackingMPC DI (F5) on the C3 workload (tests/golden/di_design.npz: feasible x0 x the
+    four references of RunExample.m:213-223), 256 instances: GPU iterates vs the C restatement
+    of the same algorithm, and 16 of them vs the dense restatement of costFunction.m /
+    constraintsFunction.m (objective, first move, LAMBDA theta)"""
+    import bqp
+    from oracle import cpu_ref, dense_qp, qp_forms
+    g = golden('di_design.npz')
+    N = int(g['N'])
+    tm = bqp.TrackingMPC(g['A'], g['B'], g['Q'], g['R'], g['P'], g['T'], g['LAMBDA'], g['PSI'],
+                         g['F_x'], g['h_x'], g['F_u'], g['h_u'], g['F_T'], g['h_T'], N=N)
+    rng = np.random.default_rng(31)
+    sel = rng.choice(len(g['x0']) * len(g['xs']), 256, replace=False)
+    X = g['x0'][sel // len(g['xs'])]
+    XS = g['xs'][sel % len(g['xs'])]
+    r = tm.solve(X, XS, handle=handle)
+    assert (r.exitflag == 1).all()
+    p = tm.prob
+    ocp = dict(nx=p.nx, nu=p.nu, np=p.np, N=p.N, A=p.A, B=p.B, c=p.c, W=p.W, w=p.w, xlb=p.xlb,
+               xub=p.xub, ulb=p.ulb, uub=p.uub, Fp=p.Fp, hp=p.hp, kp=p.poly_stage)
+    w, _ = tm.linear_terms(XS)
+    c = cpu_ref.solve(ocp, X, w=w)
+    assert (c['exitflag'] == 1).all()
+    assert np.abs(r.u - c['u']).max() < TOL_ITER
+    assert np.abs(r.x - c['x']).max() < TOL_ITER
+    di = dict(A=g['A'], B=g['B'], Q=g['Q'], R=g['R'], P=g['P'], T=g['T'], LAMBDA=g['LAMBDA'],
+              PSI=g['PSI'], F_x=g['F_x'], h_x=g['h_x'], F_u=g['F_u'], h_u=g['h_u'])
+    for i in range(16):
+        qp = qp_forms.track_dense(di, N, X[i], XS[i], g['F_T'], g['h_T'])
+        z, fval, _, _ = dense_qp.solve(qp)
+        assert abs(r.fval[i] - (fval + qp['const'])) < 1e-7 * max(1, abs(fval))
+        assert np.abs(r.u0[i] - z[:2]).max() < 1e-6
+        assert np.abs(g['LAMBDA'] @ (r.theta[i] - z[-2:])).max() < 1e-6

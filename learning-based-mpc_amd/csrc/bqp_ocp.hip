@@ -960,6 +960,46 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     };
 
     // primal/dual stage update by alpha along (ids, idu); dpi_k = P_k ds_k + p_k
+    // the dual direction dpi_k = P_k ds_k + p_k of the corrector does not depend on the step
+    // length: it is formed while the row wave runs the ratio test (before B5) and parked in the
+    // cw_k slot (dead until the next factorisation); the update after B6 only scales it
+    auto dual_dir = [&](int ids) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N || k < 1) continue;
+            real dsk[NS];
+#pragma unroll
+            for (int i = 0; i < NS; ++i) dsk[i] = W[ids + k * NS + i];
+            real Pk_[LNG ? PST : 1];
+            const real* Pk = W + L.P + k * PST;
+            if constexpr (LNG) { load_pk(k, Pk_); Pk = Pk_; }
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                real v = W[L.pv + k * NS + i];
+#pragma unroll
+                for (int c = 0; c < NS; ++c) v += Pk[pk_idx(NS, i, c)] * dsk[c];
+                W[L.wv + k * NS + i] = v;
+            }
+        }
+    };
+    auto update_stage_dir = [&](real al, int ids, int idu) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < SPL; ++j) {
+            const int k = lane + WAVE * j;
+            if (k > N) continue;
+            if (k >= 1) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) pi[j][i] += al * W[L.wv + k * NS + i];
+            }
+#pragma unroll
+            for (int i = 0; i < NS; ++i) s[j][i] += al * W[ids + k * NS + i];
+            if (k < N) {
+#pragma unroll
+                for (int i = 0; i < NU; ++i) u[j][i] += al * W[idu + k * NU + i];
+            }
+        }
+    };
     auto update_stage = [&](real al, int ids, int idu) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -1083,10 +1123,11 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         solve(L.dsc, L.duc);                              // corrector
         STAMP(7);
         BARRIER();                                        // B5: corrector direction out
+        dual_dir(L.dsc);                                  // overlaps the row wave's ratio test
         BARRIER();                                        // B6: step length ready
         STAMP(8);
         const real al = X[X_ALPHA];
-        update_stage(al, L.dsc, L.duc);
+        update_stage_dir(al, L.dsc, L.duc);
         write_state();
         stage_partials(feasA, gsA);
         STAMP(9);

@@ -414,7 +414,8 @@ def main():
         if not args.dry_run:
             present = len(os.sched_getaffinity(0))
             threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or present
-            cpu, kref_u = cpu_reference(prob, wl['sample'], threads, not args.no_cpu)
+            # the CPU baseline is timed at N=1 only (the multi-GPU lines carry K_ref, not a timing)
+            cpu, kref_u = cpu_reference(prob, wl['sample'], threads, not args.no_cpu and world == 1)
             if cpu is not None:
                 cpu['cores_present'] = present
                 cpu['cores_note'] = ('threads = OMP_NUM_THREADS (the per-GPU CPU share the box '

@@ -62,3 +62,44 @@ def test_per_instance_sets_same_polytope(mg, term_set):
     r0 = lm.solve(X0)
     assert (r.exitflag == 1).all()
     assert np.abs(r.opt_var - r0.opt_var).max() < 1e-8
+
+
+def test_terminal_sets_rebuilt_per_model(di):
+    """per-model terminal sets (bqp.sets, compute_MPIS.m / RunExample.m:77-108 per model): each
+    instance's set is rebuilt from its own state constraints - here tightened by a per-model
+    margin, as a learned-uncertainty bound would tighten them (the sets differ in shape and row
+    count and are padded with 0 <= 1) - and one batched solve takes the per-instance polytopes
+    and right-hand sides; vs the C restatement solving each instance with its own set"""
+    import bqp
+    from bqp import sets
+    from oracle import cpu_ref
+    g = golden('di_design.npz')
+    N = int(g['N'])
+    rng = np.random.default_rng(12)
+    M = 24
+    scale = rng.uniform(0.6, 1.0, M)
+    ts = [sets.tracking_terminal_set(di['A'], di['B'], di['K'], di['LAMBDA'], di['PSI'],
+                                     di['F_x'], scale[i] * di['h_x'], di['F_u'], di['h_u'])
+          for i in range(M)]
+    rows = max(len(h) for _, h in ts)
+    Fp, hp = sets.pack_sets(ts, nx=2, nu=2, rows=rows)
+    assert len({round(float(h.sum()), 9) for _, h in ts}) > 1      # the sets really differ
+    F0 = np.zeros((rows, 4)); F0[:len(g['h_T'])] = g['F_T']
+    h0 = np.ones(rows); h0[:len(g['h_T'])] = g['h_T']
+    tm = bqp.TrackingMPC(di['A'], di['B'], di['Q'], di['R'], di['P'], di['T'], di['LAMBDA'],
+                         di['PSI'], di['F_x'], di['h_x'], di['F_u'], di['h_u'], F0, h0, N=N)
+    X = g['x0'][rng.choice(len(g['x0']), M, replace=False)] * 0.5
+    XS = g['xs'][rng.integers(0, len(g['xs']), M)] * 0.5
+    r = tm.solve(X, XS, Fp=Fp, hp=hp)
+    p = tm.prob
+    w, _ = tm.linear_terms(XS)
+    ok = 0
+    for i in range(M):
+        ocp = dict(nx=2, nu=2, np=2, N=N, A=p.A, B=p.B, c=p.c, W=p.W, w=p.w, xlb=p.xlb,
+                   xub=p.xub, ulb=p.ulb, uub=p.uub, Fp=Fp[i], hp=hp[i], kp=p.poly_stage)
+        c = cpu_ref.solve(ocp, X[i:i + 1], w=w[i:i + 1])
+        assert r.exitflag[i] == c['exitflag'][0], i
+        if c['exitflag'][0] == 1:
+            ok += 1
+            assert np.abs(r.u[i] - c['u'][0]).max() < 1e-8, i
+    assert ok >= M // 2

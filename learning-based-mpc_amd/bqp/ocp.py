@@ -54,10 +54,11 @@ class OcpResult(dict):
     __getattr__ = dict.__getitem__
 
 
-def pack(prob, x0, w=None, hp=None, A=None, B=None, Fp=None):
+def pack(prob, x0, w=None, hp=None, A=None, B=None, Fp=None, W=None):
     """Builds (dims, data, keepalive) for a batch.  x0: (batch, nx); per-instance overrides
     w (batch, N+1, nv), hp (batch, mp), A (batch, nx, nx), B (batch, nx, nu) and the polytope
-    Fp (batch, mp, nv) (same row count and stage as prob's)."""
+    Fp (batch, mp, nv) (same row count and stage as prob's) and the stage costs W (batch, N+1, nv,
+    nv)."""
     x0 = np.ascontiguousarray(np.atleast_2d(x0), dtype=np.float64)
     batch = x0.shape[0]
     keep = [x0]
@@ -70,7 +71,7 @@ def pack(prob, x0, w=None, hp=None, A=None, B=None, Fp=None):
     nx, nu, nv, N, mp = prob.nx, prob.nu, prob.nv, prob.N, prob.mp
     Aa = arr(_cm(prob.A if A is None else A))
     Ba = arr(_cm(prob.B if B is None else B))
-    Wa = arr(_cm(prob.W))
+    Wa = arr(_cm(prob.W if W is None else W))
     wa = arr(prob.w if w is None else w)
     Fa = arr(_cm(prob.Fp if Fp is None else Fp)) if mp else None
     ha = arr(prob.hp if hp is None else hp) if mp else None
@@ -81,19 +82,20 @@ def pack(prob, x0, w=None, hp=None, A=None, B=None, Fp=None):
         A=_lib.ptr(Aa), B=_lib.ptr(Ba), c=_lib.ptr(ca), W=_lib.ptr(Wa), w=_lib.ptr(wa),
         xlb=_lib.ptr(xlb), xub=_lib.ptr(xub), ulb=_lib.ptr(ulb), uub=_lib.ptr(uub),
         Fp=_lib.ptr(Fa), hp=_lib.ptr(ha), x0=_lib.ptr(x0),
-        sA=0 if A is None else nx * nx, sB=0 if B is None else nx * nu, sc=0, sW=0,
+        sA=0 if A is None else nx * nx, sB=0 if B is None else nx * nu, sc=0,
+        sW=0 if W is None else (N + 1) * nv * nv,
         sw=0 if w is None else (N + 1) * nv, sxb=0, sub=0, sFp=0 if Fp is None else mp * nv,
         shp=0 if hp is None else mp, sx0=nx)
     return dims, data, batch, keep
 
 
 def solve_ocp(prob, x0, w=None, hp=None, A=None, B=None, handle=None, want_duals=False, Fp=None,
-              **opts):
+              W=None, **opts):
     """Solve a batch on the GPU.  Returns OcpResult(x (b,N+1,nx), u (b,N,nu), theta (b,np),
     fval, exitflag, iterations, firstorderopt, constrviolation, mu[, pi, lam_x, lam_u, lam_p])."""
     lib = _lib.load()
     h = handle or _default_handle()
-    dims, data, batch, keep = pack(prob, x0, w, hp, A, B, Fp)
+    dims, data, batch, keep = pack(prob, x0, w, hp, A, B, Fp, W)
     N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
     x = np.zeros((batch, N + 1, nx)); u = np.zeros((batch, N, nu)); th = np.zeros((batch, npar))
     fval = np.zeros(batch); flag = np.zeros(batch, np.int32)

@@ -47,6 +47,7 @@ struct bqp_handle_s {
     DevBuf cwork;  // closed-loop simulation buffers
     DevBuf hwork;  // mixed precision: fp32 -> fp64 handoff records
     DevBuf pwork;  // long-horizon layout: global Riccati tables
+    DevBuf wwork;  // per-instance stage-cost tables
     int last_batch = 0;
 };
 
@@ -145,6 +146,7 @@ int bqp_destroy(bqp_handle h) {
         h->cwork.release();
         h->hwork.release();
         h->pwork.release();
+        h->wwork.release();
         if (h->ev0) hipEventDestroy(h->ev0);
         if (h->ev1) hipEventDestroy(h->ev1);
         if (h->stream) hipStreamDestroy(h->stream);
@@ -177,7 +179,8 @@ static int ocp_check(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D) {
     if (d->n_poly > 0 && (!D->Fp || !D->hp)) return BQP_E_ARG;
     if (!bqp::ocp_supported(d->nx, d->nu, d->np)) return BQP_E_UNSUPPORTED;
     if (d->N > 127 || bqp::ocp_rpl_for(std::max(d->n_poly, 1)) < 0) return BQP_E_UNSUPPORTED;
-    if (D->sW != 0) return BQP_E_UNSUPPORTED;                // shared stage costs
+    if (D->sW != 0 && D->sW < (int64_t)(d->N + 1) * (d->nx + d->nu + d->np) * (d->nx + d->nu + d->np))
+        return BQP_E_ARG;                                     // per-instance stage costs overlap
     if (D->sFp != 0 && D->sFp < (int64_t)d->n_poly * (d->nx + d->nu + d->np)) return BQP_E_ARG;
     return BQP_OK;
 }
@@ -222,6 +225,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     const int mpad = 64 * bqp::ocp_rpl_for(std::max(mp, 1));   // = the kernel's RPL * 64
     // per-instance polytope (sFp != 0): each instance's LDS slot holds its own NV x mpad table
     const bool fpi = mp > 0 && D->sFp != 0;
+    const bool hinst = D->sW != 0;        // per-instance stage costs (the instance's H table)
     // long horizons (two stages per lane): H read from global, Riccati tables in global scratch,
     // polytope rhs / box bounds in the shared tables when the batch shares them (QpLds lng)
     // (fp64 instantiation only; the fp32 one keeps the plain layout)
@@ -232,7 +236,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         o.hpsh = o.lng && mp > 0 && D->shp == 0;
         o.bndsh = o.lng && D->sxb == 0 && D->sub == 0;
         const int nbr = (N + 1) * 2 * (nx + nu);
-        int sh = o.lng ? 0 : (N + 1) * hstride;
+        int sh = (o.lng || hinst) ? 0 : (N + 1) * hstride;
         o.sh_F = sh;
         sh += fpi ? 0 : nv * mpad;
         o.sh_hp = o.hpsh ? sh : -1;
@@ -248,8 +252,8 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     auto fit_wpb = [&](bool single, int& wpb) -> bool {
         const Shared& S = single ? L32 : L64;
         const int shared_doubles = S.doubles;
-        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi, false, false, false)
-                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi, S.lng, S.hpsh, S.bndsh);
+        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi, false, false, false, hinst)
+                                    : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi, S.lng, S.hpsh, S.bndsh, hinst);
         const size_t lds_budget = 160 * 1024 / (single ? sizeof(float) : sizeof(double));
         // long horizons (N + 1 > 64, two stages per lane) are compiled for <= 256 threads per
         // workgroup: one wave per SIMD, whose 512 registers hold the doubled stage state
@@ -270,6 +274,12 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     double* Hd = (double*)h->work.p;
     double* Fd = Hd + nH;
     double* Sd = Fd + nF;
+    const double* Hinst = nullptr;
+    if (hinst) {   // per-instance prepared stage-cost tables
+        HIP_TRY(h->wwork.reserve(sizeof(double) * (size_t)batch * nH));
+        HIP_TRY(bqp::launch_ocp_prep_h(D->W, D->sW, batch, nx, nu, np, N, hstride, (double*)h->wwork.p, st));
+        Hinst = (const double*)h->wwork.p;
+    }
     void* Pg = nullptr;
     if (lng) {   // global Riccati tables of the long-horizon layout
         HIP_TRY(h->pwork.reserve(sizeof(double) * (size_t)batch * (N + 1) * bqp::ocp_pstride(nx + np)));
@@ -282,7 +292,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     a.N = N; a.mp = mp; a.kp = d->poly_stage; a.batch = batch; a.wpb = wpb;
     const Shared& LS = f32 ? L32 : L64;
     a.hstride = hstride; a.mpad = mpad; a.shared_doubles = LS.doubles;
-    a.Pg = Pg; a.sh_F = LS.sh_F; a.sh_hp = LS.sh_hp; a.sh_bnd = LS.sh_bnd;
+    a.Pg = Pg; a.sh_F = LS.sh_F; a.sh_hp = LS.sh_hp; a.sh_bnd = LS.sh_bnd; a.H_inst = Hinst;
     a.max_iter = o.max_iter; a.tol_stat = o.tol_stat; a.tol_feas = o.tol_feas;
     a.tol_comp = o.tol_comp; a.tau = o.tau;
     a.H = Hd; a.Fp = Fd;
@@ -825,7 +835,7 @@ static int closed_loop_host(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
         {D->A, span(batch, D->sA, (size_t)nx * nx), nullptr},
         {D->B, span(batch, D->sB, (size_t)nx * nu), nullptr},
         {D->c, D->c ? span(batch, D->sc, nx) : 0, nullptr},
-        {D->W, (size_t)(N + 1) * nv * nv, nullptr},
+        {D->W, span(batch, D->sW, (size_t)(N + 1) * nv * nv), nullptr},
         {D->w, D->w ? span(batch, D->sw, (size_t)(N + 1) * nv) : 0, nullptr},
         {D->xlb, D->xlb ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},
         {D->xub, D->xub ? span(batch, D->sxb, (size_t)(N + 1) * nx) : 0, nullptr},

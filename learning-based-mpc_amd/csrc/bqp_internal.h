@@ -50,6 +50,9 @@ struct OcpKernelArgs {
     // The stage-cost table H is then read from global (L2) instead of LDS.
     void* Pg;
     int sh_F, sh_hp, sh_bnd;
+    // per-instance stage costs (bqp_ocp_data.sW != 0): prepared tables batch x (N+1) x hstride;
+    // short horizons copy the instance's table into its LDS slot, long ones read it from L2
+    const double* H_inst;
 };
 
 bool ocp_supported(int nx, int nu, int np);
@@ -57,16 +60,18 @@ int ocp_rpl_for(int mp);
 int ocp_bpl_for(int N, int nx, int nu);
 int ocp_hand_floats(int N, int nx, int nu, int np, int mp);
 int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad, bool fpi, bool lng, bool hpsh,
-                         bool bndsh);
+                         bool bndsh, bool hinst);
 int ocp_pstride(int ns);
 hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 // fp32 instantiation (bqp_ocp_f32.hip): LDS element count per instance (floats) and launch
 int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad, bool fpi, bool lng,
-                             bool hpsh, bool bndsh);
+                             bool hpsh, bool bndsh, bool hinst);
 hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,
                            hipStream_t st);
+hipError_t launch_ocp_prep_h(const double* W, int64_t sW, int batch, int nx, int nu, int np,
+                             int N, int hstride, double* Hout, hipStream_t st);
 hipError_t launch_ocp_finalize(const double* stats, int batch, void* out, hipStream_t st);
 
 // Dense quadprog kernel arguments.

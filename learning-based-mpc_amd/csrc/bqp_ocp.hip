@@ -145,7 +145,7 @@ enum : int {
 // Per-instance LDS layout (in doubles), sized from N at run time.
 struct QpLds {
     int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, bw, qu, fv, dsv, duv, dsc, duc, Dx, FD,
-        blam, ebox, bnd, gpp, gpe, prp, hp, xch, Fi, total;
+        blam, ebox, bnd, gpp, gpe, prp, hp, xch, Fi, Hi, total;
     // fpi: the instance carries its own polytope matrix (bqp_ocp_data.sFp != 0), NV x mpad.
     // lng: long-horizon layout (N + 1 > 64, two instances per workgroup at fp64 N = 100): the
     // Riccati P_k live in global scratch (an LDS ring of two stages feeds the recursion), the
@@ -153,8 +153,10 @@ struct QpLds {
     // stored per box variable ([upper] - [lower]), the predictor products dt*dlam of the
     // polytope rows stay in the row wave's registers, and the polytope right-hand side and box
     // bounds sit in the shared tables when the batch shares them (hpsh, bndsh).
+    // hinst: per-instance stage-cost table (bqp_ocp_data.sW != 0) in the slot (short horizons)
     __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false,
-                                          bool lng = false, bool hpsh = false, bool bndsh = false) {
+                                          bool lng = false, bool hpsh = false, bool bndsh = false,
+                                          bool hinst = false) {
         const int NS = NX + NP, NV = NS + NU, NB = NX + NU;
         QpLds o;
         int c = 0;
@@ -193,6 +195,7 @@ struct QpLds {
         o.hp = c;     c += hpsh ? 0 : mpad;          // polytope right-hand side
         o.xch = c;    c += X_NXCH;
         o.Fi = c;     c += fpi ? NV * mpad : 0;      // per-instance polytope (column-major)
+        o.Hi = c;     c += (hinst && !lng) ? (N + 1) * (NV * NV + 1) : 0;   // per-instance H table
         o.total = (c + 1) & ~1;
         return o;
     }
@@ -276,9 +279,18 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // stage cost of stage k: the shared LDS table, or (long horizons) the prepared table in
     // global memory (L2-resident, read-only); a stage pointer per use, as the address
     // arithmetic of the short-horizon kernels is register-critical
-#define BQP_HK(k) const real* Hk = Hs + (k) * hstride; const double* Hkg = a.H + (int64_t)(k) * hstride
+#define BQP_HK(k) const real* Hk = Hs + (k) * hstride; const double* Hkg = Hg + (int64_t)(k) * hstride
 #define BQP_HV(idx) (LNG ? (real)Hkg[idx] : Hk[idx])
     real* Pgl = LNG ? (real*)a.Pg + (int64_t)inst * (N + 1) * pk_stride(NS) : nullptr;
+    // per-instance stage costs: the instance's prepared table (global), copied into the LDS slot
+    // on short horizons
+    const double* Hg = a.H_inst ? a.H_inst + (int64_t)inst * (N + 1) * hstride : a.H;
+    if (!LNG && a.H_inst) {
+        real* Hl = W + L.Hi;
+        for (int i = lane; i < (N + 1) * hstride; i += WAVE) Hl[i] = (real)Hg[i];
+        wave_sync();
+        Hs = Hl;
+    }
 
     // ---------------- per-instance model -> LDS (Abar row-major, Bbar) ---------------------
     {
@@ -1922,7 +1934,7 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     // the polytope rhs and box bounds when the batch shares them
     real* Hs = lds;
     real* Fs = lds + a.sh_F;
-    if (!LNG)
+    if (!LNG && !a.H_inst)
         for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
     if (!fpi)
         for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
@@ -1952,7 +1964,7 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
         !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
         return;                        // mixed mode, cold retry launch: nothing to redo here
     const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, LNG && a.sh_hp >= 0,
-                                LNG && a.sh_bnd >= 0);
+                                LNG && a.sh_bnd >= 0, a.H_inst != nullptr);
     real* W = lds + a.shared_doubles + slot * L.total;
     if (fpi && rowwave) {
         // the instance's polytope, external column-major [x; u; theta] (n_poly rows) -> internal
@@ -2087,11 +2099,11 @@ int ocp_hand_floats(int N, int nx, int nu, int np, int mp) {
 
 // LDS elements (of the instantiation's precision) per instance
 int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mpad, bool fpi,
-                                          bool lng, bool hpsh, bool bndsh) {
+                                          bool lng, bool hpsh, bool bndsh, bool hinst) {
 #ifdef BQP_F32
-    return sp::QpLds::make(N, nx, nu, np, mpad, fpi, lng, hpsh, bndsh).total;
+    return sp::QpLds::make(N, nx, nu, np, mpad, fpi, lng, hpsh, bndsh, hinst).total;
 #else
-    return dp::QpLds::make(N, nx, nu, np, mpad, fpi, lng, hpsh, bndsh).total;
+    return dp::QpLds::make(N, nx, nu, np, mpad, fpi, lng, hpsh, bndsh, hinst).total;
 #endif
 }
 
@@ -2103,7 +2115,8 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
                                        (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad,
                                                                                       a.Fp_inst != nullptr, BQP_LNG_OK && spl == 2,
                                                                                       BQP_LNG_OK && spl == 2 && a.sh_hp >= 0,
-                                                                                      BQP_LNG_OK && spl == 2 && a.sh_bnd >= 0));
+                                                                                      BQP_LNG_OK && spl == 2 && a.sh_bnd >= 0,
+                                                                                      a.H_inst != nullptr));
     if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st);
 #ifndef BQP_ISA_ONLY_MG10
     if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/bqp.h"
 #include "bqp_internal.h"
 
@@ -54,6 +56,37 @@ hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, in
     const int blocks = (total + 255) / 256;
     hipLaunchKernelGGL(ocp_prep_kernel, dim3(blocks), dim3(256), 0, st, W, Fp, nx, nu, np, N,
                        mp, kp, hstride, mpad, Hout, Fout);
+    return hipGetLastError();
+}
+
+// per-instance stage-cost tables (bqp_ocp_data.sW != 0): batch x (N+1) x hstride, same layout
+// as the shared table of ocp_prep_kernel
+__global__ void ocp_prep_h_kernel(const double* __restrict__ W, int64_t sW, int batch, int nx,
+                                  int nu, int np, int N, int hstride, double* __restrict__ Hout) {
+    const int nv = nx + nu + np, ns = nx + np;
+    const int64_t per = (int64_t)(N + 1) * hstride;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < per * batch;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = t / per;
+        const int q = (int)(t - b * per);
+        const int k = q / hstride, e = q % hstride;
+        double v = 0.0;
+        if (e < nv * nv) {
+            const int i = e / nv, j = e % nv;
+            const int ei = ext_index(i, nx, nu, np), ej = ext_index(j, nx, nu, np);
+            v = W[b * sW + (int64_t)k * nv * nv + (int64_t)ej * nv + ei];
+            if (k == N && (i >= ns || j >= ns)) v = 0.0;
+        }
+        Hout[t] = v;
+    }
+}
+
+hipError_t launch_ocp_prep_h(const double* W, int64_t sW, int batch, int nx, int nu, int np,
+                             int N, int hstride, double* Hout, hipStream_t st) {
+    const int64_t total = (int64_t)(N + 1) * hstride * batch;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(ocp_prep_h_kernel, dim3(blocks), dim3(256), 0, st, W, sW, batch, nx, nu, np,
+                       N, hstride, Hout);
     return hipGetLastError();
 }
 

@@ -103,3 +103,33 @@ def test_terminal_sets_rebuilt_per_model(di):
             ok += 1
             assert np.abs(r.u[i] - c['u'][0]).max() < 1e-8, i
     assert ok >= M // 2
+
+
+@pytest.mark.parametrize('N', [20, 100])
+def test_per_instance_stage_costs(mg, term_set, N):
+    """per-instance stage costs (bqp_ocp_data.sW != 0; e.g. a model's own weights or steady-state
+    parametrisation): a batch whose instances carry different input weights R_i gives, instance
+    by instance, the solve of that instance's own problem with shared costs (short horizons: the
+    table in the LDS slot; N = 100: read from L2 by the long-horizon layout)"""
+    import bqp
+    g = golden('dms_DSS_tLMPC.npz')
+    X = g['x'][g['idx'][:12]]
+    rs = np.array([0.25, 0.5, 1.0, 2.0, 4.0, 8.0] * 2)
+
+    def tl(r):
+        return bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], r * np.atleast_2d(mg['R']), mg['P'],
+                                mg['Tscalar'], mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'],
+                                mg['F_u'], mg['h_u'], term_set[0], term_set[1], mg['x_wp'],
+                                mg['u_wp'], N=N)
+    probs = [tl(r) for r in rs]
+    W = np.stack([p.prob.W for p in probs])
+    rb = probs[0].solve(X, W=W)
+    assert (rb.exitflag == 1).all()
+    for i, p in enumerate(probs):
+        ri = p.solve(X[i:i + 1])
+        assert ri.exitflag[0] == 1
+        assert np.abs(rb.u[i] - ri.u[0]).max() < 1e-12 * max(1.0, np.abs(ri.u[0]).max())
+        assert np.abs(rb.x[i] - ri.x[0]).max() < 1e-12 * max(1.0, np.abs(ri.x[0]).max())
+    # the weights matter: with the shared costs of instance 0 the other instances move differently
+    r0 = probs[0].solve(X)
+    assert np.abs(rb.u[rs != rs[0], 0, 0] - r0.u[rs != rs[0], 0, 0]).min() > 1e-9

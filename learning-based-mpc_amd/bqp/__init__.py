@@ -10,6 +10,6 @@ from .mpc import LMPC, TrackingLBMPC, TrackingLMPC, TrackingMPC  # noqa: F401
 from .quadprog import quadprog  # noqa: F401
 from .lbmpc import LBMPC, HybridLBMPC, nw_oracle  # noqa: F401
 from .loop import closed_loop  # noqa: F401
-from . import condense, sets  # noqa: F401
+from . import condense, design, sets  # noqa: F401
 
 __version__ = '0.1.0'

@@ -279,14 +279,15 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // stage cost of stage k: the shared LDS table, or (long horizons) the prepared table in
     // global memory (L2-resident, read-only); a stage pointer per use, as the address
     // arithmetic of the short-horizon kernels is register-critical
-#define BQP_HK(k) const real* Hk = Hs + (k) * hstride; const double* Hkg = Hg + (int64_t)(k) * hstride
+#define BQP_HK(k) const real* Hk = Hs + (k) * hstride; \
+    const double* Hkg = (a.H_inst ? a.H_inst + (int64_t)inst * (N + 1) * hstride : a.H) + (int64_t)(k) * hstride
 #define BQP_HV(idx) (LNG ? (real)Hkg[idx] : Hk[idx])
     real* Pgl = LNG ? (real*)a.Pg + (int64_t)inst * (N + 1) * pk_stride(NS) : nullptr;
     // per-instance stage costs: the instance's prepared table (global), copied into the LDS slot
     // on short horizons
-    const double* Hg = a.H_inst ? a.H_inst + (int64_t)inst * (N + 1) * hstride : a.H;
     if (!LNG && a.H_inst) {
         real* Hl = W + L.Hi;
+        const double* Hg = a.H_inst + (int64_t)inst * (N + 1) * hstride;
         for (int i = lane; i < (N + 1) * hstride; i += WAVE) Hl[i] = (real)Hg[i];
         wave_sync();
         Hs = Hl;

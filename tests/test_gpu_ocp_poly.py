@@ -133,3 +133,52 @@ def test_per_instance_stage_costs(mg, term_set, N):
     # the weights matter: with the shared costs of instance 0 the other instances move differently
     r0 = probs[0].solve(X)
     assert np.abs(rb.u[rs != rs[0], 0, 0] - r0.u[rs != rs[0], 0, 0]).min() > 1e-9
+
+
+def test_c4_per_model_design_end_to_end(di):
+    """config C4's use end to end on the tracking MPC: perturbed models (A_i, B_i), each with its
+    own LQR gain, steady-state parametrisation and terminal weights (bqp.design,
+    RunExample.m:42-60), its own stage costs (sW != 0) and its own terminal set (bqp.sets) - one
+    batched GPU solve vs the C restatement solving each instance's own problem"""
+    import bqp
+    from bqp import design, sets
+    from oracle import cpu_ref
+    g = golden('di_design.npz')
+    N = int(g['N'])
+    rng = np.random.default_rng(21)
+    M = 16
+    A = di['A'][None] + 0.01 * rng.standard_normal((M, 2, 2)) * np.abs(di['A'])[None]
+    Bm = di['B'][None] + 0.01 * rng.standard_normal((M, 2, 2)) * np.abs(di['B'])[None]
+    probs, tsets = [], []
+    for i in range(M):
+        d = design.tracking_design(A[i], Bm[i], di['C'], di['Q'], di['R'])
+        F_T, h_T = sets.tracking_terminal_set(A[i], Bm[i], d['K'], d['LAMBDA'], d['PSI'],
+                                              di['F_x'], di['h_x'], di['F_u'], di['h_u'])
+        tsets.append((F_T, h_T))
+        probs.append(bqp.TrackingMPC(A[i], Bm[i], di['Q'], di['R'], d['P'], d['T'], d['LAMBDA'],
+                                     d['PSI'], di['F_x'], di['h_x'], di['F_u'], di['h_u'], F_T,
+                                     h_T, N=N))
+    rows = max(len(h) for _, h in tsets)
+    Fp, hp = sets.pack_sets(tsets, nx=2, nu=2, rows=rows)
+    F0 = np.zeros((rows, 4)); F0[:len(tsets[0][1])] = tsets[0][0]
+    h0 = np.ones(rows); h0[:len(tsets[0][1])] = tsets[0][1]
+    d0 = design.tracking_design(A[0], Bm[0], di['C'], di['Q'], di['R'])
+    base = bqp.TrackingMPC(A[0], Bm[0], di['Q'], di['R'], d0['P'], d0['T'], d0['LAMBDA'], d0['PSI'],
+                           di['F_x'], di['h_x'], di['F_u'], di['h_u'], F0, h0, N=N)
+    X = g['x0'][rng.choice(len(g['x0']), M, replace=False)] * 0.5
+    XS = g['xs'][rng.integers(0, len(g['xs']), M)] * 0.5
+    # per-model linear terms follow each model's own T and LAMBDA
+    w = np.stack([p.linear_terms(XS[i:i + 1])[0][0] for i, p in enumerate(probs)])
+    W = np.stack([p.prob.W for p in probs])
+    r = bqp.solve_ocp(base.prob, X, w=w, A=A, B=Bm, W=W, Fp=Fp, hp=hp)
+    ok = 0
+    for i, p in enumerate(probs):
+        q = p.prob
+        ocp = dict(nx=2, nu=2, np=2, N=N, A=q.A, B=q.B, c=q.c, W=q.W, w=q.w, xlb=q.xlb, xub=q.xub,
+                   ulb=q.ulb, uub=q.uub, Fp=q.Fp, hp=q.hp, kp=q.poly_stage)
+        c = cpu_ref.solve(ocp, X[i:i + 1], w=w[i:i + 1])
+        assert r.exitflag[i] == c['exitflag'][0], i
+        if c['exitflag'][0] == 1:
+            ok += 1
+            assert np.abs(r.u[i] - c['u'][0]).max() < 1e-8, i
+    assert ok >= M // 2

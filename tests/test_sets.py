@@ -36,3 +36,11 @@ def test_pack_sets_pads_inactive_rows():
     assert Fp.shape == (2, 2, 5) and hp.shape == (2, 2)
     assert np.array_equal(Fp[0, 0], [1.0, 0, 0, 0, 2.0]) and (Fp[0, 1] == 0).all() and hp[0, 1] == 1.0
     assert np.array_equal(Fp[1, 1], [1.0, 1.0, 0, 0, 1.0]) and hp[1, 1] == 2.0
+
+
+def test_tracking_design_matches_oracle(di):
+    """bqp.design (RunExample.m:42-60) on the nominal double integrator = the oracle's restatement"""
+    from bqp import design
+    d = design.tracking_design(di['A'], di['B'], di['C'], di['Q'], di['R'])
+    for k in ('K', 'P', 'T', 'LAMBDA', 'PSI'):
+        assert np.abs(d[k] - di[k]).max() < 1e-12, k

@@ -149,10 +149,10 @@ struct QpLds {
     // fpi: the instance carries its own polytope matrix (bqp_ocp_data.sFp != 0), NV x mpad.
     // lng: long-horizon layout (N + 1 > 64, two instances per workgroup at fp64 N = 100): the
     // Riccati P_k live in global scratch (an LDS ring of two stages feeds the recursion), the
-    // forward drift f_k shares the qhat_k slot, box multipliers and right-hand-side terms are
-    // stored per box variable ([upper] - [lower]), the predictor products dt*dlam of the
-    // polytope rows stay in the row wave's registers, and the polytope right-hand side and box
-    // bounds sit in the shared tables when the batch shares them (hpsh, bndsh).
+    // forward drift f_k shares the qhat_k slot, the dynamics residual re_k is recomputed from the
+    // iterate where it is used, box multipliers and right-hand-side terms are stored per box
+    // variable ([upper] - [lower]), and the polytope right-hand side and box bounds sit in the
+    // shared tables when the batch shares them (hpsh, bndsh).
     // hinst: per-instance stage-cost table (bqp_ocp_data.sW != 0) in the slot (short horizons)
     __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false,
                                           bool lng = false, bool hpsh = false, bool bndsh = false,
@@ -170,7 +170,7 @@ struct QpLds {
         o.qt_xpi = c; c += (N + 1) * NS;             // pi_k in the residuals, qhat_k in the solves
         o.rs = c;     c += (N + 1) * NS;             // stationarity residual (s part)
         o.ru = c;     c += (N + 1) * NU;             // stationarity residual (u part)
-        o.re = c;     c += (N + 1) * NS;             // dynamics residual
+        o.re = c;     c += lng ? 0 : (N + 1) * NS;   // dynamics residual (lng: recomputed at use)
         o.pv = c;     c += (N + 1) * NS;             // p_k of the backward sweep
         o.wv = c;     c += (N + 1) * NS;             // cw_k = Phi_k' P_{k+1} re_k (prep_iter)
         o.bw = c;     c += (N + 1) * NU;             // Bbar' P_{k+1} re_k
@@ -191,7 +191,7 @@ struct QpLds {
         o.bnd = c;    c += bndsh ? 0 : (N + 1) * NB * 2;   // box bounds [upper, lower]
         o.gpp = c;    c += NV;                       // Fp' lam
         o.gpe = c;    c += NV;                       // Fp' e
-        o.prp = c;    c += lng ? 0 : mpad;           // predictor dt*dlam of the polytope rows
+        o.prp = c;    c += mpad;                     // predictor dt*dlam of the polytope rows
         o.hp = c;     c += hpsh ? 0 : mpad;          // polytope right-hand side
         o.xch = c;    c += X_NXCH;
         o.Fi = c;     c += fpi ? NV * mpad : 0;      // per-instance polytope (column-major)
@@ -404,13 +404,24 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                     for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
 #pragma unroll
                     for (int c = 0; c < NU; ++c) acc += Bbar(i, c) * u[j][c];
-                    W[L.re + k * NS + i] = acc;
+                    if constexpr (!LNG) W[L.re + k * NS + i] = acc;
                     fe = fmax(fe, fabs(acc));
                 }
             }
         }
         feasA = wmax(fe);
         gsA = wmax(gs);
+    };
+
+    // long horizons: the dynamics residual re_k of stage k = lane + 64 j, recomputed from the
+    // iterate (registers) in the operation order of stage_partials instead of kept in LDS
+    auto re_at = [&](int j, int k, int i) __attribute__((always_inline)) -> real {
+        real acc = cb[i] - W[L.xs + (k + 1) * NS + i];
+#pragma unroll
+        for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) acc += Bbar(i, c) * u[j][c];
+        return acc;
     };
 
     // ---- add the row multipliers (box [upper, lower] in that order, polytope at kp) and
@@ -721,7 +732,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                 const real* Kk = W + L.K + k * NU * NS;
                 real rek[NS], wk[NS];
 #pragma unroll
-                for (int c = 0; c < NS; ++c) rek[c] = W[L.re + k * NS + c];
+                for (int c = 0; c < NS; ++c) rek[c] = LNG ? re_at(j, k, c) : W[L.re + k * NS + c];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
                     real v = 0.0;
@@ -892,7 +903,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                 for (int x = 0; x < NU; ++x) kff[j][x] = r[x];
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    real v = W[L.re + k * NS + i];
+                    real v = LNG ? re_at(j, k, i) : W[L.re + k * NS + i];
 #pragma unroll
                     for (int x = 0; x < NU; ++x) v += Bbar(i, x) * kff[j][x];
                     W[L.fv + k * NS + i] = v;
@@ -1313,10 +1324,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     // residuals are re-formed from the LDS stage vector and bounds when needed)
     real tx[BPL], lx[BPL];
     real tp[RPL], lp[RPL], rp[RPL];
-    real prr[LNG ? RPL : 1];             // long horizons: predictor dt*dlam of the polytope rows
     auto prp_get = [&](int q, int r) __attribute__((always_inline)) -> real {
-        if constexpr (LNG) return prr[q];
-        else return W[L.prp + r];
+        (void)q;
+        return W[L.prp + r];
     };
 #pragma unroll
     for (int b = 0; b < BPL; ++b) { tx[b] = 1.0; lx[b] = 1.0; }
@@ -1601,8 +1611,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             rm = fmax(rm, -dl * frcp(l));
             const real pr = dt * dl;
             s2 += pr;
-            if constexpr (LNG) prr[q] = pr;
-            else W[L.prp + r] = pr;
+            W[L.prp + r] = pr;
             const real e0 = (l * rp[q] - (rc + pr)) * it;
 #pragma unroll
             for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }

@@ -3,6 +3,11 @@
 ``OcpProblem`` holds one stage-wise problem description (shared by the whole batch unless a
 per-instance array is given); ``solve_ocp`` solves a batch of instances that differ in x0 (and
 optionally the linear terms w, the polytope right-hand side hp, or the model A/B).
+
+Dimensions without a compiled structured kernel ((nx, nu, np) other than the MG (4, 1, 1) and
+DI (2, 2, 2) families, or N + 1 > 128) take the condensed route: the states are eliminated on
+the host once per problem (bqp.condense) and the batch runs through bqp_quadprog_batched, the
+dense GPU kernels — same iterate semantics (exit flags, iterations), no CPU solve.
 """
 import ctypes as C
 
@@ -90,9 +95,11 @@ def pack(prob, x0, w=None, hp=None, A=None, B=None, Fp=None, W=None):
 
 
 def solve_ocp(prob, x0, w=None, hp=None, A=None, B=None, handle=None, want_duals=False, Fp=None,
-              W=None, **opts):
+              W=None, route='auto', **opts):
     """Solve a batch on the GPU.  Returns OcpResult(x (b,N+1,nx), u (b,N,nu), theta (b,np),
-    fval, exitflag, iterations, firstorderopt, constrviolation, mu[, pi, lam_x, lam_u, lam_p])."""
+    fval, exitflag, iterations, firstorderopt, constrviolation, mu[, pi, lam_x, lam_u, lam_p]).
+    route: 'auto' (structured kernel; condensed when the C ABI reports the dimensions
+    unsupported), 'structured' (no condensed route) or 'condensed'."""
     lib = _lib.load()
     h = handle or _default_handle()
     dims, data, batch, keep = pack(prob, x0, w, hp, A, B, Fp, W)
@@ -106,10 +113,14 @@ def solve_ocp(prob, x0, w=None, hp=None, A=None, B=None, handle=None, want_duals
         dd = dict(pi=np.zeros((batch, N, nx)), lam_x=np.zeros((batch, N + 1, 2, nx)),
                   lam_u=np.zeros((batch, N, 2, nu)), lam_p=np.zeros((batch, max(mp, 1))))
         duals = _lib.OcpDuals(*(_lib.ptr(dd[k]) for k in ('pi', 'lam_x', 'lam_u', 'lam_p')))
+    if route == 'condensed':
+        return solve_ocp_condensed(prob, x0, w, hp, A, B, handle, want_duals, Fp, W, **opts)
     o = _lib.options(**opts)
     rc = lib.bqp_solve_ocp_batched(h.value, C.byref(dims), batch, C.byref(data), C.byref(o),
                                    _lib.ptr(x), _lib.ptr(u), _lib.ptr(th), _lib.ptr(fval),
                                    _lib.iptr(flag), out, C.byref(duals) if duals else None)
+    if rc == _lib.BQP_E_UNSUPPORTED and route == 'auto':
+        return solve_ocp_condensed(prob, x0, w, hp, A, B, handle, want_duals, Fp, W, **opts)
     _lib.check(rc, 'bqp_solve_ocp_batched')
     res = OcpResult(x=x, u=u, theta=th, fval=fval + prob.const, exitflag=flag,
                     iterations=np.array([o_.iterations for o_ in out]),
@@ -131,3 +142,44 @@ def _default_handle(device=-1):
         h = _lib.Handle(device)
         _handles[device] = h
     return h
+
+
+def condensed_rhs(prob, X0, hp=None):
+    """per-instance (f, b) of the condensed QP (bqp.condense) for states X0 (batch, nx) and
+    optional per-instance polytope right-hand sides hp (batch, mp); the polytope rows are the
+    last mp rows of Condensed.A"""
+    from .condense import Condensed
+    cd = getattr(prob, '_condensed', None)
+    if cd is None:
+        cd = prob._condensed = Condensed(prob)
+    f, b = cd.rhs(X0)
+    if hp is not None and prob.mp:
+        b = b.copy()
+        b[:, -prob.mp:] += np.asarray(hp, float).reshape(len(b), prob.mp) - prob.hp
+    return cd, f, b
+
+
+def solve_ocp_condensed(prob, x0, w=None, hp=None, A=None, B=None, handle=None, want_duals=False,
+                        Fp=None, W=None, **opts):
+    """The condensed route of solve_ocp: one host condensing per problem, the batch on the dense
+    GPU kernels (bqp_quadprog_batched), trajectories recovered through the dynamics.  Per-instance
+    x0 and hp; the model, costs and polytope matrix are shared (they define the dense H and A)."""
+    from .quadprog import quadprog
+    if any(a is not None for a in (w, A, B, Fp, W)):
+        raise ValueError('condensed route: only x0 and hp may vary per instance')
+    if want_duals:
+        raise ValueError('condensed route: stage-wise multipliers are not returned '
+                         '(bqp.quadprog gives the condensed rows\' multipliers)')
+    X0 = np.ascontiguousarray(np.atleast_2d(x0), dtype=np.float64)
+    cd, f, b = condensed_rhs(prob, X0, hp)
+    z, _, flag, out, _ = quadprog(cd.H, f, cd.A, b, options=opts or None,
+                                  handle=handle or _default_handle())
+    N, nx, nu = prob.N, prob.nx, prob.nu
+    V = np.einsum('kaj,bj->bka', cd.S, z) + np.einsum('kax,bx->bka', cd.T, X0) + cd.const_e[None]
+    Wc = prob.W.copy(); wc = prob.w.copy()
+    Wc[N, nx:nx + nu, :] = 0.0; Wc[N, :, nx:nx + nu] = 0.0; wc[N, nx:nx + nu] = 0.0
+    fval = 0.5 * np.einsum('bka,kac,bkc->b', V, Wc, V) + np.einsum('bka,ka->b', V, wc)
+    return OcpResult(x=V[:, :, :nx], u=V[:, :N, nx:nx + nu], theta=z[:, N * nu:],
+                     fval=fval + prob.const, exitflag=flag, iterations=out['iterations'],
+                     firstorderopt=out['firstorderopt'], constrviolation=out['constrviolation'],
+                     mu=np.full(len(X0), np.nan))

@@ -1,12 +1,12 @@
 """Per-launch HBM bytes of the solve kernel from rocprofv3 PMC passes (tools/gpu_prof.sh).
 
-    python tools/pmc_summary.py gpurun_out/TAG profiles/rNN_TAG [--kernel ocp_ipm_kernel]
+    python tools/pmc_summary.py gpurun_out/TAG profiles/rNN_TAG [--kernel ocp_ipm_kernel] [--no-latest]
 
 Reads TAG/pmc_fetch/run_counter_collection.csv (FETCH_SIZE, KB) and TAG/pmc_write/... (WRITE_SIZE,
 KB), keeps the dispatches of the named kernel, and applies the gfx950 correction of
 /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half the bytes of a wide
 read (x2); WRITE_SIZE is taken as is.  Writes OUT/pmc.json and profiles/pmc_latest.json (read by
-bench.py as roofline.traffic), and copies the kernel-trace stats + PMC csvs into OUT.
+bench.py as roofline.traffic of the default C2 line; --no-latest for other configs), and copies the kernel-trace stats + PMC csvs into OUT.
 """
 import csv
 import json
@@ -48,7 +48,8 @@ def main():
                       'WRITE_SIZE x 1024; separate --pmc passes',
     }
     json.dump(res, open(os.path.join(dst, 'pmc.json'), 'w'), indent=1)
-    json.dump(res, open(os.path.join(ROOT, 'profiles', 'pmc_latest.json'), 'w'), indent=1)
+    if '--no-latest' not in sys.argv:
+        json.dump(res, open(os.path.join(ROOT, 'profiles', 'pmc_latest.json'), 'w'), indent=1)
     for sub, name in (('trace', 'run_kernel_stats.csv'), ('pmc_fetch', 'run_counter_collection.csv'),
                       ('pmc_write', 'run_counter_collection.csv')):
         p = os.path.join(src, sub, name)

@@ -22,7 +22,14 @@
 #define MAXNU 4
 #define MAXNV 12
 #define PIV_FLOOR 1e-14
-#define MU_BLOWUP 1e6     /* mu > MU_BLOWUP * min(mu) with stalled feasibility: infeasible */
+#define MU_BLOWUP 1e6     /* mu > MU_BLOWUP * min(mu) with the rows still infeasible: -2       */
+#define FEAS_GUARD 1e-8   /* rows "still infeasible": residual > FEAS_GUARD (1 + |data|)         */
+#define SOC_ALPHA 0.1     /* predictor step below this on a feasible iterate: corrector without  */
+                          /* the second-order term (a centring step; Mehrotra's stall safeguard)  */
+#define DEG_POLISH 1e-10  /* polish a converged iterate whose max_i min(t_i, lam_i) exceeds this  */
+#define POL_RHO 2e6       /* polish weight rho = POL_RHO (1 + |H v + g|_inf)                      */
+#define POL_ALM 8         /* augmented-Lagrangian iterations per polish round (at most)           */
+#define POL_ROUNDS 4      /* active-set corrections                                               */
 
 typedef struct {
     int nx, nu, np, ns, nv, N, mp, kp;
@@ -47,6 +54,9 @@ typedef struct {
      * kernel's row wave does (no residual pass before the factorisation); fe_rows is their norm */
     int rip_live;
     double fe_rows;
+    /* active-set polish: weight rho on the rows taken as equalities, 0 on the dropped ones */
+    int pol;
+    double *wx, *wu, *wp;
 } work_t;
 
 static int perm_of(const prob_t* P, int i) {
@@ -235,22 +245,30 @@ static int factor(const prob_t* P, work_t* W) {
         for (int i = 0; i < nx; ++i) {
             int o = (k * nx + i) * 2;
             double d = 0;
-            if (k > 0 && isfinite(W->xub[k * nx + i])) d += W->lx[o] * W->itx[o];
-            if (k > 0 && isfinite(W->xlb[k * nx + i])) d += W->lx[o + 1] * W->itx[o + 1];
+            if (W->pol) {
+                if (k > 0) d = W->wx[o] + W->wx[o + 1];
+            } else {
+                if (k > 0 && isfinite(W->xub[k * nx + i])) d += W->lx[o] * W->itx[o];
+                if (k > 0 && isfinite(W->xlb[k * nx + i])) d += W->lx[o + 1] * W->itx[o + 1];
+            }
             W->Dx[k * nx + i] = d;
         }
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < nu; ++i) {
             int o = (k * nu + i) * 2;
             double d = 0;
-            if (isfinite(W->uub[k * nu + i])) d += W->lu[o] * W->itu[o];
-            if (isfinite(W->ulb[k * nu + i])) d += W->lu[o + 1] * W->itu[o + 1];
+            if (W->pol) {
+                d = W->wu[o] + W->wu[o + 1];
+            } else {
+                if (isfinite(W->uub[k * nu + i])) d += W->lu[o] * W->itu[o];
+                if (isfinite(W->ulb[k * nu + i])) d += W->lu[o + 1] * W->itu[o + 1];
+            }
             W->Du[k * nu + i] = d;
         }
     memset(W->FD, 0, sizeof(double) * nv * nv);
     for (int r = 0; r < P->mp; ++r) {
         const double* F = P->Fp + (size_t)r * nv;
-        double d = W->lp[r] * W->itp[r];
+        double d = W->pol ? W->wp[r] : W->lp[r] * W->itp[r];
         for (int i = 0; i < nv; ++i) {
             double di = d * F[i];
             for (int j = i; j < nv; ++j) W->FD[i * nv + j] += di * F[j];
@@ -374,16 +392,25 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
         for (int i = 0; i < nx; ++i) {
             int o = (k * nx + i) * 2;
             double e = 0;
-            if (k > 0 && isfinite(W->xub[k * nx + i])) e += (W->lx[o] * W->rix[o] - rcx[o]) * W->itx[o];
-            if (k > 0 && isfinite(W->xlb[k * nx + i])) e -= (W->lx[o + 1] * W->rix[o + 1] - rcx[o + 1]) * W->itx[o + 1];
+            if (W->pol) {
+                /* polish: the augmented-Lagrangian gradient term rho (C v - b) of active rows */
+                if (k > 0) e = W->wx[o] * W->rix[o] - W->wx[o + 1] * W->rix[o + 1];
+            } else {
+                if (k > 0 && isfinite(W->xub[k * nx + i])) e += (W->lx[o] * W->rix[o] - rcx[o]) * W->itx[o];
+                if (k > 0 && isfinite(W->xlb[k * nx + i])) e -= (W->lx[o + 1] * W->rix[o + 1] - rcx[o + 1]) * W->itx[o + 1];
+            }
             W->qs[k * ns + i] += e;
         }
         if (k < N)
             for (int i = 0; i < nu; ++i) {
                 int o = (k * nu + i) * 2;
                 double e = W->ru[k * nu + i];
-                if (isfinite(W->uub[k * nu + i])) e += (W->lu[o] * W->riu[o] - rcu[o]) * W->itu[o];
-                if (isfinite(W->ulb[k * nu + i])) e -= (W->lu[o + 1] * W->riu[o + 1] - rcu[o + 1]) * W->itu[o + 1];
+                if (W->pol) {
+                    e += W->wu[o] * W->riu[o] - W->wu[o + 1] * W->riu[o + 1];
+                } else {
+                    if (isfinite(W->uub[k * nu + i])) e += (W->lu[o] * W->riu[o] - rcu[o]) * W->itu[o];
+                    if (isfinite(W->ulb[k * nu + i])) e -= (W->lu[o + 1] * W->riu[o + 1] - rcu[o + 1]) * W->itu[o + 1];
+                }
                 W->qu[k * nu + i] = e;
             }
     }
@@ -391,7 +418,7 @@ static void solve_kkt(const prob_t* P, work_t* W, const double* rcx, const doubl
         double gp[MAXNV];
         memset(gp, 0, sizeof(gp));
         for (int r = 0; r < P->mp; ++r) {
-            double e = (W->lp[r] * W->rip[r] - rcp[r]) * W->itp[r];
+            double e = W->pol ? W->wp[r] * W->rip[r] : (W->lp[r] * W->rip[r] - rcp[r]) * W->itp[r];
             const double* F = P->Fp + (size_t)r * nv;
             for (int j = 0; j < nv; ++j) gp[j] += F[j] * e;
         }
@@ -558,10 +585,113 @@ static double comp_s2(const prob_t* P, work_t* W) {
     return s;
 }
 
+/* ---------------- active-set polish ---------------- */
+/* Rows with lam > t at the end of the IPM are taken as equalities and the others are dropped; the
+ * equality-constrained QP is solved by augmented-Lagrangian iterations on the same Riccati
+ * factorisation (weight rho on the active rows, D = 0 elsewhere: one factorisation per round),
+ * nu += rho (C v - b) after each solve.  Rows whose multiplier turns negative leave the set and
+ * violated rows enter it, for up to POL_ROUNDS rounds.  The polished point replaces the IPM
+ * iterate only if it is primal feasible, dual feasible and stationary; it is what makes weakly
+ * active (degenerate) rows, whose slack and multiplier both stay ~sqrt(mu), and problems with
+ * multipliers ~1e3-1e5 (D = lam/t beyond fp64 range near mu = 1e-14) end at
+ * the exact optimum. */
+#define FOR_ROWS(BX, BU, BP)                                                                    \
+    for (int i = 0; i < nxr; ++i) {                                                            \
+        const int k_ = i / (2 * nx), xi_ = (i / 2) % nx;                                        \
+        if (!(k_ > 0 && isfinite((i & 1) ? W->xlb[k_ * nx + xi_] : W->xub[k_ * nx + xi_])))   \
+            continue;                                                                           \
+        BX;                                                                                     \
+    }                                                                                           \
+    for (int i = 0; i < nur; ++i) {                                                            \
+        if (!isfinite((i & 1) ? W->ulb[i / 2] : W->uub[i / 2])) continue;                       \
+        BU;                                                                                     \
+    }                                                                                           \
+    for (int i = 0; i < mp; ++i) { BP; }
+
+static int polish(const prob_t* P, work_t* W, double bs, double rho, double* kkt_out) {
+    const int N = P->N, nx = P->nx, ns = P->ns;
+    const int nxr = (N + 1) * nx * 2, nur = N * P->nu * 2, mp = P->mp;
+    const int S = (N + 1) * ns, U = N * P->nu;
+    /* keep the IPM iterate for the fall-back */
+    const size_t tot = 2 * (size_t)S + U + 2 * ((size_t)nxr + nur + mp);
+    double* sv = (double*)malloc(sizeof(double) * tot);
+    double* q = sv;
+#define SAVE(a, n) do { memcpy(q, a, sizeof(double) * (n)); q += (n); } while (0)
+#define LOAD(a, n) do { memcpy(a, q, sizeof(double) * (n)); q += (n); } while (0)
+    SAVE(W->s, S); SAVE(W->pi, S); SAVE(W->u, U); SAVE(W->tx, nxr); SAVE(W->lx, nxr);
+    SAVE(W->tu, nur); SAVE(W->lu, nur); SAVE(W->tp, mp); SAVE(W->lp, mp);
+    memset(W->wx, 0, sizeof(double) * nxr); memset(W->wu, 0, sizeof(double) * nur);
+    memset(W->wp, 0, sizeof(double) * mp);
+    FOR_ROWS({ if (W->lx[i] > W->tx[i]) W->wx[i] = rho; else W->lx[i] = 0.0; },
+             { if (W->lu[i] > W->tu[i]) W->wu[i] = rho; else W->lu[i] = 0.0; },
+             { if (W->lp[i] > W->tp[i]) W->wp[i] = rho; else W->lp[i] = 0.0; })
+    /* t = 0: the row residual C v + t - b is the constraint value C v - b */
+    memset(W->tx, 0, sizeof(double) * nxr); memset(W->tu, 0, sizeof(double) * nur);
+    memset(W->tp, 0, sizeof(double) * mp);
+    W->pol = 1;
+    W->rip_live = 0;
+    double stat = 0, feas = 0, cs, gs = 0, viol = 0;
+    int mc, ok = 0;
+    for (int rd = 0; rd < POL_ROUNDS && !ok; ++rd) {
+        residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+        if (factor(P, W)) break;
+        double va_prev = INFINITY;
+        for (int j = 0; j < POL_ALM; ++j) {
+            if (j > 0) residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+            prep_iter(P, W);
+            solve_kkt(P, W, W->dtx, W->dtu, W->dtp);    /* complementarity rhs unused */
+            for (int i = 0; i < S; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
+            for (int i = 0; i < U; ++i) W->u[i] += W->du[i];
+            residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+            double va = 0.0;
+            FOR_ROWS({ W->lx[i] += W->wx[i] * W->rix[i]; if (W->wx[i] > 0) va = fmax(va, fabs(W->rix[i])); },
+                     { W->lu[i] += W->wu[i] * W->riu[i]; if (W->wu[i] > 0) va = fmax(va, fabs(W->riu[i])); },
+                     { W->lp[i] += W->wp[i] * W->rip[i]; if (W->wp[i] > 0) va = fmax(va, fabs(W->rip[i])); })
+            if (va <= 1e-14 * (1.0 + bs) || va >= 0.5 * va_prev) break;
+            va_prev = va;
+        }
+        residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+        double va = 0.0, lneg = 0.0, lmx = 0.0;
+        viol = 0.0;
+        FOR_ROWS({ viol = fmax(viol, W->rix[i]); if (W->wx[i] > 0) { va = fmax(va, fabs(W->rix[i])); lneg = fmin(lneg, W->lx[i]); lmx = fmax(lmx, W->lx[i]); } },
+                 { viol = fmax(viol, W->riu[i]); if (W->wu[i] > 0) { va = fmax(va, fabs(W->riu[i])); lneg = fmin(lneg, W->lu[i]); lmx = fmax(lmx, W->lu[i]); } },
+                 { viol = fmax(viol, W->rip[i]); if (W->wp[i] > 0) { va = fmax(va, fabs(W->rip[i])); lneg = fmin(lneg, W->lp[i]); lmx = fmax(lmx, W->lp[i]); } })
+        double fe = 0.0;
+        for (int i = 0; i < N * ns; ++i) fe = fmax(fe, fabs(W->re[i]));
+        const double tf = 1e-12 * (1.0 + bs), td = 1e-9 * (1.0 + lmx);
+        ok = isfinite(stat) && stat <= 1e-8 * (1.0 + gs) && viol <= tf && va <= tf && lneg >= -td && fe <= tf;
+        if (ok) break;
+        /* active-set correction: negative multipliers leave, violated rows enter */
+        int ch = 0;
+        FOR_ROWS({ if (W->wx[i] > 0 && W->lx[i] < -td) { W->wx[i] = 0; W->lx[i] = 0; ++ch; } else if (W->wx[i] == 0 && W->rix[i] > tf) { W->wx[i] = rho; ++ch; } },
+                 { if (W->wu[i] > 0 && W->lu[i] < -td) { W->wu[i] = 0; W->lu[i] = 0; ++ch; } else if (W->wu[i] == 0 && W->riu[i] > tf) { W->wu[i] = rho; ++ch; } },
+                 { if (W->wp[i] > 0 && W->lp[i] < -td) { W->wp[i] = 0; W->lp[i] = 0; ++ch; } else if (W->wp[i] == 0 && W->rip[i] > tf) { W->wp[i] = rho; ++ch; } })
+        if (!ch) break;
+    }
+    W->pol = 0;
+    if (ok) {
+        /* slacks of the polished point t = b - C v (>= 0 up to tf), multipliers >= 0 */
+        for (int i = 0; i < nxr; ++i) { W->tx[i] = fmax(-W->rix[i], 0.0); W->lx[i] = fmax(W->lx[i], 0.0); }
+        for (int i = 0; i < nur; ++i) { W->tu[i] = fmax(-W->riu[i], 0.0); W->lu[i] = fmax(W->lu[i], 0.0); }
+        for (int r = 0; r < mp; ++r) { W->tp[r] = fmax(-W->rip[r], 0.0); W->lp[r] = fmax(W->lp[r], 0.0); }
+        kkt_out[0] = stat; kkt_out[1] = viol; kkt_out[2] = 0.0;
+    } else {
+        q = sv;
+        LOAD(W->s, S); LOAD(W->pi, S); LOAD(W->u, U); LOAD(W->tx, nxr); LOAD(W->lx, nxr);
+        LOAD(W->tu, nur); LOAD(W->lu, nur); LOAD(W->tp, mp); LOAD(W->lp, mp);
+    }
+#undef SAVE
+#undef LOAD
+    free(sv);
+    return ok;
+}
+#undef FOR_ROWS
+
 /* ---------------- one instance ---------------- */
 typedef struct {
     int max_iter;
     double tol_stat, tol_feas, tol_comp, tau;
+    int polish;
 } opts_t;
 
 /* Fp(r,:) [ds_kp; du_kp] in the kernel's order (fdot) */
@@ -574,10 +704,12 @@ static double poly_fdv(const prob_t* P, const work_t* W, int r) {
     return acc;
 }
 
-static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, double* kkt) {
+static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, double* kkt, int* polished) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns;
     W->rip_live = 0;
     W->fe_rows = 0.0;
+    W->pol = 0;
+    if (polished) *polished = 0;
     const int nxr = (N + 1) * nx * 2, nur = N * nu * 2;
     double stat, feas, cs, gs;
     int mc;
@@ -680,7 +812,7 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         mu = cs / (mc > 0 ? mc : 1);
         if (stat <= op->tol_stat * (1.0 + gs) && feas <= op->tol_feas * (1.0 + bs) && mu <= op->tol_comp) { flag = 1; break; }
         if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
-        if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bs)) { flag = -2; break; }
+        if (mu > MU_BLOWUP * mu_min && feas > FEAS_GUARD * (1.0 + bs)) { flag = -2; break; }
         if (mu < mu_min) mu_min = mu;
         if (it == op->max_iter) break;
         if (factor(P, W)) { flag = -8; break; }
@@ -695,9 +827,13 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         double mua = (cs * (1.0 - a) + a * a * comp_s2(P, W)) / (mc > 0 ? mc : 1);
         double sg = mua / mu;
         sg = sg * sg * sg;
-        for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i] + W->dtx[i] * W->dlx[i] - sg * mu;
-        for (int i = 0; i < nur; ++i) rcu[i] = W->tu[i] * W->lu[i] + W->dtu[i] * W->dlu[i] - sg * mu;
-        for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r] + W->dtp[r] * W->dlp[r] - sg * mu;
+        /* a short predictor step on a feasible iterate: the second-order term dt_a dlam_a is
+         * dropped (pure centring, Mehrotra's safeguard against the alternating stall of
+         * nearly-degenerate rows; C4 instance 6264) */
+        const double soc = (a < SOC_ALPHA && feas <= FEAS_GUARD * (1.0 + bs)) ? 0.0 : 1.0;
+        for (int i = 0; i < nxr; ++i) rcx[i] = W->tx[i] * W->lx[i] + soc * (W->dtx[i] * W->dlx[i]) - sg * mu;
+        for (int i = 0; i < nur; ++i) rcu[i] = W->tu[i] * W->lu[i] + soc * (W->dtu[i] * W->dlu[i]) - sg * mu;
+        for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r] + soc * (W->dtp[r] * W->dlp[r]) - sg * mu;
         solve_kkt(P, W, rcx, rcu, rcp);
         a = max_step(P, W) * op->tau;
         if (a > 1.0) a = 1.0;
@@ -737,6 +873,27 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
                     }
         for (int r = 0; r < P->mp; ++r) { W->tp[r] += a * W->dtp[r]; W->lp[r] += a * W->dlp[r]; }
     }
+    if (flag != -2 && op->polish) {
+        /* polish when the IPM did not converge (0 / -8: the factorisation left fp64 range) or
+         * converged with a weakly active row (max_i min(t_i, lam_i) > DEG_POLISH) */
+        double degm = 0.0;
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < nx; ++i)
+                for (int h = 0; h < 2; ++h)
+                    if (PRESENT_X(k, i, h)) { const int o = (k * nx + i) * 2 + h; degm = fmax(degm, fmin(W->tx[o], W->lx[o])); }
+        for (int k = 0; k < N; ++k)
+            for (int i = 0; i < nu; ++i)
+                for (int h = 0; h < 2; ++h)
+                    if (PRESENT_U(k, i, h)) { const int o = (k * nu + i) * 2 + h; degm = fmax(degm, fmin(W->tu[o], W->lu[o])); }
+        for (int r = 0; r < P->mp; ++r) degm = fmax(degm, fmin(W->tp[r], W->lp[r]));
+        if (flag != 1 || degm > DEG_POLISH) {
+            double k3p[3];
+            if (isfinite(gs) && polish(P, W, bs, POL_RHO * (1.0 + gs), k3p)) {
+                flag = 1; stat = k3p[0]; feas = k3p[1]; mu = k3p[2];
+                if (polished) *polished = 1;
+            }
+        }
+    }
 #undef PRESENT_X
 #undef PRESENT_U
     free(rcx);
@@ -750,11 +907,12 @@ static double* alloc0(size_t n) { return (double*)calloc(n ? n : 1, sizeof(doubl
 
 int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int max_iter,
                   double tol_stat, double tol_feas, double tol_comp, double tau, int nthreads,
-                  double* x, double* u, double* theta, int* exitflag, int* iters, double* kkt3) {
+                  double* x, double* u, double* theta, int* exitflag, int* iters, double* kkt3,
+                  int polish, int* polished) {
     const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
     const int ns = nx + np, nv = ns + nu, mp = d->n_poly;
     if (ns > MAXNS || nu > MAXNU || nv > MAXNV || N < 1) return BQP_E_ARG;
-    opts_t op = {max_iter, tol_stat, tol_feas, tol_comp, tau};
+    opts_t op = {max_iter, tol_stat, tol_feas, tol_comp, tau, polish};
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
@@ -787,6 +945,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.Dx = alloc0((N + 1) * nx); W.Du = alloc0(N * nu); W.FD = alloc0(nv * nv);
         W.itx = alloc0((N + 1) * nx * 2); W.ilx = alloc0((N + 1) * nx * 2);
         W.itu = alloc0(N * nu * 2); W.ilu = alloc0(N * nu * 2); W.itp = alloc0(mp); W.ilp = alloc0(mp);
+        W.wx = alloc0((N + 1) * nx * 2); W.wu = alloc0(N * nu * 2); W.wp = alloc0(mp);
         prob_t P;
         memset(&P, 0, sizeof(P));
         P.nx = nx; P.nu = nu; P.np = np; P.ns = ns; P.nv = nv; P.N = N; P.mp = mp;
@@ -838,7 +997,9 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
             for (int i = 0; i < nx; ++i) W.s[i] = D->x0[b * D->sx0 + i];
             int it = 0;
             double k3[3] = {0, 0, 0};
-            int fl = solve_one(&P, &W, &op, &it, k3);
+            int pz = 0;
+            int fl = solve_one(&P, &W, &op, &it, k3, &pz);
+            if (polished) polished[b] = pz;
             if (fl == -8) { /* keep going; report */ }
             for (int k = 0; k <= N; ++k)
                 for (int i = 0; i < nx; ++i) x[((size_t)b * (N + 1) + k) * nx + i] = W.s[k * ns + i];
@@ -857,7 +1018,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Phit); free(W.Ktab); free(W.Rinv); free(W.p);
         free(W.qs); free(W.qu); free(W.wv); free(W.cw); free(W.qt); free(W.qh); free(W.kff); free(W.f); free(W.Dx);
         free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
-        free(W.ilp);
+        free(W.ilp); free(W.wx); free(W.wu); free(W.wp);
     }
     return err;
 }

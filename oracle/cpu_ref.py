@@ -84,16 +84,20 @@ def pack_ocp(ocp, x0, w=None, hp=None, A=None, B=None):
 
 
 def solve(ocp, x0, w=None, hp=None, A=None, B=None, max_iter=50, tol_stat=1e-8,
-          tol_feas=1e-10, tol_comp=1e-14, tau=0.995, threads=0):
+          tol_feas=1e-10, tol_comp=1e-14, tau=0.995, threads=0, polish=True):
+    """polish=False: the IPM iterates alone (iterate-level parity with a kernel that does not
+    polish); the result's 'polished' marks instances whose answer is the active-set polish."""
     dims, d, batch, keep = pack_ocp(ocp, x0, w, hp, A, B)
     nx, nu, p, N = ocp['nx'], ocp['nu'], ocp['np'], ocp['N']
     x = np.zeros((batch, N + 1, nx)); u = np.zeros((batch, N, nu)); th = np.zeros((batch, p))
     flag = np.zeros(batch, np.int32); it = np.zeros(batch, np.int32); k3 = np.zeros((batch, 3))
+    pol = np.zeros(batch, np.int32)
     rc = lib().cpu_ocp_solve(C.byref(dims), C.c_int(batch), C.byref(d), C.c_int(max_iter),
                              C.c_double(tol_stat), C.c_double(tol_feas), C.c_double(tol_comp),
                              C.c_double(tau), C.c_int(threads), _ptr(x), _ptr(u), _ptr(th),
                              flag.ctypes.data_as(C.POINTER(C.c_int)),
-                             it.ctypes.data_as(C.POINTER(C.c_int)), _ptr(k3))
+                             it.ctypes.data_as(C.POINTER(C.c_int)), _ptr(k3), C.c_int(int(polish)),
+                             pol.ctypes.data_as(C.POINTER(C.c_int)))
     if rc != 0:
         raise RuntimeError('cpu_ocp_solve failed: %d' % rc)
-    return dict(x=x, u=u, theta=th, exitflag=flag, iterations=it, kkt=k3)
+    return dict(x=x, u=u, theta=th, exitflag=flag, iterations=it, kkt=k3, polished=pol)

@@ -1,0 +1,176 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Exact ground truth for strictly convex inequality-constrained QPs that does not depend on any
+interior-point iterate:
+
+    min 0.5 z'Hz + f'z   s.t.  A z <= b
+
+solved as a least-distance problem (Lawson & Hanson, "Solving Least Squares Problems", ch. 23):
+with H = R'R and y = R z + R^{-T} f the problem is  min ||y||  s.t.  G y >= h,
+G = -A R^{-1}, h = -(b + A H^{-1} f), and the LDP is one non-negative least-squares problem
+(scipy.optimize.nnls, Lawson-Hanson active set, finite termination).  A non-zero NNLS residual
+gives the solution; a zero residual certifies infeasibility (Farkas: u >= 0 with G'u = 0,
+h'u = 1).  The active set it returns is then polished by one KKT solve in fp64.
+
+This is the ground truth for the Monte-Carlo models (config C4) on which the plain IPM of
+``oracle/dense_qp.py`` breaks down (degenerate terminal vertices, multipliers ~1e3): round-3
+VERDICT item 1.  ``condense_ocp`` eliminates the states of a structured OCP (qp_forms *_ocp
+dict: the reference's QP after ``costLMPC.m`` / ``constraintsLMPC.m`` restatement) with an
+optional per-instance model (A_i, B_i), i.e. the perturbed ``nominalModel.m:28`` solved at the
+call site ``ocpLMPC.m:24``.
+"""
+import numpy as np
+import scipy.linalg as sla
+from scipy.optimize import nnls
+
+
+def condense_ocp(ocp, x0, A=None, B=None, w=None, hp=None):
+    """z = [u_0 .. u_{N-1}; theta]; returns dict(H, f, A, b, S, s) with x_k = S[k] z + s[k]."""
+    nx, nu, p, N = ocp['nx'], ocp['nu'], ocp['np'], ocp['N']
+    A = ocp['A'] if A is None else np.asarray(A, float).reshape(nx, nx)
+    B = ocp['B'] if B is None else np.asarray(B, float).reshape(nx, nu)
+    w = ocp['w'] if w is None else w
+    hp = ocp['hp'] if hp is None else hp
+    c = np.asarray(ocp['c'], float)
+    nz = N * nu + p
+    S = np.zeros((N + 1, nx, nz)); s = np.zeros((N + 1, nx))
+    s[0] = x0
+    for k in range(N):
+        S[k + 1] = A @ S[k]
+        S[k + 1][:, k * nu:(k + 1) * nu] += B
+        s[k + 1] = A @ s[k] + c
+
+    def stage(k):
+        """v_k = [x_k; u_k; theta] = M z + m"""
+        M = np.zeros((nx + nu + p, nz)); m = np.zeros(nx + nu + p)
+        M[:nx] = S[k]; m[:nx] = s[k]
+        if k < N:
+            M[nx + np.arange(nu), k * nu + np.arange(nu)] = 1.0
+        M[nx + nu + np.arange(p), N * nu + np.arange(p)] = 1.0
+        return M, m
+
+    H = np.zeros((nz, nz)); f = np.zeros(nz)
+    for k in range(N + 1):
+        M, m = stage(k)
+        Wk = np.array(ocp['W'][k], float); wk = np.array(w[k], float)
+        if k == N:
+            Wk[nx:nx + nu, :] = 0; Wk[:, nx:nx + nu] = 0; wk[nx:nx + nu] = 0
+        H += M.T @ Wk @ M
+        f += M.T @ (Wk @ m + wk)
+    rows, rhs = [], []
+    for k in range(1, N + 1):
+        for i in range(nx):
+            if np.isfinite(ocp['xub'][k][i]):
+                rows.append(S[k][i]); rhs.append(ocp['xub'][k][i] - s[k][i])
+            if np.isfinite(ocp['xlb'][k][i]):
+                rows.append(-S[k][i]); rhs.append(s[k][i] - ocp['xlb'][k][i])
+    for k in range(N):
+        for i in range(nu):
+            e = np.zeros(nz); e[k * nu + i] = 1.0
+            if np.isfinite(ocp['uub'][k][i]):
+                rows.append(e); rhs.append(ocp['uub'][k][i])
+            if np.isfinite(ocp['ulb'][k][i]):
+                rows.append(-e); rhs.append(-ocp['ulb'][k][i])
+    M, m = stage(ocp['kp'])
+    Fp = np.array(ocp['Fp'], float)
+    if ocp['kp'] == N:
+        Fp[:, nx:nx + nu] = 0
+    Ain = np.vstack(rows + [Fp @ M]) if rows else Fp @ M
+    bin_ = np.concatenate([np.array(rhs), hp - Fp @ m])
+    return dict(H=0.5 * (H + H.T), f=f, A=Ain, b=bin_, S=S, s=s, nz=nz)
+
+
+def _kkt_refined(H, f, Aa, ba, steps=3):
+    """Equality-constrained KKT [H Aa'; Aa 0][z; l] = [-f; ba] in fp64 with iterative refinement
+    whose residuals are formed in extended precision (np.longdouble, 64-bit mantissa on x86)."""
+    n, na = H.shape[0], Aa.shape[0]
+    K = np.block([[H, Aa.T], [Aa, np.zeros((na, na))]])
+    rhs = np.concatenate([-f, ba])
+    Kl = K.astype(np.longdouble)
+    rl = rhs.astype(np.longdouble)
+    try:
+        lu = sla.lu_factor(K)
+        sol = sla.lu_solve(lu, rhs)
+        for _ in range(steps):
+            res = (rl - Kl @ sol.astype(np.longdouble)).astype(np.float64)
+            sol = sol + sla.lu_solve(lu, res)
+    except (np.linalg.LinAlgError, ValueError):
+        sol = np.linalg.lstsq(K, rhs, rcond=1e-15)[0]
+    return sol[:n], sol[n:]
+
+
+def solve(H, f, A, b, polish=True):
+    """Returns dict(z, lam, status ('optimal' | 'infeasible'), active, fval, kkt)."""
+    n = H.shape[0]
+    nrm = np.maximum(np.linalg.norm(A, axis=1), 1e-300)  # unit-norm rows: same feasible set
+    A, b = A / nrm[:, None], b / nrm
+    R = sla.cholesky(H, lower=False)                       # H = R'R
+    Rinv = sla.solve_triangular(R, np.eye(n), lower=False)
+    Hf = sla.cho_solve((R, False), f)
+    G = -A @ Rinv
+    h = -(b + A @ Hf)
+    scale = np.maximum(1.0, np.linalg.norm(G, axis=1))     # row scaling (does not change the LDP)
+    Gs, hs = G / scale[:, None], h / scale
+    E = np.vstack([Gs.T, hs[None, :]])
+    e = np.zeros(n + 1); e[n] = 1.0
+    u, _ = nnls(E, e, maxiter=50 * E.shape[1])
+    r = E @ u - e
+    bs = max(1.0, np.abs(b).max())
+    if abs(r[n]) < 1e-13 or np.linalg.norm(r) < 1e-13:
+        return dict(z=None, lam=None, status='infeasible', active=None, fval=None, kkt=None)
+    y = -r[:n] / r[n]
+    z = Rinv @ y - Hf
+    lam = np.maximum(u / (-r[n]) / scale, 0.0)
+    act = u > 0
+    if polish:
+        # primal-dual active-set polish from the NNLS active set: exact KKT on the set, drop
+        # rows with negative multipliers, add violated rows, until both hold
+        for _ in range(20):
+            zp, lp = _kkt_refined(H, f, A[act], b[act])
+            viol = A @ zp - b
+            lfull = np.zeros(A.shape[0]); lfull[act] = lp
+            neg = act & (lfull < -1e-10 * max(1.0, np.abs(lp).max(initial=0)))
+            bad = (~act) & (viol > 1e-12 * bs)
+            if not neg.any() and not bad.any():
+                z, lam = zp, np.maximum(lfull, 0.0)
+                break
+            act = (act & ~neg) | bad
+    if (A @ z - b).max(initial=-1) > 1e-9 * bs:
+        return dict(z=None, lam=None, status='infeasible', active=None, fval=None, kkt=None)
+    g = H @ z + f + A.T @ lam
+    lam = lam / nrm                                        # multipliers of the caller's rows
+    kkt = dict(stationarity=float(np.abs(g).max()),
+               primal=float(max(0.0, (A @ z - b).max(initial=0))),
+               complementarity=float(np.abs(lam * nrm * (b - A @ z)).max(initial=0)),
+               dual=float(-min(0.0, lam.min(initial=0))))
+    return dict(z=z, lam=lam, status='optimal', active=np.flatnonzero(act),
+                fval=float(0.5 * z @ H @ z + f @ z), kkt=kkt)
+
+
+def lp_margin(A, b):
+    """max s such that A z + s <= b (row-normalised rows): > 0 strictly feasible, < 0 infeasible
+    (scipy HiGHS).  The LP classification of VERDICT round 2, item 1."""
+    from scipy.optimize import linprog
+    nrm = np.maximum(np.linalg.norm(A, axis=1), 1e-300)
+    An, bn = A / nrm[:, None], b / nrm
+    n = A.shape[1]
+    c = np.zeros(n + 1); c[-1] = -1.0
+    res = linprog(c, A_ub=np.hstack([An, np.ones((len(bn), 1))]), b_ub=bn,
+                  bounds=[(None, None)] * n + [(None, 1.0)], method='highs')
+    return float(res.x[-1]) if res.status == 0 else float('nan')
+
+
+def solve_ocp(ocp, x0, A=None, B=None, w=None, hp=None):
+    """Exact optimum of one structured OCP: dict(status, u (N, nu), theta, x (N+1, nx), fval, kkt,
+    margin)."""
+    qp = condense_ocp(ocp, x0, A, B, w, hp)
+    r = solve(qp['H'], qp['f'], qp['A'], qp['b'])
+    r['margin'] = lp_margin(qp['A'], qp['b'])
+    if r['status'] != 'optimal':
+        return r
+    N, nu, p = ocp['N'], ocp['nu'], ocp['np']
+    z = r['z']
+    r['u'] = z[:N * nu].reshape(N, nu)
+    r['theta'] = z[N * nu:]
+    r['x'] = np.einsum('kij,j->ki', qp['S'], z) + qp['s']
+    return r

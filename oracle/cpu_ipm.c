@@ -13,6 +13,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -26,7 +27,12 @@
 #define FEAS_GUARD 1e-8   /* rows "still infeasible": residual > FEAS_GUARD (1 + |data|)         */
 #define SOC_ALPHA 0.1     /* predictor step below this on a feasible iterate: corrector without  */
                           /* the second-order term (a centring step; Mehrotra's stall safeguard)  */
+#ifndef CMAX_K
+#define CMAX_K 100.0     /* and every row: t_i lam_i <= CMAX_K tol_comp (the average alone lets one */
+#endif            /* weakly active row keep t ~ 1e-10: first moves off by 1e-7 at N = 100) */
+#ifndef DEG_POLISH
 #define DEG_POLISH 1e-10  /* polish a converged iterate whose max_i min(t_i, lam_i) exceeds this  */
+#endif
 #define POL_RHO 2e6       /* polish weight rho = POL_RHO (1 + |H v + g|_inf)                      */
 #define POL_ALM 8         /* augmented-Lagrangian iterations per polish round (at most)           */
 #define POL_ROUNDS 4      /* active-set corrections                                               */
@@ -56,6 +62,7 @@ typedef struct {
     double fe_rows;
     /* active-set polish: weight rho on the rows taken as equalities, 0 on the dropped ones */
     int pol;
+    double cmax;   /* max_i t_i lam_i of the last residuals() */
     double *wx, *wu, *wp;
 } work_t;
 
@@ -118,6 +125,7 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
                       int* mcount, double* gscale) {
     const int N = P->N, nx = P->nx, nu = P->nu, ns = P->ns, nv = P->nv;
     double st = 0, fe = 0, cs = 0, gs = 0;
+    W->cmax = 0.0;
     int mc = 0;
     for (int k = 0; k <= N; ++k) {
         const double* H = P->H + (size_t)k * nv * nv;
@@ -153,12 +161,12 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
             if (k > 0 && isfinite(W->xub[k * nx + i])) {
                 W->rs[k * ns + i] += W->lx[o];
                 ri_u = xi + W->tx[o] - W->xub[k * nx + i];
-                cs += W->tx[o] * W->lx[o]; ++mc;
+                cs += W->tx[o] * W->lx[o]; ++mc; W->cmax = fmax(W->cmax, W->tx[o] * W->lx[o]);
             }
             if (k > 0 && isfinite(W->xlb[k * nx + i])) {
                 W->rs[k * ns + i] -= W->lx[o + 1];
                 ri_l = -xi + W->tx[o + 1] + W->xlb[k * nx + i];
-                cs += W->tx[o + 1] * W->lx[o + 1]; ++mc;
+                cs += W->tx[o + 1] * W->lx[o + 1]; ++mc; W->cmax = fmax(W->cmax, W->tx[o + 1] * W->lx[o + 1]);
             }
             W->rix[o] = ri_u; W->rix[o + 1] = ri_l;
         }
@@ -170,12 +178,12 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
                 if (isfinite(W->uub[k * nu + i])) {
                     W->ru[k * nu + i] += W->lu[o];
                     ri_u = ui + W->tu[o] - W->uub[k * nu + i];
-                    cs += W->tu[o] * W->lu[o]; ++mc;
+                    cs += W->tu[o] * W->lu[o]; ++mc; W->cmax = fmax(W->cmax, W->tu[o] * W->lu[o]);
                 }
                 if (isfinite(W->ulb[k * nu + i])) {
                     W->ru[k * nu + i] -= W->lu[o + 1];
                     ri_l = -ui + W->tu[o + 1] + W->ulb[k * nu + i];
-                    cs += W->tu[o + 1] * W->lu[o + 1]; ++mc;
+                    cs += W->tu[o + 1] * W->lu[o + 1]; ++mc; W->cmax = fmax(W->cmax, W->tu[o + 1] * W->lu[o + 1]);
                 }
                 W->riu[o] = ri_u; W->riu[o + 1] = ri_l;
             }
@@ -203,7 +211,7 @@ static void residuals(const prob_t* P, work_t* W, double* stat, double* feas, do
                 gp[j] += F[j] * W->lp[r];
             }
             if (!W->rip_live) W->rip[r] = a;
-            cs += W->tp[r] * W->lp[r]; ++mc;
+            cs += W->tp[r] * W->lp[r]; ++mc; W->cmax = fmax(W->cmax, W->tp[r] * W->lp[r]);
         }
         for (int i = 0; i < ns; ++i) W->rs[kp * ns + i] += gp[i];
         if (kp < N)
@@ -660,6 +668,9 @@ static int polish(const prob_t* P, work_t* W, double bs, double rho, double* kkt
         for (int i = 0; i < N * ns; ++i) fe = fmax(fe, fabs(W->re[i]));
         const double tf = 1e-12 * (1.0 + bs), td = 1e-9 * (1.0 + lmx);
         ok = isfinite(stat) && stat <= 1e-8 * (1.0 + gs) && viol <= tf && va <= tf && lneg >= -td && fe <= tf;
+        if (getenv("CPU_IPM_TRACE"))
+            fprintf(stderr, "polish round %d: stat %.3e (tol %.3e) viol %.3e act %.3e lneg %.3e lmax %.3e dyn %.3e -> %d\n",
+                    rd, stat, 1e-8 * (1.0 + gs), viol, va, lneg, lmx, fe, ok);
         if (ok) break;
         /* active-set correction: negative multipliers leave, violated rows enter */
         int ch = 0;
@@ -810,7 +821,7 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     for (it = 0; it <= op->max_iter; ++it) {
         residuals(P, W, &stat, &feas, &cs, &mc, &gs);
         mu = cs / (mc > 0 ? mc : 1);
-        if (stat <= op->tol_stat * (1.0 + gs) && feas <= op->tol_feas * (1.0 + bs) && mu <= op->tol_comp) { flag = 1; break; }
+        if (stat <= op->tol_stat * (1.0 + gs) && feas <= op->tol_feas * (1.0 + bs) && mu <= op->tol_comp && W->cmax <= CMAX_K * op->tol_comp) { flag = 1; break; }
         if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
         if (mu > MU_BLOWUP * mu_min && feas > FEAS_GUARD * (1.0 + bs)) { flag = -2; break; }
         if (mu < mu_min) mu_min = mu;

@@ -191,7 +191,7 @@ class GpuSolver:
     """One batched structured solve per step through bqp_solve_ocp_batched_device (inputs and
     outputs resident in HBM, caller stream)."""
 
-    def __init__(self, wl, local, precision):
+    def __init__(self, wl, local, precision, polish=True):
         import torch
         import bqp
         from bqp import _lib
@@ -228,7 +228,7 @@ class GpuSolver:
         self.oo = torch.empty((B * C.sizeof(_lib.Output),), dtype=torch.uint8, device=dev)
         self.lib = bqp.load()
         self.h = bqp.Handle(local)
-        self.opt = _lib.options(precision={'fp64': 0, 'fp32': 1, 'mixed': 2}[precision])
+        self.opt = _lib.options(precision={'fp64': 0, 'fp32': 1, 'mixed': 2}[precision], polish=polish)
         self.stream = torch.cuda.current_stream(dev)
 
     def step(self, with_out=False):
@@ -255,7 +255,8 @@ class GpuSolver:
         raw = self.oo.cpu().numpy().tobytes()
         out = (self._lib.Output * self.B).from_buffer_copy(raw)
         return dict(iterations=np.array([o.iterations for o in out]),
-                    kkt=np.array([list(o.kkt) for o in out]))
+                    kkt=np.array([list(o.kkt) for o in out]),
+                    polished=np.array([o.polished for o in out]))
 
 
 class StubSolver:
@@ -301,6 +302,8 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32', 'mixed'],
                     help='structured solver arithmetic (C5 compares both)')
+    ap.add_argument('--no-polish', action='store_true',
+                    help='interior-point iterates only (bqp_options.polish = -1)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
     args = ap.parse_args()
@@ -327,7 +330,7 @@ def main():
     wl = workload(args.config, args.batch, rank, world)
     prob, B = wl['prob'], wl['X'].shape[0]
     N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
-    solver = StubSolver(wl) if args.dry_run else GpuSolver(wl, local, args.precision)
+    solver = StubSolver(wl) if args.dry_run else GpuSolver(wl, local, args.precision, not args.no_polish)
 
     for _ in range(args.warmup):
         solver.step()
@@ -362,6 +365,9 @@ def main():
     check = {'converged_frac': float((flags == 1).mean()),
              'converged_frac_all_ranks': float((fl_all == 1).mean()),
              'infeasible_count_all_ranks': int((fl_all == -2).sum()),
+             # every exit flag of the whole job (quadprog meanings: 1 converged, 0 iteration
+             # limit, -2 primal infeasible, -8 numerical failure)
+             'exitflag_hist_all_ranks': {str(int(k)): int((fl_all == k).sum()) for k in np.unique(fl_all)},
              'gathered_rows': int(u0_all.shape[0])}
     if args.dry_run and rank == 0:
         # the gathered rows must equal the unsharded run of the same workload
@@ -382,7 +388,9 @@ def main():
                      kkt_primal_eq_max=float(kk[:, 1].max()),
                      kkt_primal_ineq_max=float(kk[:, 2].max()),
                      kkt_mu_max=float(kk[:, 3].max()),
-                     iterations_mean=float(o['iterations'].mean()))
+                     iterations_mean=float(o['iterations'].mean()),
+                     iterations_max=int(o['iterations'].max()),
+                     polished_count=int(o['polished'].sum()))
         if args.config == 'C2':
             g = np.load(os.path.join(GOLD, 'lmpc_N20.npz'))
             pos = {int(i): j for j, i in enumerate(g['idx'])}

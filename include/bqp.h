@@ -61,6 +61,14 @@ typedef struct {
                           long horizons (N >= 64), shorter ones are solved in fp64 */
     int want_duals;    /* reserved (set 0): the structured API writes the multiplier outputs
                           whenever its `duals` argument is non-NULL */
+    int polish;        /* structured API, fp64 active-set polish: the rows with lam > t are solved
+                          as equalities (augmented Lagrangian on the Riccati factorisation, with
+                          active-set corrections) and the result replaces the interior-point
+                          iterate if it passes the KKT checks (bqp_output.polished).
+                          0 (default) or 1: after an iteration-limit or numerical-failure exit
+                          (e.g. multipliers ~1e3-1e5 drive D = lam/t out of fp64 range);
+                          2: also when a row is left weakly active (slack and multiplier both
+                          above 1e-10); -1: off (interior-point iterate only) */
 } bqp_options;
 
 typedef struct {
@@ -70,6 +78,7 @@ typedef struct {
     double mu;               /* average complementarity at exit */
     double kkt[4];           /* stationarity, primal eq, primal ineq (inf-norms of the solver's
                                 residuals at exit), complementarity (average t.lam = mu) */
+    int polished;            /* 1: the answer is the active-set polish (bqp_options.polish) */
 } bqp_output;
 
 /* ------------------------------------------------------------------------------------------

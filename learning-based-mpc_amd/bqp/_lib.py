@@ -21,12 +21,13 @@ _PI = C.POINTER(C.c_int)
 class Options(C.Structure):
     _fields_ = [('max_iter', C.c_int), ('tol_stat', C.c_double), ('tol_feas', C.c_double),
                 ('tol_comp', C.c_double), ('tau', C.c_double), ('precision', C.c_int),
-                ('want_duals', C.c_int)]
+                ('want_duals', C.c_int), ('polish', C.c_int)]
 
 
 class Output(C.Structure):
     _fields_ = [('iterations', C.c_int), ('constrviolation', C.c_double),
-                ('firstorderopt', C.c_double), ('mu', C.c_double), ('kkt', C.c_double * 4)]
+                ('firstorderopt', C.c_double), ('mu', C.c_double), ('kkt', C.c_double * 4),
+                ('polished', C.c_int)]
 
 
 class OcpDims(C.Structure):
@@ -128,6 +129,13 @@ def load():
     return lib
 
 
+def ocp_dims_supported(nx, nu, np_, N, mp):
+    """the structured kernels' compiled set (csrc/bqp_api.cpp: ocp_supported, N + 1 <= 128,
+    at most 1024 polytope rows): outside it bqp_solve_ocp_batched answers BQP_E_UNSUPPORTED by
+    design"""
+    return ((nx, nu, np_) in ((4, 1, 1), (2, 2, 2))) and N + 1 <= 128 and mp <= 1024
+
+
 def check(rc, what):
     if rc != BQP_OK:
         raise BqpError('%s failed: %s (%d)' % (what, _ERR.get(rc, 'error'), rc))
@@ -185,11 +193,13 @@ class Handle:
 
 
 def options(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995,
-            want_duals=0, precision=0):
-    """precision: 0 fp64, 1 fp32 (structured solver; see include/bqp.h)"""
+            want_duals=0, precision=0, polish=1):
+    """precision: 0 fp64, 1 fp32 (structured solver; see include/bqp.h); polish (bqp_options
+    .polish): 1 after 0 / -8 exits (default), 2 also with weakly active rows, 0/False off"""
     o = Options()
     load().bqp_default_options(C.byref(o))
     o.max_iter, o.tol_stat, o.tol_feas, o.tol_comp, o.tau = max_iter, tol_stat, tol_feas, tol_comp, tau
     o.want_duals = want_duals
     o.precision = precision
+    o.polish = -1 if polish is False or polish == 0 else int(polish)
     return o

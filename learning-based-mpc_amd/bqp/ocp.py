@@ -100,6 +100,8 @@ def solve_ocp(prob, x0, w=None, hp=None, A=None, B=None, handle=None, want_duals
     fval, exitflag, iterations, firstorderopt, constrviolation, mu[, pi, lam_x, lam_u, lam_p]).
     route: 'auto' (structured kernel; condensed when the C ABI reports the dimensions
     unsupported), 'structured' (no condensed route) or 'condensed'."""
+    if route not in ('auto', 'structured', 'condensed'):
+        raise ValueError("route must be 'auto', 'structured' or 'condensed', not %r" % (route,))
     lib = _lib.load()
     h = handle or _default_handle()
     dims, data, batch, keep = pack(prob, x0, w, hp, A, B, Fp, W)
@@ -119,14 +121,19 @@ def solve_ocp(prob, x0, w=None, hp=None, A=None, B=None, handle=None, want_duals
     rc = lib.bqp_solve_ocp_batched(h.value, C.byref(dims), batch, C.byref(data), C.byref(o),
                                    _lib.ptr(x), _lib.ptr(u), _lib.ptr(th), _lib.ptr(fval),
                                    _lib.iptr(flag), out, C.byref(duals) if duals else None)
-    if rc == _lib.BQP_E_UNSUPPORTED and route == 'auto':
+    # the condensed route takes only x0 and hp per instance: anything else keeps the structured
+    # solver's own error (an LDS fit failure is not a reason to change the algorithm)
+    condensable = all(v is None for v in (w, A, B, Fp, W)) and not want_duals
+    if rc == _lib.BQP_E_UNSUPPORTED and route == 'auto' and condensable and \
+            not _lib.ocp_dims_supported(prob.nx, prob.nu, prob.np, prob.N, prob.mp):
         return solve_ocp_condensed(prob, x0, w, hp, A, B, handle, want_duals, Fp, W, **opts)
     _lib.check(rc, 'bqp_solve_ocp_batched')
     res = OcpResult(x=x, u=u, theta=th, fval=fval + prob.const, exitflag=flag,
                     iterations=np.array([o_.iterations for o_ in out]),
                     firstorderopt=np.array([o_.firstorderopt for o_ in out]),
                     constrviolation=np.array([o_.constrviolation for o_ in out]),
-                    mu=np.array([o_.mu for o_ in out]))
+                    mu=np.array([o_.mu for o_ in out]),
+                    polished=np.array([o_.polished for o_ in out], dtype=np.int32))
     if want_duals:
         dd['lam_p'] = dd['lam_p'][:, :mp]
         res.update(dd)

@@ -80,6 +80,7 @@ void resolve(const bqp_options* in, bqp_options* o) {
     if (in->tau > 0 && in->tau < 1) o->tau = in->tau;
     o->precision = in->precision;
     o->want_duals = in->want_duals;
+    o->polish = in->polish;
 }
 
 #define HIP_TRY(x)                                                        \
@@ -106,6 +107,7 @@ void bqp_default_options(bqp_options* o) {
     o->tau = 0.995;
     o->precision = 0;
     o->want_duals = 0;
+    o->polish = 0;
 }
 
 int bqp_create(bqp_handle* h, int device) {
@@ -295,6 +297,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     a.Pg = Pg; a.sh_F = LS.sh_F; a.sh_hp = LS.sh_hp; a.sh_bnd = LS.sh_bnd; a.H_inst = Hinst;
     a.max_iter = o.max_iter; a.tol_stat = o.tol_stat; a.tol_feas = o.tol_feas;
     a.tol_comp = o.tol_comp; a.tau = o.tau;
+    a.polish = o.polish < 0 ? 0 : (o.polish == 0 ? 1 : std::min(o.polish, 2));
     a.H = Hd; a.Fp = Fd;
     a.A = D->A; a.B = D->B; a.c = D->c; a.w = D->w; a.xlb = D->xlb; a.xub = D->xub;
     a.ulb = D->ulb; a.uub = D->uub; a.hp = mp > 0 ? D->hp : Hd; a.x0 = D->x0;

@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
         double* so = a.stats + (int64_t)inst * STATS_W;
-        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin;
+        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin; so[6] = 0.0;
     }
 }
 
@@ -957,7 +957,7 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
         double* so = a.stats + (int64_t)inst * STATS_W;
-        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin;
+        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin; so[6] = 0.0;
     }
 }
 

@@ -8,8 +8,8 @@ namespace bqp {
 
 // per-instance exit statistics written by every solve kernel and turned into bqp_output by
 // finalize_kernel: iterations, stationarity, max(primal eq, primal ineq), mu, primal eq,
-// primal ineq (inf-norms at exit)
-constexpr int STATS_W = 6;
+// primal ineq (inf-norms at exit), 1 if the answer is the structured solver's active-set polish
+constexpr int STATS_W = 7;
 
 // Structured OCP kernel arguments (device pointers).  H and Fp are the prepared shared tables:
 //   H  : (N+1) stages x hstride doubles, stage cost in internal order [x; theta; u], row-major
@@ -53,6 +53,9 @@ struct OcpKernelArgs {
     // per-instance stage costs (bqp_ocp_data.sW != 0): prepared tables batch x (N+1) x hstride;
     // short horizons copy the instance's table into its LDS slot, long ones read it from L2
     const double* H_inst;
+    // active-set polish (fp64 instantiation, bqp_options.polish): 0 off, 1 after a 0 / -8 exit,
+    // 2 also with a weakly active row
+    int polish;
 };
 
 bool ocp_supported(int nx, int nu, int np);

@@ -64,6 +64,36 @@ namespace dp {
 #define PIV_FLOOR 1e-14
 #endif
 #define MU_BLOWUP 1e6
+// round 3 safeguards (oracle/cpu_ipm.c states the same rules):
+//   -2 only while the rows are still infeasible above FEAS_GUARD (1 + |data|) (was 1e-6: nearly
+//   infeasible Monte-Carlo models ended 0 after 50 iterations);
+//   convergence needs every row's t lam <= CMAX_K tol_comp besides the average mu;
+//   a predictor step below SOC_ALPHA on a feasible iterate drops the corrector's second-order
+//   term (pure centring: the alternating stall of nearly degenerate rows);
+//   the active-set polish (fp64 only) after a 0 / -8 exit (bqp_options.polish 2: also with a
+//   weakly active row).
+#ifdef BQP_F32
+#define FEAS_GUARD 1e-6
+#define BQP_POLISH 0
+#else
+#define FEAS_GUARD 1e-8
+#define BQP_POLISH 1
+#endif
+#ifndef BQP_EXP_NOROW
+#define BQP_EXP_NOROW 0
+#endif
+#ifndef BQP_EXP_NOSTAGE
+#define BQP_EXP_NOSTAGE 0
+#endif
+#ifndef BQP_POLISH_CODE
+#define BQP_POLISH_CODE BQP_POLISH
+#endif
+#define CMAX_K 100.0
+#define SOC_ALPHA 0.1
+#define DEG_POLISH 1e-10
+#define POL_RHO 2e6
+#define POL_ALM 8
+#define POL_ROUNDS 4
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
 // 1/t for the row slacks and multipliers (t > 0 inside the IPM): hardware reciprocal estimate
@@ -139,7 +169,19 @@ enum : int {
     X_CS,        // sum t.lam over the rows (row wave, per iteration)
     X_STOP,      // 1: leave the loop at B2 (stage wave)
     X_ALPHA,     // corrector step length (row wave)
-    X_NXCH = 8
+    X_CMAX,      // max t.lam over the rows (row wave, per iteration)
+    X_FEASOK,    // 1: the iterate is primal feasible to FEAS_GUARD (stage wave, per iteration)
+    X_FLAG,      // exit flag of the IPM (stage wave, at the stop)
+    X_RHO,       // polish weight rho (stage wave, at the stop)
+    X_TF,        // polish feasibility tolerance 1e-12 (1 + |data|) (stage wave)
+    X_DEG,       // max over rows of min(t, lam) at the exit (row wave)
+    X_PVA,       // polish: max |C v - b| over the active rows (row wave)
+    X_PVIOL,     //         max (C v - b) over all rows
+    X_PLNEG,     //         min multiplier over the active rows
+    X_PLMX,      //         max multiplier over the active rows
+    X_PCHG,      //         rows an active-set correction would move
+    X_PDEC,      //         decision (stage wave): 0 step, 1 accept, 2 correct the set, 3 give up
+    X_NXCH = 18
 };
 
 // Per-instance LDS layout (in doubles), sized from N at run time.
@@ -1115,7 +1157,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         if (flag != 0) {
             stop = true;
         } else if (stat <= a.tol_stat * (1.0 + gsA) && feas <= a.tol_feas * (1.0 + bscale) &&
-                   mu <= a.tol_comp) {
+                   mu <= a.tol_comp && (!BQP_POLISH || X[X_CMAX] <= CMAX_K * a.tol_comp)) {
             flag = 1; stop = true;
 #ifdef BQP_F32
         } else if (mu <= a.tol_comp && feas <= a.tol_feas * (1.0 + bscale) && isfinite(stat)) {
@@ -1126,7 +1168,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #endif
         } else if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) {
             flag = -8; stop = true;
-        } else if (mu > MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) {
+        } else if (mu > MU_BLOWUP * mu_min && feas > FEAS_GUARD * (1.0 + bscale)) {
             flag = -2; stop = true;
         } else {
             mu_min = fmin(mu_min, mu);
@@ -1135,7 +1177,13 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         if (!stop && !factor()) { flag = -8; stop = true; }
         if (!stop) prep_iter();
         STAMP(3);
-        if (lane == 0) X[X_STOP] = stop ? 1.0 : 0.0;
+        if (lane == 0) {
+            X[X_STOP] = stop ? 1.0 : 0.0;
+            X[X_FEASOK] = (feas <= FEAS_GUARD * (1.0 + bscale)) ? 1.0 : 0.0;
+            X[X_FLAG] = (real)flag;
+            X[X_RHO] = POL_RHO * (1.0 + gsA);
+            X[X_TF] = 1e-12 * (1.0 + bscale);
+        }
         BARRIER();                                        // B2: predictor rhs ready; stop flag
         STAMP(4);
         if (stop) break;
@@ -1155,6 +1203,96 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         write_state();
         stage_partials(feasA, gsA);
         STAMP(9);
+    }
+
+    // ======================= active-set polish (fp64) ========================================
+    // oracle/cpu_ipm.c polish(): rows with lam > t are equalities, the others are dropped; the
+    // equality-constrained QP is solved by augmented-Lagrangian steps on the Riccati machinery
+    // (D = rho on the active rows, e = rho (C v - b), multipliers nu += rho (C v - b) by the row
+    // wave after each step); negative multipliers leave the set and violated rows enter it.
+    // The polished point replaces the IPM iterate only if it passes the KKT checks.
+    real polished = 0.0;
+    bool pi_kept = false;                                 // pi_out already holds the IPM's pi
+    if constexpr (BQP_POLISH_CODE && !BQP_EXP_NOSTAGE) {
+        BARRIER();                                        // Q0: row wave published max min(t, lam)
+        const bool dopol = a.polish > 0 && flag != -2 &&
+                           (flag != 1 || (a.polish > 1 && X[X_DEG] > DEG_POLISH)) && isfinite(gsA);
+        if (dopol) {
+            STAMP(15);
+            // the IPM iterate for the fall-back: s, u in the predictor-direction slots; pi goes
+            // to its output now (overwritten below only if the polish is accepted)
+#pragma unroll
+            for (int j = 0; j < SPL; ++j) {
+                const int k = lane + WAVE * j;
+                if (a.pi_out && k >= 1 && k <= N) {
+                    double* po = a.pi_out + ((int64_t)inst * N + (k - 1)) * NX;
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) po[i] = pi[j][i];
+                }
+                if (k <= N) {
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) W[L.dsv + k * NS + i] = s[j][i];
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) W[L.duv + k * NU + i] = (k < N) ? u[j][i] : 0.0;
+                }
+            }
+            const real tf = 1e-12 * (1.0 + bscale);
+            int rd = 0, jj = 0, dec = 0;
+            bool pfail = false, fresh = false;
+            real va_prev = INFINITY, pst = 0.0;
+            for (;;) {
+                // combine() adds the row terms into the stage residuals in place: they are
+                // re-formed before every use
+                if (!fresh) stage_partials(feasA, gsA);
+                fresh = false;
+                BARRIER();                                // P_B: row tables of (v, nu) ready
+                pst = combine();
+                const real va = X[X_PVA];
+                if (pfail) {
+                    dec = 3;
+                } else if (jj == 0 || (jj < POL_ALM && va > 1e-14 * (1.0 + bscale) && va < 0.5 * va_prev)) {
+                    dec = 0;
+                } else {
+                    const bool ok = isfinite(pst) && pst <= a.tol_stat * (1.0 + gsA) && X[X_PVIOL] <= tf &&
+                                    va <= tf && X[X_PLNEG] >= -1e-9 * (1.0 + X[X_PLMX]) && feasA <= tf;
+                    dec = ok ? 1 : ((rd + 1 < POL_ROUNDS && X[X_PCHG] > 0.0) ? 2 : 3);
+                }
+                va_prev = (jj == 0) ? INFINITY : va;      // the first step of a round always runs
+                if (lane == 0) X[X_PDEC] = (real)dec;
+                BARRIER();                                // P_C: decision out
+                if (dec == 1 || dec == 3) break;
+                if (dec == 2) { ++rd; jj = 0; va_prev = INFINITY; continue; }
+                if (jj == 0 && !factor()) pfail = true;
+                if (!pfail) {
+                    prep_iter();
+                    solve(L.dsc, L.duc);
+                    dual_dir(L.dsc);
+                    update_stage_dir(1.0, L.dsc, L.duc);
+                    write_state();
+                    stage_partials(feasA, gsA);
+                    fresh = true;
+                }
+                ++jj;
+                BARRIER();                                // P_D: the stepped stage vectors
+            }
+            if (dec == 1) {
+                polished = 1.0;
+                flag = 1;
+                stat = pst; feas = fmax(feasA, X[X_PVIOL]); mu = 0.0; feq = feasA; fin = X[X_PVIOL];
+            } else {
+                pi_kept = true;
+#pragma unroll
+                for (int j = 0; j < SPL; ++j) {
+                    const int k = lane + WAVE * j;
+                    if (k <= N) {
+#pragma unroll
+                        for (int i = 0; i < NS; ++i) s[j][i] = W[L.dsv + k * NS + i];
+#pragma unroll
+                        for (int i = 0; i < NU; ++i) u[j][i] = (k < N) ? W[L.duv + k * NU + i] : 0.0;
+                    }
+                }
+            }
+        }
     }
 
     // ======================= outputs =======================================================
@@ -1208,7 +1346,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             for (int c = 0; c < NV; ++c) hv += BQP_HV(i * NV + c) * v[c];
             fv += v[i] * (0.5 * hv + gterm(k, i));
         }
-        if (a.pi_out && k >= 1) {
+        if (a.pi_out && k >= 1 && !pi_kept) {
             double* po = a.pi_out + ((int64_t)inst * N + (k - 1)) * NX;
 #pragma unroll
             for (int i = 0; i < NX; ++i) po[i] = pi[j][i];
@@ -1222,6 +1360,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         if (a.stats) {
             double* so = a.stats + (int64_t)inst * STATS_W;
             so[0] = (double)(it + it0); so[1] = stat; so[2] = feas; so[3] = mu; so[4] = feq; so[5] = fin;
+            so[6] = polished;
         }
     }
 }
@@ -1324,9 +1463,12 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     // residuals are re-formed from the LDS stage vector and bounds when needed)
     real tx[BPL], lx[BPL];
     real tp[RPL], lp[RPL], rp[RPL];
+    // 1: the corrector carries Mehrotra's second-order term dt_a dlam_a; 0: this iteration's
+    // predictor step was short on a feasible iterate, the corrector is a pure centring step
+    real socf = 1.0;
     auto prp_get = [&](int q, int r) __attribute__((always_inline)) -> real {
         (void)q;
-        return W[L.prp + r];
+        return socf * W[L.prp + r];
     };
 #pragma unroll
     for (int b = 0; b < BPL; ++b) { tx[b] = 1.0; lx[b] = 1.0; }
@@ -1336,7 +1478,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     // ---- multiplier-side tables (depend on t, lam only): box multipliers, Fp'lam, 1/t,
     //      D = lam/t per stage, F'DF, sum t.lam ----
     auto lam_side = [&]() __attribute__((always_inline)) {
-        real cs = 0.0;
+        real cs = 0.0, cm = 0.0;
 #pragma unroll
         for (int pv = 0; pv < BPL / 2; ++pv) {
             ROW_FENCE(pv);
@@ -1348,6 +1490,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 if (bpres(b)) {
                     d += lx[b] * frcp(tx[b]);
                     cs += tx[b] * lx[b];
+                    if constexpr (BQP_POLISH) cm = fmax(cm, tx[b] * lx[b]);
                 }
                 if constexpr (LNG) {
                     if (bpres(b)) blv += h ? -lx[b] : lx[b];
@@ -1380,6 +1523,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpp[c] += f[c] * lp[q];
                 cs += tp[q] * lp[q];
+                if constexpr (BQP_POLISH) cm = fmax(cm, tp[q] * lp[q]);
                 const real d = lp[q] * frcp(tp[q]);
                 int idx = 0;
 #pragma unroll
@@ -1416,6 +1560,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             W[L.FD + j2 * NV + i2] = tot;
         } else if (lane == NV + NT) {
             X[X_CS] = tot;
+        }
+        if constexpr (BQP_POLISH) {
+            cm = wmax(cm);                                // per-row complementarity (stop test)
+            if (lane == 0) X[X_CMAX] = cm;
         }
     };
 
@@ -1462,10 +1610,13 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         return -box_res(b) - ((bcode(b) & 1) == 0 ? dv : -dv);
     };
     // box-row predictor product dt_a * dlam_a (recomputed from the predictor direction)
-    auto box_pred_prod = [&](int b) __attribute__((always_inline)) -> real {
+    auto box_pred_raw = [&](int b) __attribute__((always_inline)) -> real {
         const real dt = box_dir(b, L.dsv, L.duv);
         const real dl = (-(tx[b] * lx[b]) - lx[b] * dt) * frcp(tx[b]);
         return dt * dl;
+    };
+    auto box_pred_prod = [&](int b) __attribute__((always_inline)) -> real {
+        return socf * box_pred_raw(b);
     };
 
     // ---- right-hand-side terms (lam o ri - rc)/t: box [upper, lower] per stage, Fp'e ----
@@ -1644,7 +1795,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     //      entries once for both): residual by the linear update r + a (Fp dv + dt), t, lam,
     //      then Fp'lam, F'DF, sum t.lam exactly as lam_side; feb = the box rows' residual norm ----
     auto poly_apply_lam = [&](real smu, real al, real feb) __attribute__((always_inline)) {
-        real cs = 0.0;
+        real cs = 0.0, cm = 0.0;
 #pragma unroll
         for (int pv = 0; pv < BPL / 2; ++pv) {
             ROW_FENCE(pv);
@@ -1655,6 +1806,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 if (bpres(b)) {
                     d += lx[b] * frcp(tx[b]);
                     cs += tx[b] * lx[b];
+                    if constexpr (BQP_POLISH) cm = fmax(cm, tx[b] * lx[b]);
                 }
                 if constexpr (LNG) {
                     if (bpres(b)) blv += h ? -lx[b] : lx[b];
@@ -1700,6 +1852,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpp[c] += f[c] * lp[q];
                 cs += tp[q] * lp[q];
+                if constexpr (BQP_POLISH) cm = fmax(cm, tp[q] * lp[q]);
                 const real d = lp[q] * frcp(tp[q]);
                 int idx = 0;
 #pragma unroll
@@ -1736,6 +1889,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         } else if (lane == NV + NT) {
             X[X_CS] = tot;
         }
+        if constexpr (BQP_POLISH) {
+            cm = wmax(cm);
+            if (lane == 0) X[X_CMAX] = cm;
+        }
     };
 
     auto rhs_corr_finish = [&](real smu, real tot) __attribute__((always_inline)) {
@@ -1755,6 +1912,38 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         // tot (from the joint reduction): lane 2c = Fp'e0 (c), lane 2c+1 = Fp'(1/t) (c)
         const real other = dpp_mov<0xB1, 0xf>(real(0), tot);
         if (lane < 2 * NV && (lane & 1) == 0) W[L.gpe + lane / 2] = tot + smu * other;
+    };
+    // pure centring step (socf = 0): the predictor pass formed the corrector terms with
+    // dt_a dlam_a; take it back out, (lam ri - rc - pr)/t + pr/t (rare: short predictor steps)
+    auto rhs_drop_soc = [&]() __attribute__((always_inline)) {
+        if constexpr (LNG) {
+#pragma unroll
+            for (int pv = 0; pv < BPL / 2; ++pv) {
+                real add = 0.0;
+                if (bpres(2 * pv)) add += box_pred_raw(2 * pv) * frcp(tx[2 * pv]);
+                if (bpres(2 * pv + 1)) add -= box_pred_raw(2 * pv + 1) * frcp(tx[2 * pv + 1]);
+                if (binrange(2 * pv)) W[L.ebox + lane + WAVE * pv] += add;
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < BPL; ++b)
+                if (bpres(b)) W[L.ebox + brow(b)] += box_pred_raw(b) * frcp(tx[b]);
+        }
+        real gc[NV];
+#pragma unroll
+        for (int c = 0; c < NV; ++c) gc[c] = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int r = lane + WAVE * q;
+            if (r >= mp) continue;
+            const real e = W[L.prp + r] * frcp(tp[q]);
+#pragma unroll
+            for (int c = 0; c < NV; ++c) gc[c] += Fs[c * mpad + r] * e;
+        }
+        const real tot = wsum_t(gc, lane);
+        wave_sync();
+        if (lane < NV) W[L.gpe + lane] += tot;
+        wave_sync();
     };
 
     // ======================= initial point ==================================================
@@ -1859,6 +2048,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         sg = sg * sg * sg;
         const real smu = sg * mu;
         rhs_corr_finish(smu, tot);
+        socf = (BQP_POLISH && al_aff < SOC_ALPHA && X[X_FEASOK] != 0.0) ? 0.0 : 1.0;
+        if (socf == 0.0) rhs_drop_soc();
         STAMP(5);
         BARRIER();                                        // B4
         BARRIER();                                        // B5: corrector direction in (dsc, duc)
@@ -1891,26 +2082,229 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         STAMP_STORE(16);
         return;
     }
+    // multipliers of the box rows [lower; upper] per stage and of the polytope rows
+    auto out_duals = [&](const real (&lb)[BPL], const real (&lq)[RPL]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int b = 0; b < BPL; ++b) {
-        ROW_FENCE(b);
-        if (!binrange(b)) continue;
-        const int vi = lane + WAVE * (b >> 1), h = b & 1;
-        const int k = vi / NB, sl = vi - k * NB;
-        const real lv = bpres(b) ? lx[b] : 0.0;      // layout per stage: [lower; upper]
-        if (sl < NX) {
-            if (a.lamx_out) a.lamx_out[((int64_t)inst * (N + 1) + k) * NX * 2 + (h ? sl : NX + sl)] = lv;
-        } else if (k < N) {
-            if (a.lamu_out) a.lamu_out[((int64_t)inst * N + k) * NU * 2 + (h ? sl - NX : NU + sl - NX)] = lv;
+        for (int b = 0; b < BPL; ++b) {
+            ROW_FENCE(b);
+            if (!binrange(b)) continue;
+            const int vi = lane + WAVE * (b >> 1), h = b & 1;
+            const int k = vi / NB, sl = vi - k * NB;
+            const real lv = bpres(b) ? lb[b] : 0.0;      // layout per stage: [lower; upper]
+            if (sl < NX) {
+                if (a.lamx_out) a.lamx_out[((int64_t)inst * (N + 1) + k) * NX * 2 + (h ? sl : NX + sl)] = lv;
+            } else if (k < N) {
+                if (a.lamu_out) a.lamu_out[((int64_t)inst * N + k) * NU * 2 + (h ? sl - NX : NU + sl - NX)] = lv;
+            }
+        }
+        if (a.lamp_out) {
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const int r = lane + WAVE * q;
+                if (r < mp) a.lamp_out[(int64_t)inst * mp + r] = lq[q];
+            }
+        }
+    };
+
+    // ======================= active-set polish (fp64): row side ==============================
+    if constexpr (BQP_POLISH_CODE && !BQP_EXP_NOROW) {
+        // max over rows of min(t, lam): a weakly active row keeps both ~ sqrt(mu) at the exit
+        real dg = 0.0;
+#pragma unroll
+        for (int b = 0; b < BPL; ++b)
+            if (bpres(b)) dg = fmax(dg, fmin(tx[b], lx[b]));
+#pragma unroll
+        for (int q = 0; q < RPL; ++q)
+            if (prow(q)) dg = fmax(dg, fmin(tp[q], lp[q]));
+        dg = wmax(dg);
+        if (lane == 0) X[X_DEG] = dg;
+        BARRIER();                                        // Q0
+        const int flag = (int)X[X_FLAG];
+        const bool dopol = a.polish > 0 && flag != -2 &&
+                           (flag != 1 || (a.polish > 1 && X[X_DEG] > DEG_POLISH)) && isfinite(X[X_RHO]);
+        if (dopol) {
+            STAMP(15);
+            // the IPM's multipliers go out now (the fall-back); the row state is dead after this
+            out_duals(lx, lp);
+            const real rho = X[X_RHO], tf = X[X_TF];
+            unsigned bact = 0, pact = 0;                 // rows taken as equalities
+            real nb[BPL], npq[RPL];                       // their multipliers (0 on dropped rows)
+            real lmx_r = 0.0;
+#pragma unroll
+            for (int b = 0; b < BPL; ++b) {
+                const bool ac = bpres(b) && lx[b] > tx[b];
+                if (ac) bact |= 1u << b;
+                nb[b] = ac ? lx[b] : real(0);
+            }
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const bool ac = prow(q) && lp[q] > tp[q];
+                if (ac) pact |= 1u << q;
+                npq[q] = ac ? lp[q] : real(0);
+            }
+            // constraint values C v - b of the current stage vectors (t = 0), multiplier update
+            // (mode 1: nu += rho (C v - b)) or active-set correction (mode 2), then the tables
+            // the stage wave reads: box multipliers / diagonal / rhs terms, Fp'nu, Fp'e and
+            // (modes 0, 2: a new set) F'DF; the check values to the exchange block
+            auto pol_tables = [&](int mode) __attribute__((always_inline)) {
+                const real td = 1e-9 * (1.0 + lmx_r);
+                real va = 0.0, vio = 0.0, ln = 0.0, lm = 0.0, chg = 0.0;
+#pragma unroll
+                for (int pv = 0; pv < BPL / 2; ++pv) {
+                    ROW_FENCE(pv);
+                    real d = 0.0, blv = 0.0, ev[2] = {0.0, 0.0};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int b = 2 * pv + h;
+                        if (!bpres(b)) continue;
+                        const real v = bvar(b, L.xs, L.xu);
+                        const real bd = bndp[brow(b)];
+                        const real ri = h == 0 ? v - bd : -v + bd;
+                        bool ac = (bact >> b) & 1u;
+                        if (mode == 1 && ac) nb[b] += rho * ri;
+                        if (mode == 2) {
+                            if (ac && nb[b] < -td) { bact &= ~(1u << b); nb[b] = 0.0; ac = false; }
+                            else if (!ac && ri > tf) { bact |= 1u << b; ac = true; }
+                        }
+                        vio = fmax(vio, ri);
+                        if (ac) {
+                            va = fmax(va, fabs(ri)); ln = fmin(ln, nb[b]); lm = fmax(lm, nb[b]);
+                            d += rho;
+                            ev[h] = rho * ri;
+                        } else if (ri > tf) {
+                            chg += 1.0;
+                        }
+                        blv += h ? -nb[b] : nb[b];
+                    }
+                    if constexpr (LNG) {
+                        if (binrange(2 * pv)) {
+                            W[L.blam + lane + WAVE * pv] = blv;
+                            W[L.ebox + lane + WAVE * pv] = ev[0] - ev[1];
+                        }
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int b = 2 * pv + h;
+                            if (binrange(b)) {
+                                W[L.blam + brow(b)] = bpres(b) ? nb[b] : 0.0;
+                                W[L.ebox + brow(b)] = ev[h];
+                            }
+                        }
+                    }
+                    if (binrange(2 * pv)) {
+                        const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
+                        W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
+                    }
+                }
+                real vp[NV];
+                load_v(vp, L.xs, L.xu);
+                constexpr int NT = NV * (NV + 1) / 2;
+                real red[2 * NV], rfd[NT];                // [Fp'nu, Fp'e], F'DF (wsum_t: <= 32 values)
+#pragma unroll
+                for (int c = 0; c < 2 * NV; ++c) red[c] = 0.0;
+#pragma unroll
+                for (int c = 0; c < NT; ++c) rfd[c] = 0.0;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    ROW_FENCE(q);
+                    const int r = lane + WAVE * q;
+                    if (r >= mp) continue;
+                    real f[NV];
+#pragma unroll
+                    for (int c = 0; c < NV; ++c) f[c] = Fs[c * mpad + r];
+                    real fv = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NV; ++c) fv += f[c] * vp[c];
+                    const real ri = fv - hpi[r];
+                    bool ac = (pact >> q) & 1u;
+                    if (mode == 1 && ac) npq[q] += rho * ri;
+                    if (mode == 2) {
+                        if (ac && npq[q] < -td) { pact &= ~(1u << q); npq[q] = 0.0; ac = false; }
+                        else if (!ac && ri > tf) { pact |= 1u << q; ac = true; }
+                    }
+                    vio = fmax(vio, ri);
+                    real e = 0.0;
+                    if (ac) {
+                        va = fmax(va, fabs(ri)); ln = fmin(ln, npq[q]); lm = fmax(lm, npq[q]);
+                        e = rho * ri;
+                    } else if (ri > tf) {
+                        chg += 1.0;
+                    }
+#pragma unroll
+                    for (int c = 0; c < NV; ++c) { red[c] += f[c] * npq[q]; red[NV + c] += f[c] * e; }
+                    if (mode != 1 && ac) {
+                        int idx = 0;
+#pragma unroll
+                        for (int i2 = 0; i2 < NV; ++i2) {
+                            const real di = rho * f[i2];
+#pragma unroll
+                            for (int j2 = i2; j2 < NV; ++j2) rfd[idx++] += di * f[j2];
+                        }
+                    }
+                }
+                // Fp'nu, Fp'e (and, for a new set, F'DF) by transposed wave sums
+                {
+                    const real tot = wsum_t(red, lane);
+                    if (lane < NV) W[L.gpp + lane] = tot;
+                    else if (lane < 2 * NV) W[L.gpe + lane - NV] = tot;
+                }
+                if (mode != 1) {
+                    const real tot = wsum_t(rfd, lane);
+                    if (lane < NT) {
+                        const int idx = lane;
+                        int i2 = 0, st = 0;
+#pragma unroll
+                        for (int r = 1; r < NV; ++r) {
+                            const int sr = r * NV - r * (r - 1) / 2;
+                            if (idx >= sr) { i2 = r; st = sr; }
+                        }
+                        const int j2 = i2 + (idx - st);
+                        W[L.FD + i2 * NV + j2] = tot;
+                        W[L.FD + j2 * NV + i2] = tot;
+                    }
+                }
+                va = wmax(va); vio = wmax(vio); lm = wmax(lm); ln = wmin(ln);
+                // rows a correction would move: violated dropped rows (counted above) and
+                // active rows whose multiplier is negative beyond this point's tolerance
+                const real tdn = 1e-9 * (1.0 + lm);
+#pragma unroll
+                for (int b = 0; b < BPL; ++b)
+                    if (((bact >> b) & 1u) && nb[b] < -tdn) chg += 1.0;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q)
+                    if (((pact >> q) & 1u) && npq[q] < -tdn) chg += 1.0;
+                chg = wsum(chg);
+                lmx_r = lm;
+                if (lane == 0) {
+                    X[X_PVA] = va; X[X_PVIOL] = vio; X[X_PLNEG] = ln; X[X_PLMX] = lm; X[X_PCHG] = chg;
+                }
+                wave_sync();
+            };
+            pol_tables(0);
+            for (;;) {
+                BARRIER();                                // P_B
+                BARRIER();                                // P_C
+                const int dec = (int)X[X_PDEC];
+                if (dec == 1) {
+                    // polished: the active rows' multipliers (>= 0), 0 on the dropped rows
+#pragma unroll
+                    for (int b = 0; b < BPL; ++b) nb[b] = fmax(nb[b], real(0));
+#pragma unroll
+                    for (int q = 0; q < RPL; ++q) npq[q] = fmax(npq[q], real(0));
+                    out_duals(nb, npq);
+                    break;
+                }
+                if (dec == 3) break;
+                if (dec == 2) { pol_tables(2); continue; }
+                BARRIER();                                // P_D
+                pol_tables(1);
+            }
+            STAMP_STORE(16);
+            return;
         }
     }
-    if (a.lamp_out) {
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-            const int r = lane + WAVE * q;
-            if (r < mp) a.lamp_out[(int64_t)inst * mp + r] = lp[q];
-        }
-    }
+    out_duals(lx, lp);
+
     STAMP_STORE(16);
 }
 

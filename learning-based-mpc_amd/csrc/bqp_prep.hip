@@ -103,6 +103,7 @@ __global__ void finalize_kernel(const double* __restrict__ stats, int batch, bqp
     o.kkt[1] = s[4];
     o.kkt[2] = s[5];
     o.kkt[3] = s[3];
+    o.polished = (int)s[6];
     out[b] = o;
 }
 

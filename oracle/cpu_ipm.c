@@ -31,7 +31,7 @@
 #define CMAX_K 100.0     /* and every row: t_i lam_i <= CMAX_K tol_comp (the average alone lets one */
 #endif            /* weakly active row keep t ~ 1e-10: first moves off by 1e-7 at N = 100) */
 #ifndef DEG_POLISH
-#define DEG_POLISH 1e-10  /* polish a converged iterate whose max_i min(t_i, lam_i) exceeds this  */
+#define DEG_POLISH 1e-10  /* polish = 2: also a converged iterate with max_i min(t_i, lam_i) > this */
 #endif
 #define POL_RHO 2e6       /* polish weight rho = POL_RHO (1 + |H v + g|_inf)                      */
 #define POL_ALM 8         /* augmented-Lagrangian iterations per polish round (at most)           */
@@ -884,9 +884,10 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
                     }
         for (int r = 0; r < P->mp; ++r) { W->tp[r] += a * W->dtp[r]; W->lp[r] += a * W->dlp[r]; }
     }
-    if (flag != -2 && op->polish) {
-        /* polish when the IPM did not converge (0 / -8: the factorisation left fp64 range) or
-         * converged with a weakly active row (max_i min(t_i, lam_i) > DEG_POLISH) */
+    if (flag != -2 && op->polish > 0) {
+        /* polish when the IPM did not converge (0 / -8: the factorisation left fp64 range) and,
+         * with polish = 2, when it converged with a weakly active row
+         * (max_i min(t_i, lam_i) > DEG_POLISH) */
         double degm = 0.0;
         for (int k = 0; k <= N; ++k)
             for (int i = 0; i < nx; ++i)
@@ -897,7 +898,7 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
                 for (int h = 0; h < 2; ++h)
                     if (PRESENT_U(k, i, h)) { const int o = (k * nu + i) * 2 + h; degm = fmax(degm, fmin(W->tu[o], W->lu[o])); }
         for (int r = 0; r < P->mp; ++r) degm = fmax(degm, fmin(W->tp[r], W->lp[r]));
-        if (flag != 1 || degm > DEG_POLISH) {
+        if (flag != 1 || (op->polish > 1 && degm > DEG_POLISH)) {
             double k3p[3];
             if (isfinite(gs) && polish(P, W, bs, POL_RHO * (1.0 + gs), k3p)) {
                 flag = 1; stat = k3p[0]; feas = k3p[1]; mu = k3p[2];

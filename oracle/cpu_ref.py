@@ -84,9 +84,10 @@ def pack_ocp(ocp, x0, w=None, hp=None, A=None, B=None):
 
 
 def solve(ocp, x0, w=None, hp=None, A=None, B=None, max_iter=50, tol_stat=1e-8,
-          tol_feas=1e-10, tol_comp=1e-14, tau=0.995, threads=0, polish=True):
-    """polish=False: the IPM iterates alone (iterate-level parity with a kernel that does not
-    polish); the result's 'polished' marks instances whose answer is the active-set polish."""
+          tol_feas=1e-10, tol_comp=1e-14, tau=0.995, threads=0, polish=1):
+    """polish: 1 (True, default) after 0 / -8 exits, 2 also with weakly active rows, 0 (False)
+    off - the bqp_options.polish levels of the GPU solver; the result's 'polished' marks the
+    instances whose answer is the active-set polish."""
     dims, d, batch, keep = pack_ocp(ocp, x0, w, hp, A, B)
     nx, nu, p, N = ocp['nx'], ocp['nu'], ocp['np'], ocp['N']
     x = np.zeros((batch, N + 1, nx)); u = np.zeros((batch, N, nu)); th = np.zeros((batch, p))

@@ -83,18 +83,25 @@ def condense_ocp(ocp, x0, A=None, B=None, w=None, hp=None):
 def _kkt_refined(H, f, Aa, ba, steps=3):
     """Equality-constrained KKT [H Aa'; Aa 0][z; l] = [-f; ba] in fp64 with iterative refinement
     whose residuals are formed in extended precision (np.longdouble, 64-bit mantissa on x86)."""
+    import warnings
     n, na = H.shape[0], Aa.shape[0]
+    if na > n:                                           # more equalities than unknowns
+        K = np.block([[H, Aa.T], [Aa, np.zeros((na, na))]])
+        sol = np.linalg.lstsq(K, np.concatenate([-f, ba]), rcond=1e-15)[0]
+        return sol[:n], sol[n:]
     K = np.block([[H, Aa.T], [Aa, np.zeros((na, na))]])
     rhs = np.concatenate([-f, ba])
     Kl = K.astype(np.longdouble)
     rl = rhs.astype(np.longdouble)
     try:
-        lu = sla.lu_factor(K)
-        sol = sla.lu_solve(lu, rhs)
-        for _ in range(steps):
-            res = (rl - Kl @ sol.astype(np.longdouble)).astype(np.float64)
-            sol = sol + sla.lu_solve(lu, res)
-    except (np.linalg.LinAlgError, ValueError):
+        with warnings.catch_warnings(), np.errstate(all='ignore'):
+            warnings.simplefilter('error', sla.LinAlgWarning)
+            lu = sla.lu_factor(K)
+            sol = sla.lu_solve(lu, rhs)
+            for _ in range(steps):
+                res = (rl - Kl @ sol.astype(np.longdouble)).astype(np.float64)
+                sol = sol + sla.lu_solve(lu, res)
+    except (np.linalg.LinAlgError, ValueError, sla.LinAlgWarning):
         sol = np.linalg.lstsq(K, rhs, rcond=1e-15)[0]
     return sol[:n], sol[n:]
 

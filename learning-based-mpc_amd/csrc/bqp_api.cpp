@@ -477,6 +477,7 @@ int bqp_quadprog_batched_device(bqp_handle h, const bqp_dims* d, int batch, cons
     a.x = x; a.fval = fval; a.lam_ineqlin = lam_ineqlin; a.lam_eqlin = lam_eqlin;
     a.lam_lower = lam_lower; a.lam_upper = lam_upper; a.exitflag = exitflag; a.stats = Sd;
     a.work = wk; a.work_stride = wst;
+    a.polish = o.polish < 0 ? 0 : 1;
     HIP_TRY(hipEventRecord(h->ev0, st));
     HIP_TRY(bqp::launch_dense(a, st));
     HIP_TRY(hipEventRecord(h->ev1, st));
@@ -664,6 +665,7 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     q.sH = (int64_t)n * n; q.sf = n; q.sA = 0; q.sb = m;
     q.x = a.d; q.lam_ineqlin = a.lam; q.exitflag = a.qpflag;
     q.work = (double*)h->dwork.p; q.work_stride = wst;
+    q.polish = o.polish < 0 ? 0 : 1;
     q.stats = (double*)h->dwork.p + (size_t)wst * B;
     HIP_TRY(hipEventRecord(h->ev0, st));
     int launches = 0;

@@ -31,15 +31,22 @@ namespace bqp {
 #define DQ_CONVEX_EPS 1e-10   // shift of the convexity test (relative)
 #define DQ_MU_BLOWUP 1e6
 #define DQ_Z_BIG 1e12
+// round-3 safeguards, as the structured kernel (bqp_ocp.hip) and oracle/dense_ipm.py:
+#define DQ_FEAS_GUARD 1e-8    // -2 needs the primal residual above this (relative)
+#define DQ_CMAX_K 100.0       // convergence also needs every row's t lam <= CMAX_K tol_comp
+#define DQ_SOC_ALPHA 0.1      // predictor step below this on a primal-feasible iterate: no SOC term
+#define DQ_POL_ROUNDS 4       // active-set corrections of the polish
 
 struct DWork {
     int64_t K, Y, S, z, y, q, w, dz, dy, rd, re, tA, lA, riA, rcA, dtA, dlA, tB, lB, riB, rcB, dtB, dlB, total;
     __host__ __device__ static DWork make(int n, int m, int me) {
         DWork o;
         int64_t c = 0;
+        // Y / S also hold the polish's [Aeq; active rows] (at most max(me, n) of them)
+        const int64_t ne = me > n ? me : n;
         o.K = c; c += (int64_t)n * n;
-        o.Y = c; c += (int64_t)n * me;
-        o.S = c; c += (int64_t)me * me;
+        o.Y = c; c += (int64_t)n * ne;
+        o.S = c; c += ne * ne;
         o.z = c; c += n; o.y = c; c += me; o.q = c; c += n; o.w = c; c += n;
         o.dz = c; c += n; o.dy = c; c += me; o.rd = c; c += n; o.re = c; c += me;
         o.tA = c; c += m; o.lA = c; c += m; o.riA = c; c += m; o.rcA = c; c += m;
@@ -94,6 +101,7 @@ struct Red {
 // in-place lower Cholesky of an n x n column-major matrix (global/L2).  fl >= 0: every pivot is
 // floored at fl (static pivoting; never fails on finite input); fl < 0: returns false at the
 // first non-positive pivot (the convexity test)
+template <int NTH = DT>
 __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
     const int tid = threadIdx.x;
     for (int j = 0; j < n; ++j) {
@@ -107,12 +115,12 @@ __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
         const double dj = sc[8];
         if (!(dj > 0.0)) return false;
         const double ljj = sqrt(dj);
-        for (int i = j + 1 + tid; i < n; i += DT) K[(int64_t)j * n + i] /= ljj;
+        for (int i = j + 1 + tid; i < n; i += NTH) K[(int64_t)j * n + i] /= ljj;
         __syncthreads();
         // trailing update of the lower triangle: K[c][r] -= L[j][r] * L[j][c], r >= c > j
         const int rem = n - j - 1;
         const int64_t cnt = (int64_t)rem * (rem + 1) / 2;
-        for (int64_t e = tid; e < cnt; e += DT) {
+        for (int64_t e = tid; e < cnt; e += NTH) {
             // map e -> (c, r) with c <= r in the trailing block (column-wise packing)
             int c = (int)((2 * rem + 1 - sqrt((double)(2 * rem + 1) * (2 * rem + 1) - 8.0 * e)) / 2);
             if (c < 0) c = 0;
@@ -128,11 +136,12 @@ __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
 }
 
 // solve L L' x = b in place (x in LDS vector xs of length n), thread-parallel dot products
-__device__ void chol_solve_vec(const double* L, int n, double* xs, Red& red) {
+template <int NTH = DT, class R = Red>
+__device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
     // forward L y = b
     for (int i = 0; i < n; ++i) {
         double part = 0.0;
-        for (int k = threadIdx.x; k < i; k += DT) part += L[(int64_t)k * n + i] * xs[k];
+        for (int k = threadIdx.x; k < i; k += NTH) part += L[(int64_t)k * n + i] * xs[k];
         const double s = red.sum(part);
         if (threadIdx.x == 0) xs[i] = (xs[i] - s) / L[(int64_t)i * n + i];
         __syncthreads();
@@ -140,7 +149,7 @@ __device__ void chol_solve_vec(const double* L, int n, double* xs, Red& red) {
     // backward L' x = y
     for (int i = n - 1; i >= 0; --i) {
         double part = 0.0;
-        for (int k = i + 1 + threadIdx.x; k < n; k += DT) part += L[(int64_t)i * n + k] * xs[k];
+        for (int k = i + 1 + threadIdx.x; k < n; k += NTH) part += L[(int64_t)i * n + k] * xs[k];
         const double s = red.sum(part);
         if (threadIdx.x == 0) xs[i] = (xs[i] - s) / L[(int64_t)i * n + i];
         __syncthreads();
@@ -159,6 +168,213 @@ __device__ void chol_solve_col(const double* L, int n, double* x) {
         for (int k = i + 1; k < n; ++k) v -= L[(int64_t)i * n + k] * x[k];
         x[i] = v / L[(int64_t)i * n + i];
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// active-set polish after a 0 / -8 exit (oracle/dense_ipm.py::_polish): the rows with lam > t
+// join the equality rows and the equality-constrained QP is solved directly from z - K = H +
+// rho G_a'G_a (rho = max(1, max H_ii): positive definite whenever the reduced problem is), the
+// Schur complement of Ex = [Aeq; G_a], one exact Newton step.  Accepted when stationarity
+// <= tol_stat (1 + |Hz + f|), every row and the equalities within 1e-12 (1 + |data|) and no
+// active multiplier below -1e-9 (1 + max); otherwise rows with negative multipliers leave,
+// violated rows enter (DQ_POL_ROUNDS rounds).  Scratch: the instance's global workspace
+// (its IPM vectors are dead by now); the IPM state (z, y, t, lam) is overwritten only on
+// acceptance.  Rows r: 0..m-1 the rows of A, m + j the upper bound of j, m + n + j the lower.
+struct DPolish {
+    int n, m, me;
+    const double *H, *f, *A, *b, *E, *e, *lb, *ub;
+    double *z, *y, *tA, *lA, *tB, *lB;
+    double* W;             // the instance's DWork
+    double bscale, tol_stat;
+};
+
+template <int NTH, class R>
+__device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
+    R red{sc};
+    const int n = p.n, m = p.m, me = p.me, tid = threadIdx.x;
+    const DWork L = DWork::make(n, m, me);
+    double *K = p.W + L.K, *Y = p.W + L.Y, *S = p.W + L.S;
+    double *actA = p.W + L.rcA, *actB = p.W + L.rcB, *nuA = p.W + L.dlA, *nuB = p.W + L.dlB;
+    double *riA = p.W + L.riA, *riB = p.W + L.riB, *idx = p.W + L.dtB, *zn = p.W + L.dz;
+    double *w = p.W + L.w, *mult = p.W + L.rd, *ra = p.W + L.q;
+    auto upp = [&](int j) -> bool { return p.ub && isfinite(p.ub[j]); };
+    auto lop = [&](int j) -> bool { return p.lb && isfinite(p.lb[j]); };
+    // entry i of row r and its right-hand side
+    auto g = [&](int r, int i) -> double {
+        if (r < m) return p.A[(int64_t)i * m + r];
+        if (r < m + n) return (i == r - m) ? 1.0 : 0.0;
+        return (i == r - m - n) ? -1.0 : 0.0;
+    };
+    auto hr = [&](int r) -> double { return r < m ? p.b[r] : (r < m + n ? p.ub[r - m] : -p.lb[r - m - n]); };
+    auto gdot = [&](int r, const double* v) -> double {
+        if (r < m) {
+            double s = 0.0;
+            for (int i = 0; i < n; ++i) s += p.A[(int64_t)i * m + r] * v[i];
+            return s;
+        }
+        return r < m + n ? v[r - m] : -v[r - m - n];
+    };
+    for (int r = tid; r < m; r += NTH) actA[r] = p.lA[r] > p.tA[r] ? 1.0 : 0.0;
+    for (int j = tid; j < n; j += NTH) {
+        actB[j] = (upp(j) && p.lB[j] > p.tB[j]) ? 1.0 : 0.0;
+        actB[n + j] = (lop(j) && p.lB[n + j] > p.tB[n + j]) ? 1.0 : 0.0;
+    }
+    double hd = 0.0;
+    for (int j = tid; j < n; j += NTH) hd = fmax(hd, fabs(p.H[(int64_t)j * n + j]));
+    const double rho = fmax(1.0, red.max(hd));
+    const double tf = 1e-12 * (1.0 + p.bscale);
+    for (int round = 0; round < DQ_POL_ROUNDS; ++round) {
+        __syncthreads();
+        if (tid == 0) {             // active row list (serial: a handful of rounds per instance)
+            int c = 0;
+            bool over = false;
+            for (int r = 0; r < m + 2 * n; ++r) {
+                const double av = r < m ? actA[r] : actB[r - m];
+                if (av != 0.0) {
+                    if (me + c < n) idx[c++] = (double)r;
+                    else over = true;
+                }
+            }
+            sc[9] = (over || me + c > n) ? -1.0 : (double)c;
+        }
+        __syncthreads();
+        if (sc[9] < 0.0) return false;       // more active rows than variables: degenerate
+        const int na = (int)sc[9], ne = me + na;
+        // K = H + rho G_a'G_a
+        double dmx = 0.0;
+        for (int e2 = tid; e2 < n * n; e2 += NTH) {
+            const int i = e2 % n, j = e2 / n;
+            double v = p.H[e2];
+            for (int k = 0; k < na; ++k) {
+                const int r = (int)idx[k];
+                if (r < m) v += rho * p.A[(int64_t)i * m + r] * p.A[(int64_t)j * m + r];
+                else if (i == j && (r - m) % n == i) v += rho;
+            }
+            K[e2] = v;
+            if (i == j) dmx = fmax(dmx, fabs(v));
+        }
+        const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
+        __syncthreads();
+        block_cholesky<NTH>(K, n, sc, kfl);
+        // Y = K^{-1} Ex', S = Ex Y (one thread per row of Ex)
+        for (int k = tid; k < ne; k += NTH) {
+            double* yc = Y + (int64_t)k * n;
+            if (k < me) for (int j = 0; j < n; ++j) yc[j] = p.E[(int64_t)j * me + k];
+            else { const int r = (int)idx[k - me]; for (int j = 0; j < n; ++j) yc[j] = g(r, j); }
+            chol_solve_col(K, n, yc);
+        }
+        // ra = G_a z - h_a
+        for (int k = tid; k < na; k += NTH) { const int r = (int)idx[k]; ra[k] = gdot(r, p.z) - hr(r); }
+        __syncthreads();
+        double smx = 0.0;
+        for (int t2 = tid; t2 < ne * ne; t2 += NTH) {
+            const int r1 = t2 % ne, r2 = t2 / ne;
+            const double* yc = Y + (int64_t)r2 * n;
+            double s = 0.0;
+            if (r1 < me) for (int j = 0; j < n; ++j) s += p.E[(int64_t)j * me + r1] * yc[j];
+            else s = gdot((int)idx[r1 - me], yc);
+            S[(int64_t)r2 * ne + r1] = s;
+            if (r1 == r2) smx = fmax(smx, fabs(s));
+        }
+        // w = -K^{-1}(Hz + f + rho G_a' ra)
+        for (int j = tid; j < n; j += NTH) {
+            double v = p.f[j];
+            for (int i = 0; i < n; ++i) v += p.H[(int64_t)i * n + j] * p.z[i];
+            for (int k = 0; k < na; ++k) v += rho * g((int)idx[k], j) * ra[k];
+            xs[j] = -v;
+        }
+        const double sfl = DQ_PIV_FLOOR * fmax(red.max(smx), 1e-300);
+        __syncthreads();
+        if (ne > 0) block_cholesky<NTH>(S, ne, sc, sfl);
+        chol_solve_vec<NTH>(K, n, xs, red);
+        for (int j = tid; j < n; j += NTH) w[j] = xs[j];
+        __syncthreads();
+        // mult = S^{-1}(Ex w + Ex z - ex)
+        for (int k = tid; k < ne; k += NTH) {
+            double v;
+            if (k < me) {
+                v = -p.e[k];
+                for (int j = 0; j < n; ++j) v += p.E[(int64_t)j * me + k] * (w[j] + p.z[j]);
+            } else {
+                const int r = (int)idx[k - me];
+                v = gdot(r, w) + ra[k - me];
+            }
+            xs[k] = v;
+        }
+        __syncthreads();
+        if (ne > 0) chol_solve_vec<NTH>(S, ne, xs, red);
+        for (int k = tid; k < ne; k += NTH) mult[k] = xs[k];
+        __syncthreads();
+        for (int j = tid; j < n; j += NTH) {
+            double v = p.z[j] + w[j];
+            for (int k = 0; k < ne; ++k) v -= Y[(int64_t)k * n + j] * mult[k];
+            zn[j] = v;
+        }
+        for (int r = tid; r < m; r += NTH) nuA[r] = 0.0;
+        for (int j = tid; j < 2 * n; j += NTH) nuB[j] = 0.0;
+        __syncthreads();
+        for (int k = tid; k < na; k += NTH) {
+            const int r = (int)idx[k];
+            if (r < m) nuA[r] = mult[me + k]; else nuB[r - m] = mult[me + k];
+        }
+        __syncthreads();
+        // checks at zn
+        double viol = 0.0, va = 0.0, lmx = 0.0, lneg = 0.0, fe = 0.0, st = 0.0, gs = 0.0;
+        for (int r = tid; r < m; r += NTH) {
+            const double v = gdot(r, zn) - p.b[r];
+            riA[r] = v;
+            viol = fmax(viol, v);
+            if (actA[r] != 0.0) { va = fmax(va, fabs(v)); lmx = fmax(lmx, nuA[r]); lneg = fmin(lneg, nuA[r]); }
+        }
+        for (int j = tid; j < n; j += NTH) {
+            riB[j] = upp(j) ? zn[j] - p.ub[j] : -INFINITY;
+            riB[n + j] = lop(j) ? -zn[j] + p.lb[j] : -INFINITY;
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int q2 = s2 * n + j;
+                viol = fmax(viol, riB[q2]);
+                if (actB[q2] != 0.0) { va = fmax(va, fabs(riB[q2])); lmx = fmax(lmx, nuB[q2]); lneg = fmin(lneg, nuB[q2]); }
+            }
+            double v = p.f[j];
+            for (int i = 0; i < n; ++i) v += p.H[(int64_t)i * n + j] * zn[i];
+            gs = fmax(gs, fabs(v));
+            for (int k = 0; k < me; ++k) v += p.E[(int64_t)j * me + k] * mult[k];
+            for (int r = 0; r < m; ++r) v += p.A[(int64_t)j * m + r] * nuA[r];
+            v += nuB[j] - nuB[n + j];
+            st = fmax(st, fabs(v));
+        }
+        for (int k = tid; k < me; k += NTH) {
+            double v = -p.e[k];
+            for (int j = 0; j < n; ++j) v += p.E[(int64_t)j * me + k] * zn[j];
+            fe = fmax(fe, fabs(v));
+        }
+        const double stat = red.max(st), gsc = red.max(gs), vio = red.max(viol), vac = red.max(va);
+        const double lx = red.max(lmx), ln = red.min(lneg), fq = red.max(fe);
+        const double td = 1e-9 * (1.0 + lx);
+        if (isfinite(stat) && stat <= p.tol_stat * (1.0 + gsc) && vio <= tf && vac <= tf && ln >= -td && fq <= tf) {
+            for (int j = tid; j < n; j += NTH) {
+                p.z[j] = zn[j];
+                if (upp(j)) { p.lB[j] = fmax(nuB[j], 0.0); p.tB[j] = fmax(-riB[j], 0.0); }
+                if (lop(j)) { p.lB[n + j] = fmax(nuB[n + j], 0.0); p.tB[n + j] = fmax(-riB[n + j], 0.0); }
+            }
+            for (int r = tid; r < m; r += NTH) { p.lA[r] = fmax(nuA[r], 0.0); p.tA[r] = fmax(-riA[r], 0.0); }
+            for (int k = tid; k < me; k += NTH) p.y[k] = mult[k];
+            if (tid == 0) { sc[10] = stat; sc[11] = fmax(fmax(vio, 0.0), fq); }
+            __syncthreads();
+            return true;
+        }
+        // set corrections
+        double chg = 0.0;
+        for (int r = tid; r < m; r += NTH) {
+            if (actA[r] != 0.0 && nuA[r] < -td) { actA[r] = 0.0; chg = 1.0; }
+            else if (actA[r] == 0.0 && riA[r] > tf) { actA[r] = 1.0; chg = 1.0; }
+        }
+        for (int q2 = tid; q2 < 2 * n; q2 += NTH) {
+            if (actB[q2] != 0.0 && nuB[q2] < -td) { actB[q2] = 0.0; chg = 1.0; }
+            else if (actB[q2] == 0.0 && riB[q2] > tf) { actB[q2] = 1.0; chg = 1.0; }
+        }
+        if (red.max(chg) == 0.0) return false;
+    }
+    return false;
 }
 
 __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
@@ -194,14 +410,16 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const double minv = 1.0 / fmax(mtot, 1.0);
 
     // ---------------------------------------------------------------- residuals
-    auto residuals = [&](double& stat, double& feq, double& fin, double& csum, double& gscale, double& zmax) {
-        double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0;
+    auto residuals = [&](double& stat, double& feq, double& fin, double& csum, double& gscale, double& zmax,
+                         double& cmax) {
+        double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0, cm = 0.0;
         for (int r = tid; r < m; r += DT) {
             double v = tA[r] - b[r];
             for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
             riA[r] = v;
             fe = fmax(fe, fabs(v));
             cs += tA[r] * lA[r];
+            cm = fmax(cm, tA[r] * lA[r]);
         }
         for (int r = tid; r < me; r += DT) {
             double v = -e[r];
@@ -220,11 +438,13 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 v += lB[j];
                 riB[j] = z[j] + tB[j] - ub[j];
                 cs += tB[j] * lB[j];
+                cm = fmax(cm, tB[j] * lB[j]);
             }
             if (lo_present(j)) {
                 v -= lB[n + j];
                 riB[n + j] = -z[j] + tB[n + j] + lb[j];
                 cs += tB[n + j] * lB[n + j];
+                cm = fmax(cm, tB[n + j] * lB[n + j]);
             }
             fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
             rd[j] = v;
@@ -237,6 +457,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         csum = red.sum(cs);
         gscale = red.max(gs);
         zmax = red.max(zm);
+        cmax = red.max(cm);
     };
 
     // ---------------------------------------------------------------- factorisation
@@ -429,8 +650,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         __syncthreads();
         if (!block_cholesky(K, n, sc, -1.0)) flag = -6;
     }
-    double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0;
-    residuals(stat, feq, fin, csum, gscale, zmax);
+    double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0, cmax = 0.0;
+    residuals(stat, feq, fin, csum, gscale, zmax, cmax);
     if (flag == 0 && !factor()) flag = -8;
     if (flag == 0) {
         solve();
@@ -459,14 +680,14 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
         for (it = 0; it <= a.max_iter; ++it) {
-            residuals(stat, feq, fin, csum, gscale, zmax);
+            residuals(stat, feq, fin, csum, gscale, zmax, cmax);
             const double feas = fmax(feq, fin);
             mu = csum * minv;
             if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
-                mu <= a.tol_comp) { flag = 1; break; }
+                mu <= a.tol_comp && cmax <= DQ_CMAX_K * a.tol_comp) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
             if (zmax > zbig) { flag = -3; break; }
-            if (mu > DQ_MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) { flag = -2; break; }
+            if (mu > DQ_MU_BLOWUP * mu_min && feas > DQ_FEAS_GUARD * (1.0 + bscale)) { flag = -2; break; }
             mu_min = fmin(mu_min, mu);
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }
@@ -479,14 +700,21 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             double sg = mua / mu;
             sg = sg * sg * sg;
             const double smu = sg * mu;
-            for (int r = tid; r < m; r += DT) rcA[r] = tA[r] * lA[r] + dtA[r] * dlA[r] - smu;
+            const double soc = (al < DQ_SOC_ALPHA && feas <= DQ_FEAS_GUARD * (1.0 + bscale)) ? 0.0 : 1.0;
+            for (int r = tid; r < m; r += DT) rcA[r] = tA[r] * lA[r] + soc * dtA[r] * dlA[r] - smu;
             for (int j = tid; j < n; j += DT) {
-                rcB[j] = up_present(j) ? tB[j] * lB[j] + dtB[j] * dlB[j] - smu : 0.0;
-                rcB[n + j] = lo_present(j) ? tB[n + j] * lB[n + j] + dtB[n + j] * dlB[n + j] - smu : 0.0;
+                rcB[j] = up_present(j) ? tB[j] * lB[j] + soc * dtB[j] * dlB[j] - smu : 0.0;
+                rcB[n + j] = lo_present(j) ? tB[n + j] * lB[n + j] + soc * dtB[n + j] * dlB[n + j] - smu : 0.0;
             }
             __syncthreads();
             solve();
             al = fmin(1.0, max_step() * a.tau);
+            {   // the factor left fp64 range: keep the last finite iterate
+                double bad = isfinite(al) ? 0.0 : 1.0;
+                for (int j = tid; j < n; j += DT) if (!isfinite(dz[j])) bad = 1.0;
+                for (int r = tid; r < me; r += DT) if (!isfinite(dy[r])) bad = 1.0;
+                if (red.max(bad) != 0.0) { flag = -8; break; }
+            }
             for (int j = tid; j < n; j += DT) {
                 z[j] += al * dz[j];
                 if (up_present(j)) { tB[j] += al * dtB[j]; lB[j] += al * dlB[j]; }
@@ -516,7 +744,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
         double* so = a.stats + (int64_t)inst * STATS_W;
-        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin; so[6] = 0.0;
+        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin;
+        so[6] = 0.0;
     }
 }
 
@@ -620,8 +849,8 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     const double ubj = upj ? ubs[lane] : 0.0, lbj = loj ? lbs[lane] : 0.0;
     const double minv = 1.0 / fmax(wsum((upj ? 1.0 : 0.0) + (loj ? 1.0 : 0.0)) + (double)m, 1.0);
 
-    auto residuals = [&](double& stat, double& fin, double& csum, double& gscale, double& zmax) __attribute__((always_inline)) {
-        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0;
+    auto residuals = [&](double& stat, double& fin, double& csum, double& gscale, double& zmax, double& cmax) __attribute__((always_inline)) {
+        double fe = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0, cm = 0.0;
         double zc[16 * NT];
 #pragma unroll
         for (int c = 0; c < 16 * NT; ++c) zc[c] = c < n ? z[c] : 0.0;
@@ -633,6 +862,7 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             riA[r] = v;
             fe = fmax(fe, fabs(v));
             cs = fma(tA[r], lA[r], cs);
+            cm = fmax(cm, tA[r] * lA[r]);
         }
         const double atl = atv<NT>(A, lA, m, n, lane);       // (A' lam)_lane
         if (lane < n) {
@@ -644,14 +874,14 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             gs = fabs(v);
             v += atl;
             riB[j] = 0.0; riB[n + j] = 0.0;
-            if (upj) { v += lB[j]; riB[j] = z[j] + tB[j] - ubj; cs += tB[j] * lB[j]; }
-            if (loj) { v -= lB[n + j]; riB[n + j] = -z[j] + tB[n + j] + lbj; cs += tB[n + j] * lB[n + j]; }
+            if (upj) { v += lB[j]; riB[j] = z[j] + tB[j] - ubj; cs += tB[j] * lB[j]; cm = fmax(cm, tB[j] * lB[j]); }
+            if (loj) { v -= lB[n + j]; riB[n + j] = -z[j] + tB[n + j] + lbj; cs += tB[n + j] * lB[n + j]; cm = fmax(cm, tB[n + j] * lB[n + j]); }
             fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
             rd[j] = v;
             st = fabs(v);
             zm = fabs(z[j]);
         }
-        stat = wmax(st); fin = wmax(fe); csum = wsum(cs); gscale = wmax(gs); zmax = wmax(zm);
+        stat = wmax(st); fin = wmax(fe); csum = wsum(cs); gscale = wmax(gs); zmax = wmax(zm); cmax = wmax(cm);
         wave_sync();
     };
 
@@ -874,8 +1104,8 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         if (!chol(-1.0)) flag = -6;
     }
     const double feq = 0.0;                 // no equality rows on this path
-    double stat = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0;
-    residuals(stat, fin, csum, gscale, zmax);
+    double stat = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0, cmax = 0.0;
+    residuals(stat, fin, csum, gscale, zmax, cmax);
     if (flag == 0 && !factor()) flag = -8;
     if (flag == 0) {
         solve();
@@ -901,14 +1131,14 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
         for (it = 0; it <= a.max_iter; ++it) {
-            residuals(stat, fin, csum, gscale, zmax);
+            residuals(stat, fin, csum, gscale, zmax, cmax);
             const double feas = fin;
             mu = csum * minv;
             if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
-                mu <= a.tol_comp) { flag = 1; break; }
+                mu <= a.tol_comp && cmax <= DQ_CMAX_K * a.tol_comp) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
             if (zmax > zbig) { flag = -3; break; }
-            if (mu > DQ_MU_BLOWUP * mu_min && feas > 1e-6 * (1.0 + bscale)) { flag = -2; break; }
+            if (mu > DQ_MU_BLOWUP * mu_min && feas > DQ_FEAS_GUARD * (1.0 + bscale)) { flag = -2; break; }
             mu_min = fmin(mu_min, mu);
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }
@@ -921,15 +1151,18 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             double sg = mua / mu;
             sg = sg * sg * sg;
             const double smu = sg * mu;
-            for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r] + dtA[r] * dlA[r] - smu;
+            const double soc = (al < DQ_SOC_ALPHA && feas <= DQ_FEAS_GUARD * (1.0 + bscale)) ? 0.0 : 1.0;
+            for (int r = lane; r < m; r += 64) rcA[r] = tA[r] * lA[r] + soc * dtA[r] * dlA[r] - smu;
             if (lane < n) {
                 const int j = lane;
-                rcB[j] = upj ? tB[j] * lB[j] + dtB[j] * dlB[j] - smu : 0.0;
-                rcB[n + j] = loj ? tB[n + j] * lB[n + j] + dtB[n + j] * dlB[n + j] - smu : 0.0;
+                rcB[j] = upj ? tB[j] * lB[j] + soc * dtB[j] * dlB[j] - smu : 0.0;
+                rcB[n + j] = loj ? tB[n + j] * lB[n + j] + soc * dtB[n + j] * dlB[n + j] - smu : 0.0;
             }
             wave_sync();
             solve();
             al = fmin(1.0, max_step() * a.tau);
+            // the factor left fp64 range: keep the last finite iterate
+            if (wmax((isfinite(al) && (lane >= n || isfinite(dz[lane]))) ? 0.0 : 1.0) != 0.0) { flag = -8; break; }
             if (lane < n) {
                 const int j = lane;
                 z[j] += al * dz[j];
@@ -939,6 +1172,17 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             for (int r = lane; r < m; r += 64) { tA[r] += al * dtA[r]; lA[r] += al * dlA[r]; }
             wave_sync();
         }
+    }
+    if (a.polish && (flag == 0 || flag == -8) && a.work) {
+        // hand the iterate to dense_polish_kernel through the instance's workspace (DWork)
+        const DWork L = DWork::make(n, m, 0);
+        double* W = a.work + (int64_t)inst * a.work_stride;
+        if (lane < n) {
+            W[L.z + lane] = z[lane];
+            W[L.tB + lane] = tB[lane]; W[L.tB + n + lane] = tB[n + lane];
+            W[L.lB + lane] = lB[lane]; W[L.lB + n + lane] = lB[n + lane];
+        }
+        for (int r = lane; r < m; r += 64) { W[L.tA + r] = tA[r]; W[L.lA + r] = lA[r]; }
     }
     double fv = 0.0;
     if (lane < n) {
@@ -957,7 +1201,69 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
         double* so = a.stats + (int64_t)inst * STATS_W;
-        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin; so[6] = 0.0;
+        so[0] = (double)it; so[1] = stat; so[2] = fmax(feq, fin); so[3] = mu; so[4] = feq; so[5] = fin;
+        so[6] = 0.0;
+    }
+}
+
+// the active-set polish of the instances that ended 0 / -8 (dense_polish), a kernel of its own
+// so that its registers do not weigh on the IPM kernels; the iterate is in the workspace (DWork
+// offsets: dense_ipm_kernel keeps it there, dense_wave_kernel stores it on those exits).  On
+// acceptance x, the multipliers, fval, the flag (1) and the stats are rewritten.
+__global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
+    const int inst = blockIdx.x;
+    if (inst >= a.batch) return;
+    const int flag = a.exitflag[inst];
+    if (flag != 0 && flag != -8) return;
+    const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
+    __shared__ double sc[16];
+    __shared__ double xs[DT];
+    Red red{sc};
+    const DWork L = DWork::make(n, m, me);
+    double* W = a.work + (int64_t)inst * a.work_stride;
+    const double* H = a.H + (int64_t)inst * a.sH;
+    const double* f = a.f + (int64_t)inst * a.sf;
+    const double* A = a.A ? a.A + (int64_t)inst * a.sA : nullptr;
+    const double* b = a.b ? a.b + (int64_t)inst * a.sb : nullptr;
+    const double* E = a.Aeq ? a.Aeq + (int64_t)inst * a.sAeq : nullptr;
+    const double* e = a.beq ? a.beq + (int64_t)inst * a.sbeq : nullptr;
+    const double* lb = a.lb ? a.lb + (int64_t)inst * a.slb : nullptr;
+    const double* ub = a.ub ? a.ub + (int64_t)inst * a.sub : nullptr;
+    double *z = W + L.z, *y = W + L.y, *tA = W + L.tA, *lA = W + L.lA, *tB = W + L.tB, *lB = W + L.lB;
+    // rows present, data scale and a finite iterate (oracle/dense_ipm.py: m > 0, |Hz + f| finite)
+    double cnt = 0.0, bsl = 0.0, zf = 0.0;
+    for (int r = tid; r < m; r += DT) bsl = fmax(bsl, fabs(b[r]));
+    for (int r = tid; r < me; r += DT) bsl = fmax(bsl, fabs(e[r]));
+    for (int j = tid; j < n; j += DT) {
+        if (ub && isfinite(ub[j])) { cnt += 1.0; bsl = fmax(bsl, fabs(ub[j])); }
+        if (lb && isfinite(lb[j])) { cnt += 1.0; bsl = fmax(bsl, fabs(lb[j])); }
+        if (!isfinite(z[j])) zf = 1.0;
+    }
+    const double rows = red.sum(cnt) + (double)m;
+    const double bscale = red.max(bsl);
+    if (rows == 0.0 || red.max(zf) != 0.0) return;
+    const DPolish pp{n, m, me, H, f, A, b, E, e, lb, ub, z, y, tA, lA, tB, lB, W, bscale, a.tol_stat};
+    if (!dense_polish<DT, Red>(pp, sc, xs)) return;
+    const double stat = sc[10], feas = sc[11];
+    double fv = 0.0;
+    for (int j = tid; j < n; j += DT) {
+        double hz = 0.0;
+        for (int i = 0; i < n; ++i) hz += H[(int64_t)j * n + i] * z[i];
+        fv += z[j] * (0.5 * hz + f[j]);
+        a.x[(int64_t)inst * n + j] = z[j];
+        if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = (lb && isfinite(lb[j])) ? lB[n + j] : 0.0;
+        if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = (ub && isfinite(ub[j])) ? lB[j] : 0.0;
+    }
+    for (int r = tid; r < m; r += DT)
+        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = lA[r];
+    for (int r = tid; r < me; r += DT)
+        if (a.lam_eqlin) a.lam_eqlin[(int64_t)inst * me + r] = y[r];
+    fv = red.sum(fv);
+    if (tid == 0) {
+        if (a.fval) a.fval[inst] = fv;
+        a.exitflag[inst] = 1;
+        double* so = a.stats + (int64_t)inst * STATS_W;
+        so[1] = stat; so[2] = feas; so[3] = 0.0; so[4] = 0.0; so[5] = feas; so[6] = 1.0;
     }
 }
 
@@ -969,9 +1275,12 @@ hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
             hipLaunchKernelGGL(dense_wave_kernel<1>, dim3(a.batch), dim3(64), lds, st, a);
         else
             hipLaunchKernelGGL(dense_wave_kernel<2>, dim3(a.batch), dim3(64), lds, st, a);
-        return hipGetLastError();
+    } else {
+        hipLaunchKernelGGL(dense_ipm_kernel, dim3(a.batch), dim3(DT), 0, st, a);
     }
-    hipLaunchKernelGGL(dense_ipm_kernel, dim3(a.batch), dim3(DT), 0, st, a);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess || !a.polish || !a.work) return err;
+    hipLaunchKernelGGL(dense_polish_kernel, dim3(a.batch), dim3(DT), 0, st, a);
     return hipGetLastError();
 }
 

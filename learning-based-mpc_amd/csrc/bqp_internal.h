@@ -88,6 +88,7 @@ struct DenseKernelArgs {
     double* stats;
     double* work;      // per-instance scratch (global), work_stride doubles each
     int64_t work_stride;
+    int polish;        // 1: active-set polish after a 0 / -8 exit (bqp_dense.hip::dense_polish)
 };
 
 int dense_work_doubles(int n, int m, int me);

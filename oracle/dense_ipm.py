@@ -24,8 +24,14 @@ Status (quadprog exitflag), decided in this order at the top of every iteration:
       direction v of the feasible set with Hv = 0 and f'v < 0 the iterates run away (the
       static pivot floor keeps K factorable there);
   -2  primal infeasible: mu grew by MU_BLOWUP over its minimum while the primal residual
-      stalled above 1e-6 (1 + data scale) - the structured kernel's rule (bqp_ocp.hip);
+      stayed above FEAS_GUARD (1 + data scale) - the structured kernel's rule (bqp_ocp.hip);
    0  iteration limit.
+Round-3 safeguards (the structured kernel's, oracle/cpu_ipm.c): convergence also needs every
+row's t lam <= CMAX_K tol_comp; a predictor step below SOC_ALPHA on a primal-feasible iterate
+drops the corrector's second-order term; after a 0 / -8 exit the active-set polish (rows with
+lam > t join the equality rows: K = H + rho G_a'G_a and the equality Schur complement, one
+exact Newton step; set corrections) replaces the iterate if it passes the KKT checks - the fix
+of the condensed N = 128 DMS instance whose K lost accuracy as D = lam/t grew.
 """
 import numpy as np
 
@@ -33,6 +39,10 @@ PIV_FLOOR = 1e-14     # static pivot floor of K, relative to its largest diagona
 CONVEX_EPS = 1e-10    # convexity test shift (relative)
 MU_BLOWUP = 1e6
 Z_BIG = 1e12
+FEAS_GUARD = 1e-8
+CMAX_K = 100.0
+SOC_ALPHA = 0.1
+POL_ROUNDS = 4
 
 
 def _chol_floor(K, floor):
@@ -75,7 +85,7 @@ def convex(H):
 
 
 def solve(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, max_iter=50,
-          tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995):
+          tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995, polish=True):
     H = np.asarray(H, float)
     n = H.shape[0]
     f = np.asarray(f, float).ravel()
@@ -163,7 +173,8 @@ def solve(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, max_iter=5
         stat = np.abs(rd).max(initial=0.0)
         feas = max(np.abs(re).max(initial=0.0), np.abs(ri).max(initial=0.0))
         mu = (t @ lam) * minv
-        if stat <= tol_stat * (1 + gs) and feas <= tol_feas * (1 + bscale) and mu <= tol_comp:
+        if stat <= tol_stat * (1 + gs) and feas <= tol_feas * (1 + bscale) and mu <= tol_comp \
+                and (t * lam).max(initial=0.0) <= CMAX_K * tol_comp:
             flag = 1
             break
         if not (np.isfinite(stat) and np.isfinite(feas) and np.isfinite(mu)):
@@ -172,7 +183,7 @@ def solve(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, max_iter=5
         if np.abs(z).max(initial=0.0) > zscale:
             flag = -3
             break
-        if mu > MU_BLOWUP * mu_min and feas > 1e-6 * (1 + bscale):
+        if mu > MU_BLOWUP * mu_min and feas > FEAS_GUARD * (1 + bscale):
             flag = -2
             break
         mu_min = min(mu_min, mu)
@@ -183,12 +194,73 @@ def solve(H, f, A=None, b=None, Aeq=None, beq=None, lb=None, ub=None, max_iter=5
         a = max_step(dt, dl)
         mua = (t + a * dt) @ (lam + a * dl) * minv
         sg = (mua / mu) ** 3
-        dz, dy, dt, dl = newton(fac, rd, re, ri, t * lam + dt * dl - sg * mu)
+        soc = 0.0 if (a < SOC_ALPHA and feas <= FEAS_GUARD * (1 + bscale)) else 1.0
+        dz, dy, dt, dl = newton(fac, rd, re, ri, t * lam + soc * (dt * dl) - sg * mu)
         a = min(1.0, tau * max_step(dt, dl))
+        if not (np.isfinite(a) and np.isfinite(dz).all() and np.isfinite(dy).all()):
+            flag = -8          # the factor left fp64 range: keep the last finite iterate
+            break
         z = z + a * dz
         y = y + a * dy
         t = t + a * dt
         lam = lam + a * dl
+    polished = False
+    if polish and flag in (0, -8) and m and np.isfinite(gs):
+        out = _polish(H, f, G, h, E, e, z, y, lam, t, None, bscale, tol_stat)
+        if out is not None:
+            z, y, lam, t, stat, feas = out
+            flag, mu, polished = 1, 0.0, True
     res.update(x=z, y=y, lam=lam, t=t, exitflag=flag, iterations=it, mu=mu, stat=stat,
-               feas=feas, fval=0.5 * z @ H @ z + f @ z)
+               feas=feas, fval=0.5 * z @ H @ z + f @ z, polished=polished)
     return res
+
+
+def _polish(H, f, G, h, E, e, z, y, lam, t, rho, bscale, tol_stat):
+    """active-set polish (module doc): the rows with lam > t join the equality rows and the
+    equality-constrained QP is solved directly - K = H + rho G_a'G_a (augmented, so K is
+    positive definite whenever the reduced problem is) with the Schur complement of [E; G_a] -
+    one Newton step from z is exact for the QP; rows with a negative multiplier leave, violated
+    rows enter (at most POL_ROUNDS rounds).  Returns (z, y, lam, t, stat, feas) or None."""
+    me = E.shape[0]
+    act = lam > t
+    tf = 1e-12 * (1.0 + bscale)
+    for _ in range(POL_ROUNDS):
+        Ga = G[act]
+        rho_k = max(1.0, np.abs(np.diag(H)).max(initial=0.0))
+        K = H + rho_k * (Ga.T @ Ga)
+        L = _chol_floor(K, PIV_FLOOR * max(np.abs(np.diag(K)).max(initial=0.0), 1e-300))
+        Ex = np.vstack([E, Ga])
+        ex = np.concatenate([e, h[act]])
+        # Newton step of the equality-constrained QP from z (multipliers solved fresh)
+        rd = H @ z + f
+        w = -_lsolve(L, rd + rho_k * Ga.T @ (Ga @ z - h[act]))
+        if Ex.shape[0]:
+            Y = _lsolve(L, Ex.T)
+            S = Ex @ Y
+            Ls = _chol_floor(S, PIV_FLOOR * max(np.abs(np.diag(S)).max(), 1e-300))
+            mult = _lsolve(Ls, Ex @ w + (Ex @ z - ex))
+            zn = z + w - Y @ mult
+        else:
+            mult = np.zeros(0)
+            zn = z + w
+        yn, nu_a = mult[:me], mult[me:]
+        nu = np.zeros(len(h)); nu[act] = nu_a
+        ri = G @ zn - h
+        rdn = H @ zn + f + E.T @ yn + G.T @ nu
+        stat = np.abs(rdn).max(initial=0.0)
+        gs = np.abs(H @ zn + f).max(initial=0.0)
+        viol = max(0.0, ri.max(initial=0.0))
+        va = np.abs(ri[act]).max(initial=0.0)
+        lmx = max(0.0, nu_a.max(initial=0.0))
+        lneg = min(0.0, nu_a.min(initial=0.0))
+        fe = np.abs(E @ zn - e).max(initial=0.0)
+        td = 1e-9 * (1.0 + lmx)
+        if np.isfinite(stat) and stat <= tol_stat * (1 + gs) and viol <= tf and va <= tf and \
+                lneg >= -td and fe <= tf:
+            return zn, yn, np.maximum(nu, 0.0), np.maximum(-ri, 0.0), stat, max(viol, fe)
+        drop = act & (nu < -td)
+        add = ~act & (ri > tf)
+        if not (drop.any() or add.any()):
+            return None
+        act = (act & ~drop) | add
+    return None

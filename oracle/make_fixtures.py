@@ -143,8 +143,18 @@ def main():
                  err_vs_matlab=np.abs(du_or - du[idx]))
         print('F1 N=%d: oracle vs fmincon first move: median %.2e max %.2e' %
               (N, np.median(np.abs(du_or - du[idx])), np.abs(du_or - du[idx]).max()))
+    f2_fixtures(mg, F_T, h_T, rng)
+    # ---- F4 instance (hybrid LBMPC N=100) -------------------------------------------------
+    print('lbmpc instance: y_OL', inst['y_OL'].shape, 'data', inst['data'].shape)
+
+
+def f2_fixtures(mg, F_T, h_T, rng, only=None):
     # ---- F2: DMS/DSS tracking LMPC (IPOPT) ----------------------------------------------------
-    for fname, N, nsub in (('DSS_tLMPC', 100, 64), ('DMS_tLMPC_K', 100, 8), ('DMS_N50_tLMPC', 50, 16)):
+    # tLMPC.mat: the 600-step N = 100 tracking-LMPC run (same x_init, DSS/DMS form)
+    for fname, N, nsub in (('DSS_tLMPC', 100, 64), ('DMS_tLMPC_K', 100, 8), ('DMS_N50_tLMPC', 50, 16),
+                           ('tLMPC', 100, 16)):
+        if only and fname not in only:
+            continue
         xl = sio.loadmat(DATA + '/casadi/%s.mat' % fname)['xl']
         T = xl.shape[1] - 1
         u = np.zeros(T); res = np.zeros(T)
@@ -159,9 +169,14 @@ def main():
                  idx=idx, z_star=zs, u_star=u_or, dense_iters=its, kkt=kkt, err_vs_ipopt=err)
         print('F2 %s N=%d: oracle vs IPOPT first move: median %.2e max %.2e (rk4 inv res %.1e)' %
               (fname, N, np.median(err), err.max(), res.max()))
-    # ---- F4 instance (hybrid LBMPC N=100) -------------------------------------------------
-    print('lbmpc instance: y_OL', inst['y_OL'].shape, 'data', inst['data'].shape)
 
 
 if __name__ == '__main__':
-    sys.exit(main())
+    if len(sys.argv) > 1:
+        # python -m oracle.make_fixtures tLMPC ...: only those F2 fixtures (then re-solve their
+        # optima exactly with python oracle/refine_fixtures.py)
+        ts = sio.loadmat(DATA + '/term_set.mat')
+        f2_fixtures(mg_problem(), ts['F_w_N'].astype(float), ts['h_w_N'].astype(float).ravel(),
+                    np.random.default_rng(21), only=sys.argv[1:])
+    else:
+        sys.exit(main())

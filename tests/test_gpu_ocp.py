@@ -58,8 +58,16 @@ def test_f1_matches_cpu_restatement(mg, term_set, handle):
     assert np.mean(r.iterations == c['iterations']) > 0.9
 
 
-@pytest.mark.parametrize('fname', ['dms_DSS_tLMPC.npz', 'dms_DMS_N50_tLMPC.npz'])
+@pytest.mark.parametrize('fname', ['dms_DSS_tLMPC.npz', 'dms_DMS_N50_tLMPC.npz', 'dms_DMS_tLMPC_K.npz',
+                                   'dms_tLMPC.npz'])
 def test_f2_tracking_lmpc_vs_exact(mg, term_set, handle, fname):
+    """F2 call sites DSS_tracking_LMPC_casadi.m:155-160, DMS_tracking_LMPC_casadi.m:163-167 (N=50)
+    and DMS_tracking_LMPC_casadi_K.m:168-172 (N=100; the K form adds c_k = u_k - u_eq -
+    K(x_k - x_eq) as free variables, :290, with the cost on u: the same QP in (x, u, theta))
+    against the exact optima of the restated QP (oracle/refine_fixtures.py).  The stored IPOPT
+    moves differ from z* by up to 2.5e-4 (K form, state 80): the fixture's adjudication shows
+    IPOPT's move is feasible and costs more than the optimum - IPOPT stopped at its tolerance
+    on a cost that is flat in u_0 (running weight delta = 0.01)."""
     import bqp
     g = golden(fname)
     N = int(g['N'])
@@ -77,6 +85,14 @@ def test_f2_tracking_lmpc_vs_exact(mg, term_set, handle, fname):
     assert np.abs(r.y_OL[:, -1] - zs[:, -1]).max() < TOL_Z
     err = np.abs(r.y_OL - zs).max() / max(1.0, np.abs(zs).max())
     assert err < 2e-7, err
+    # IPOPT's stored moves: where they are off the optimum by more than 1e-6 IPOPT stopped short
+    # (feasible move with a positive cost excess), except where its recovered move leaves the
+    # rest of the horizon infeasible (N=50 state 65, tLMPC state 56: IPOPT accepts constraint
+    # violations up to its constr_viol_tol, 1e-4 by default)
+    gap = np.abs(r.y_OL[:, nu0] - g['u_ipopt'][g['idx']])
+    far = gap > 1e-6
+    ok = g['ipopt_fixed_feasible'][far]
+    assert (g['ipopt_excess'][far][ok] > 0).all()
 
 
 def test_f5_tracking_mpc_di(di, handle):
@@ -218,15 +234,15 @@ def test_long_horizon_box_layouts(mg, term_set, handle):
     with pytest.raises(BqpError, match='unsupported'):
         tl(128).solve(X, handle=handle, route='structured')
     # N + 1 > 128 takes the condensed route (dense GPU kernels) by default: 129 variables, 1896
-    # rows, cond(H) 2.4e3.  Instance 1 is hard for a dense IPM (the oracle's dense IPM runs 199
-    # iterations before its active-set polish finds the optimum); the dense kernel ends it with
-    # -8 (numerical failure, reported) - measured 7 of 8 converge.  The structured kernels are the
-    # path for long horizons, the condensed route a fallback for shapes they do not cover
+    # rows, cond(H) 2.4e3.  Instance 1 is hard for a dense IPM: as D = lam / t grows its K loses
+    # accuracy and the IPM stops with -8 at iteration 16 (round 2 reported that); the active-set
+    # polish after a 0 / -8 exit (bqp_dense.hip::dense_polish, oracle/dense_ipm.py::_polish) ends
+    # it at the optimum - the dense statement's polished first move is 3e-14 from the exact
+    # LDP/NNLS optimum (oracle/exact_qp.py), the structured C restatement's 1.1e-10
     rc = tl(128).solve(X, handle=handle)
     c = cpu_ref.solve(qp_forms.dms_ocp(mg, 128, *term_set), X - mg['x_wp'].ravel())
-    ok = rc.exitflag == 1
-    assert ok.sum() >= len(X) - 1 and set(rc.exitflag[~ok]) <= {-8}
-    assert np.abs(rc.u[ok, 0] - c['u'][ok, 0]).max() < 1e-7
+    assert (rc.exitflag == 1).all(), rc.exitflag
+    assert np.abs(rc.u[:, 0] - c['u'][:, 0]).max() < 1e-8
 
 
 def test_f5_c3_workload(handle):

@@ -28,6 +28,7 @@ the same algorithm in C, OpenMP over host cores, bounded sample).
 """
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
 import sys
@@ -435,30 +436,46 @@ def main():
             F_it = flops_per_iter(N, nx + npar, nu, nx, mp)
             flops_launch = float((kref * F_it).sum())
             achieved = flops_launch / (kernel_ms * 1e-3) / 1e12
-            traffic = None
-            pmc = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
-            if args.config == 'C2' and os.path.exists(pmc):
+            # HBM bytes per launch of this config's kernel: rocprofv3 PMC passes of the same
+            # bench command (tools/gpu_r03_prof.sh -> tools/pmc_summary.py --config)
+            traffic, traffic_src = None, None
+            tag = args.config + ('' if args.precision == 'fp64' else '_' + args.precision)
+            pmc = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % tag)
+            if os.path.exists(pmc):
                 try:
-                    traffic = json.load(open(pmc)).get('hbm_bytes_per_launch')
+                    pj = json.load(open(pmc))
+                    traffic, traffic_src = pj.get('hbm_bytes_per_launch'), pj.get('source')
                 except Exception:
                     traffic = None
             check['mean_iterations_ref'] = float(kref.mean())
-            roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
+            roof = {'bound': 'mfma', 'achieved': round(achieved, 4),
                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                     'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
                     'kernel_ms': round(kernel_ms, 4), 'flops_per_launch': flops_launch,
-                    'note': 'FP64 vector-ALU roof (78.6 TF/s; the kernel issues no MFMA: 5x5 '
-                            'stage blocks); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
+                    'traffic_source': traffic_src,
+                    'note': 'FP64 compute roof: 78.6 TF/s is both the FP64 MFMA and the FP64 '
+                            'vector peak of MI355X; this kernel issues no MFMA (5x5 stage blocks, '
+                            'DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
-                            '(profiles/)'}
-            if args.config == 'C2':
+                            'passes of this config (traffic_source)'}
+            st_json = os.path.join(ROOT, 'profiles', 'stamps_%s.json' % args.config)
+            if args.precision == 'fp64' and os.path.exists(st_json):
                 # latency roof: at batch 1024 one instance runs per SIMD, so the
                 # kernel time is one instance's dependency chain; the stage wave (Riccati factor,
                 # two sweeps, update) works this fraction of the instance's cycles and waits on
-                # the row wave for the rest (s_memtime stamps, diagnostic build)
-                roof['latency'] = {'stage_wave_busy_frac': 0.757,
-                                   'stage_wave_cycles_per_iter': 54100,
-                                   'source': 'profiles/r02_h/stamps.log'}
+                # the row wave for the rest (s_memtime stamps of the diagnostic build,
+                # tools/stamps.py --json); current_source says whether they were taken on the
+                # kernel source this bench runs
+                try:
+                    sj = json.load(open(st_json))
+                    src = os.path.join(ROOT, 'learning-based-mpc_amd', 'csrc', 'bqp_ocp.hip')
+                    roof['latency'] = {
+                        'stage_wave_busy_frac': round(sj['stage_wave_busy_frac'], 4),
+                        'stage_wave_cycles_per_iter': round(sj['stage_wave_cycles_per_iter']),
+                        'current_source': sj.get('source_sha1') == hashlib.sha1(open(src, 'rb').read()).hexdigest(),
+                        'source': os.path.relpath(st_json, ROOT)}
+                except Exception:
+                    pass
         line = {
             'metric': METRIC,
             'value': round(value, 1), 'unit': 'QP-steps/s', 'n_gpus': world, 'steps': args.steps,

@@ -58,7 +58,10 @@ typedef struct {
                           that continues every instance from its fp32 iterate to the fp64
                           tolerances (fp64 results; instances the fp32 phase ends with -2/-8,
                           or whose continuation does not converge, restart in fp64); applies to
-                          long horizons (N >= 64), shorter ones are solved in fp64 */
+                          long horizons (N >= 64), shorter ones are solved in fp64.  In mixed
+                          mode max_iter applies per phase, and bqp_output.iterations counts the
+                          fp32 + fp64 iterations of a continued instance, or only the fp64
+                          restart's iterations for an instance that restarts */
     int want_duals;    /* reserved (set 0): the structured API writes the multiplier outputs
                           whenever its `duals` argument is non-NULL */
     int polish;        /* structured API, fp64 active-set polish: the rows with lam > t are solved
@@ -198,7 +201,9 @@ int bqp_quadprog_batched_device(bqp_handle h, const bqp_dims* d, int batch,
  * on the LEARNED rollout x^L (terminal x^T = learned or nominal x_N), subject to the condensed
  * NOMINAL-model constraints Ain z <= bin (the host shim builds them from constraintsLBMPC.m /
  * hybrid_LBMPC_casadi.m:283-310).  The NW window is 7 x q column-major per instance: rows 1-3
- * X = [dx1; dx2; du], rows 4-7 Y (hybrid_LBMPC_casadi.m:128 layout; no validity mask).
+ * X = [dx1; dx2; du], rows 4-7 Y (hybrid_LBMPC_casadi.m:128 layout; no validity mask), or with
+ * mask = 1 the 8 x q window of DMS_LBMPC_casadi.m:158-161 whose row 8 is the validity v of
+ * casadiL2NW.m:14-28 (normaliser lambda + sum_j v_j k_j).
  * ---------------------------------------------------------------------------------------- */
 typedef struct {
     int nx, nu, np, N;
@@ -206,6 +211,7 @@ typedef struct {
     int term_learned;   /* terminal P cost on the learned (1, F3) or nominal (0, F4) x_N */
     int q;              /* points in the NW window (<= 512) */
     int m;              /* rows of Ain */
+    int mask;           /* 0: 7 x q window, every point counts; 1: 8 x q window with validity row */
 } bqp_lbmpc_dims;
 
 typedef struct {
@@ -213,7 +219,7 @@ typedef struct {
     const double *Lq, *Lr, *Lp, *Lt;  /* upper-triangular ROW-major weight factors:
                                          Lq'Lq = w Q, Lr'Lr = w R (w = running weight), Lp'Lp = P, Lt'Lt = T */
     const double *LAMBDA, *PSI, *xs;  /* nx*np, nu*np (column-major), nx */
-    const double* data; int64_t sdata;  /* NW window 7*q per instance (stride; 0 = shared) */
+    const double* data; int64_t sdata;  /* NW window (7 or 8)*q per instance (stride; 0 = shared) */
     const double* x0;   int64_t sx0;    /* nx per instance */
     const double* Ain;                  /* m*n column-major, shared */
     const double* bin;  int64_t sbin;   /* m per instance */
@@ -270,17 +276,19 @@ int bqp_closed_loop_ocp_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
                                double* U, int* exitflag, void* stream);
 
 /* ------------------------------------------------------------------------------------------
- * LBMPC closed loop with the learned model's data window:
- * matlab/LBMPC/examples/DMS_LBMPC_casadi.m:163-218.  Per step: the structured solve at the
+ * LBMPC closed loop with the learned model's data window: the data
+ * acquisition of matlab/LBMPC/examples/DMS_LBMPC_casadi.m:198-207 around a structured QP
+ * solve (LBMPC_casadi.m:163-218).  Per step: the structured solve at the
  * measured state, the plant step, then the data acquisition of the reference -
  *   X = [dx1; dx2; du], Y = (x+ - x_eq) - (A dx + B du)          (:202-206, deviation coords)
  *   window <- get_data(X, Y, q, it, window)                     (utilities/get_data.m)
  * and the logged learned prediction xl = x_eq + A dx + B du + g(X, Y, v) with the window before
- * the update (:199, casadiL2NW.m).  In that script the learned states enter only equality rows
- * that no cost term or inequality reads, so the per-step OCP is the QP the caller poses in
- * `data` (its own form: F_x_d and the terminal set on x_1, polytope at stage 1); the window
- * drives xl.  A, B of the window update are data->A / data->B.  Same loop and outputs as
- * bqp_closed_loop_ocp, plus: */
+ * the update (:199, casadiL2NW.m).  The per-step OCP is the QP the caller poses in `data`: the
+ * loop of matlab/LBMPC/examples/LBMPC_casadi.m (its learned dynamics are commented out of the
+ * constraints, :292, so the per-step problem is the tracking QP with F_x_d and the terminal set
+ * on x_1, polytope at stage 1; the window drives xl).  The learned-model NLP loop of
+ * DMS_LBMPC_casadi.m, whose cost reads the learned states, is bqp_closed_loop_sqp below.  A, B of
+ * the window update are data->A / data->B.  Same loop and outputs as bqp_closed_loop_ocp, plus: */
 typedef struct {
     int q;               /* points in the data window (get_data.m's q) */
     int mask;            /* 1: 8 x q window with validity row v, only the first (zero) point valid
@@ -301,6 +309,45 @@ int bqp_closed_loop_lbmpc_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
                                  const bqp_closed_loop* cl, const bqp_learning* lw,
                                  const double* x_init, double* X, double* U, int* exitflag,
                                  void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Learned-model NLP closed loop: per time step the batched SQP of
+ * bqp_lbmpc_solve_batched at the measured states, one plant step with the first input, and the
+ * data acquisition of the reference into each instance's window - the loops of
+ *   matlab/LBMPC/examples/DMS_LBMPC_casadi.m:163-218   (d->mask = 1, lw->mask = 1: 8 x q window,
+ *       learned states in the cost incl. the terminal term: term_learned = 1, K = 0, n_run = N)
+ *   matlab/LBMPC/examples/hybrid_LBMPC_casadi.m:163-204 (F4: term_learned = 0, K = 0, n_run = N;
+ *       7-row window: lw->mask = 0 keeps every point valid)
+ *   matlab/LBMPC/examples/LBMPC_RunExample.m / functions/ocpLBMPC.m (F3: K = Kstabil)
+ * The solver's window is the loop's own ring buffer (8 doubles per point, data->data, data->sdata,
+ * data->x0 and data->bin are ignored): get_data.m's window with its columns in ring order (the NW
+ * sums do not depend on the column order).  The condensed nominal constraints of each step are
+ *   Ain z <= bin0 + Bx dx0   (dx0 = measured state - x_eq; bin0: m, Bx: m*nx column-major),
+ * the first input applied is u_0 = u_eq + K dx0 + z_0.  Warm start (warm = 1): the previous
+ * solution shifted one stage with a zero last move and the same theta (the scripts' guess
+ * u0 = [u_OL(2:end); u_eq + Kstabil x_N], DMS_LBMPC_casadi.m:209-213, with the tail move of the
+ * scripts' Kstabil = 0 case); warm = 0: z = 0 every step (u = u_eq, theta = 0).  opt->max_iter
+ * bounds the SQP iterations per step.  X, U, exitflag and lw->XL / lw->window as in
+ * bqp_closed_loop_lbmpc; Z (batch*steps*n, may be NULL): every step's SQP solution z;
+ * iterations (batch*steps, may be NULL): SQP iterations per step.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+    const double* bin0;  /* m */
+    const double* Bx;    /* m * nx, column-major */
+    int warm;
+    double* Z;           /* out, may be NULL */
+    int* iterations;     /* out, may be NULL */
+} bqp_sqp_loop;
+
+int bqp_closed_loop_sqp(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                        const bqp_lbmpc_data* data, const bqp_sqp_loop* sl,
+                        const bqp_options* opt, const bqp_closed_loop* cl, const bqp_learning* lw,
+                        const double* x_init, double* X, double* U, int* exitflag);
+int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                               const bqp_lbmpc_data* data, const bqp_sqp_loop* sl,
+                               const bqp_options* opt, const bqp_closed_loop* cl,
+                               const bqp_learning* lw, const double* x_init, double* X, double* U,
+                               int* exitflag, void* stream);
 
 /* Timing of the most recent solve on this handle: kernel time measured with hipEvents on the
  * launch stream (ms), and the number of kernel launches it covered. */

@@ -53,7 +53,11 @@ class Strides(C.Structure):
 
 
 class LbmpcDims(C.Structure):
-    _fields_ = [(n, C.c_int) for n in ('nx', 'nu', 'np', 'N', 'n_run', 'term_learned', 'q', 'm')]
+    _fields_ = [(n, C.c_int) for n in ('nx', 'nu', 'np', 'N', 'n_run', 'term_learned', 'q', 'm', 'mask')]
+
+
+class SqpLoop(C.Structure):
+    _fields_ = [('bin0', _PD), ('Bx', _PD), ('warm', C.c_int), ('Z', _PD), ('iterations', _PI)]
 
 
 class LbmpcData(C.Structure):
@@ -68,7 +72,7 @@ EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version',
            'bqp_quadprog_batched_device', 'bqp_last_kernel_ms', 'bqp_nw_oracle',
            'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device',
            'bqp_closed_loop_ocp', 'bqp_closed_loop_ocp_device', 'bqp_closed_loop_lbmpc',
-           'bqp_closed_loop_lbmpc_device']
+           'bqp_closed_loop_lbmpc_device', 'bqp_closed_loop_sqp', 'bqp_closed_loop_sqp_device']
 
 _lib = None
 
@@ -125,6 +129,13 @@ def load():
                                                  C.POINTER(OcpData), C.POINTER(Options),
                                                  C.c_void_p, C.c_void_p, _PD, _PD, _PD, _PI,
                                                  C.c_void_p]
+    lib.bqp_closed_loop_sqp.argtypes = [C.c_void_p, C.POINTER(LbmpcDims), C.c_int,
+                                        C.POINTER(LbmpcData), C.POINTER(SqpLoop), C.POINTER(Options),
+                                        C.c_void_p, C.c_void_p, _PD, _PD, _PD, _PI]
+    lib.bqp_closed_loop_sqp_device.argtypes = [C.c_void_p, C.POINTER(LbmpcDims), C.c_int,
+                                               C.POINTER(LbmpcData), C.POINTER(SqpLoop),
+                                               C.POINTER(Options), C.c_void_p, C.c_void_p, _PD,
+                                               _PD, _PD, _PI, C.c_void_p]
     _lib = lib
     return lib
 

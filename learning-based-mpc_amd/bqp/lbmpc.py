@@ -10,6 +10,11 @@ Nadaraya-Watson oracle (bqp_nw_oracle).
 * ``HybridLBMPC`` ``examples/hybrid_LBMPC_casadi.m:250-311``: IPOPT over
                   ``y = [x_0..x_N; u_0..u_{N-1}; theta]`` with the learned rollout in the
                   running cost (delta-weighted) and the nominal decision x_N in the terminal cost.
+* ``DMSLBMPC``    ``examples/DMS_LBMPC_casadi.m:121-129, 223-292``: IPOPT over
+                  ``y = [xl_0..xl_N; x_0..x_N; u; theta]`` - the cost reads the LEARNED states
+                  xl (running and terminal), the learned dynamics tie xl to u, the nominal x
+                  carries the constraints; the 8 x q window with the validity row of
+                  casadiL2NW.m.  Closed loop: ``bqp.closed_loop_sqp``.
 
 This module only marshals data: the nominal-model constraints are condensed once per problem
 (A_in is shared; b_in is affine in the measured state), everything iterative runs on the GPU.
@@ -25,13 +30,17 @@ from .ocp import OcpResult, _default_handle
 def _window(data):
     """7 x q NW window (rows X = [dx1; dx2; du], Y = 4 rows) -> (q, 7) C-order (= 7 x q
     column-major).  Accepts the 7-row matrix of hybrid_LBMPC_casadi.m or the struct form
-    {X: 3 x q, Y: 4 x q} of oracleL2NW.m / update_data.m."""
+    {X: 3 x q, Y: 4 x q} of oracleL2NW.m / update_data.m; an 8-row matrix is the window of
+    DMS_LBMPC_casadi.m with casadiL2NW.m's validity row -> (q, 8).  Returns the array and the
+    per-instance stride (0 = shared)."""
     if isinstance(data, dict):
         data = np.vstack([np.atleast_2d(data['X']), np.atleast_2d(data['Y'])])
     d = np.asarray(data, float)
+    if d.shape[-2] not in (7, 8):
+        raise ValueError('the NW window has 7 rows [X; Y] or 8 rows [X; Y; v], not %d' % d.shape[-2])
     if d.ndim == 2:
         return np.ascontiguousarray(d.T), 0
-    return np.ascontiguousarray(np.swapaxes(d, 1, 2)), 7 * d.shape[2]
+    return np.ascontiguousarray(np.swapaxes(d, 1, 2)), d.shape[1] * d.shape[2]
 
 
 def nw_oracle(data, xi, handle=None, bandwidth=0.5, lam=1e-3):
@@ -112,7 +121,7 @@ class _LearnedOCP:
         x0 = np.ascontiguousarray(np.atleast_2d(x0), dtype=np.float64)
         b = x0.shape[0]
         w, sd = _window(data)
-        q = w.shape[-2]
+        q, mask = w.shape[-2], int(w.shape[-1] == 8)
         bin_ = np.ascontiguousarray(self.b0[None, :] + x0 @ self.Bx.T)
         mrows = self.Ain.shape[0]
         z = np.zeros((b, self.nz)) if z0 is None else \
@@ -122,7 +131,8 @@ class _LearnedOCP:
         keep = [np.ascontiguousarray(a, dtype=np.float64) for a in
                 (self.A.T, self.B.T, self.K.T, self.Lq, self.Lr, self.Lp, self.Lt,
                  self.LAMBDA.T, self.PSI.T, self.xs)]
-        dims = _lib.LbmpcDims(self.n, self.m, self.p, self.N, self.n_run, int(self.term_learned), q, mrows)
+        dims = _lib.LbmpcDims(self.n, self.m, self.p, self.N, self.n_run, int(self.term_learned), q,
+                              mrows, mask)
         dd = _lib.LbmpcData(*[_lib.ptr(a) for a in keep], _lib.ptr(w), sd, _lib.ptr(x0), self.n,
                             _lib.ptr(self.Ain_cm), _lib.ptr(bin_), mrows, self.bandwidth, self.lam)
         o = _lib.options(max_iter=max_iter, tol_stat=tol)
@@ -168,8 +178,9 @@ class HybridLBMPC(_LearnedOCP):
         self.u_eq = np.atleast_1d(np.asarray(u_eq, float)).ravel()
 
     def solve(self, xmeasure, data, y0=None, handle=None, max_iter=50, tol=1e-8):
-        """xmeasure (batch, n) absolute states.  Returns y_OL (batch, (N+1)n + Nm + p) in the
-        reference's layout (nominal state trajectory, inputs, theta) and u0."""
+        """xmeasure (batch, n) absolute states, data the 7 x q window (or 8 x q with the validity
+        row).  Returns y_OL (batch, (N+1)n + Nm + p) in the reference's layout (nominal state
+        trajectory, inputs, theta) and u0."""
         xm = np.atleast_2d(xmeasure)
         x0 = xm - self.x_eq
         N, n, m = self.N, self.n, self.m
@@ -188,3 +199,26 @@ class HybridLBMPC(_LearnedOCP):
                             r.z[:, N * m:]], axis=1)
         r.update(y_OL=y, u0=u[:, 0, :] + self.u_eq, theta=r.z[:, N * m:])
         return r
+
+
+class DMSLBMPC(HybridLBMPC):
+    """CasADi DMS LBMPC (DMS_LBMPC_casadi.m:121-129): the running cost (delta-weighted, stages
+    k = 0..N-1, :229-233) and the terminal cost (:234, terminalcosts :245-247) on the LEARNED
+    states xl, which the learned dynamics xl_{k+1} = x_eq + A dxl + B du + casadiL2NW(dxl, du,
+    data) tie to the inputs (:268); the nominal states x carry the constraints (:262-276): at
+    k = 1 F_x_d and the robust terminal set on [x_1; theta], boxes on x_1..x_N and u_0..u_{N-1}.
+    Eliminating both state chains leaves z = [u - u_eq; theta] with the learned rollout in the
+    whole cost: the GN-SQP of HybridLBMPC with the terminal term on the learned x_N.  The window
+    is the 8 x q matrix [X; Y; v] (get_data.m; v = 1 on the valid points)."""
+
+    def __init__(self, A, B, Q, R, P, T, LAMBDA, PSI, F_x, h_x, F_u, h_u, F_w_N, h_w_N, F_x_d,
+                 h_x_d, x_eq, u_eq, N, delta=0.01, bandwidth=0.5, lam=1e-3):
+        super().__init__(A, B, Q, R, P, T, LAMBDA, PSI, F_x, h_x, F_u, h_u, F_w_N, h_w_N, F_x_d,
+                         h_x_d, x_eq, u_eq, N, delta=delta, bandwidth=bandwidth, lam=lam)
+        self.term_learned = True
+
+    def solve(self, xmeasure, data, y0=None, handle=None, max_iter=200, tol=1e-8):
+        """as HybridLBMPC.solve, data the 8 x q window [X; Y; v] (or 7 x q: every point valid);
+        the GN iteration converges linearly on these learned costs (about 60 SQP iterations on
+        the second step of the stored DMS_tLBMPC_q100 run), hence the larger default max_iter"""
+        return super().solve(xmeasure, data, y0=y0, handle=handle, max_iter=max_iter, tol=tol)

@@ -64,3 +64,53 @@ def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, **op
                                    _lib.ptr(U), _lib.iptr(flags))
     _lib.check(rc, 'bqp_closed_loop_lbmpc')
     return OcpResult(X=X, U=U, exitflag=flags, XL=XL, window=win)
+
+
+def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, handle=None,
+                    max_iter=200, tol=1e-8, log_z=False):
+    """Learned-model NLP closed loop on the GPU (bqp_closed_loop_sqp): per step the batched
+    Gauss-Newton SQP of mpc (a DMSLBMPC - DMS_LBMPC_casadi.m:163-218 -, HybridLBMPC -
+    hybrid_LBMPC_casadi.m:163-204 - or LBMPC) at the measured states, one RK4 plant step with the
+    first move, and get_data.m's window update.  x_init (batch, n) absolute.
+    learning=dict(q=100, mask=1[, bandwidth, lambda_]): mask 1 is DMS_LBMPC_casadi.m's 8 x q
+    window (only the first, zero point valid at the start), mask 0 counts every point (the 7-row
+    window of hybrid_LBMPC_casadi.m).  warm: the scripts' shifted guess (previous inputs moved one
+    stage, zero last move, theta kept); otherwise z = 0 each step.
+    Returns X (batch, steps+1, n), U (batch, steps, m) absolute, exitflag and iterations (batch,
+    steps), XL (batch, steps+1, n) the learned one-step predictions, window (batch, q, 8) the
+    final windows in ring order, and with log_z every step's solution Z (batch, steps, nz)."""
+    lib = _lib.load()
+    h = handle or _default_handle()
+    learning = dict(learning or {})
+    x_init = np.ascontiguousarray(np.atleast_2d(x_init), dtype=np.float64)
+    b = x_init.shape[0]
+    q = int(learning.get('q', 100))
+    mask = int(learning.get('mask', 1))
+    x_eq = np.ascontiguousarray(getattr(mpc, 'x_eq', np.zeros(mpc.n)), dtype=np.float64)
+    u_eq = np.ascontiguousarray(getattr(mpc, 'u_eq', np.zeros(mpc.m)), dtype=np.float64)
+    mrows = mpc.Ain.shape[0]
+    keep = [np.ascontiguousarray(a, dtype=np.float64) for a in
+            (mpc.A.T, mpc.B.T, mpc.K.T, mpc.Lq, mpc.Lr, mpc.Lp, mpc.Lt, mpc.LAMBDA.T, mpc.PSI.T,
+             mpc.xs)]
+    bin0 = np.ascontiguousarray(mpc.b0, dtype=np.float64)
+    Bx = np.ascontiguousarray(mpc.Bx.T, dtype=np.float64)        # column-major m x n
+    dims = _lib.LbmpcDims(mpc.n, mpc.m, mpc.p, mpc.N, mpc.n_run, int(mpc.term_learned), q, mrows, 1)
+    dd = _lib.LbmpcData(*[_lib.ptr(a) for a in keep], None, 0, None, 0, _lib.ptr(mpc.Ain_cm), None,
+                        0, mpc.bandwidth, mpc.lam)
+    X = np.zeros((b, steps + 1, mpc.n)); U = np.zeros((b, steps, mpc.m))
+    XL = np.zeros_like(X); win = np.zeros((b, q, 8))
+    flags = np.zeros((b, steps), np.int32); its = np.zeros((b, steps), np.int32)
+    Z = np.zeros((b, steps, mpc.nz)) if log_z else None
+    sl = _lib.SqpLoop(_lib.ptr(bin0), _lib.ptr(Bx), int(bool(warm)), _lib.ptr(Z), _lib.iptr(its))
+    cl = ClosedLoop(BQP_PLANT_MG_RK4, int(steps), float(delta), _lib.ptr(x_eq), _lib.ptr(u_eq))
+    lw = Learning(q, mask, float(learning.get('bandwidth', 0.0)), float(learning.get('lambda_', 0.0)),
+                  _lib.ptr(XL), _lib.ptr(win))
+    o = _lib.options(max_iter=max_iter, tol_stat=tol)
+    rc = lib.bqp_closed_loop_sqp(h.value, C.byref(dims), b, C.byref(dd), C.byref(sl), C.byref(o),
+                                 C.byref(cl), C.byref(lw), _lib.ptr(x_init), _lib.ptr(X),
+                                 _lib.ptr(U), _lib.iptr(flags))
+    _lib.check(rc, 'bqp_closed_loop_sqp')
+    out = OcpResult(X=X, U=U, exitflag=flags, iterations=its, XL=XL, window=win)
+    if log_z:
+        out.update(Z=Z)
+    return out

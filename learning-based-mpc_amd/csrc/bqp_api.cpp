@@ -214,10 +214,13 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         // needs ~4 iterations and ends at the fp64 solve's KKT accuracy (duals within ~3e-8 of
         // lambda*); later switches (mu 1e-7 .. 1e-9) save 3-7 % of the time but leave the duals
         // of some instances at 1e-7 .. 2e-7 (tools/diag_mixed.py, profiles/r02_mx/diag_switch.log).
-        // BQP_MIXED_MU overrides, for that sweep.
+        // BQP_MIXED_MU overrides, for that sweep (values outside (0, 1e-3] are ignored).
         o32.tol_comp = std::max(o.tol_comp, 1e-6);
-        const char* e = getenv("BQP_MIXED_MU");
-        if (e) o32.tol_comp = atof(e);
+        if (const char* e = getenv("BQP_MIXED_MU")) {
+            char* end = nullptr;
+            const double v = strtod(e, &end);
+            if (end != e && *end == '\0' && v > 0.0 && v <= 1e-3) o32.tol_comp = v;
+        }
     }
     if (f32) o = o32;
     const int nx = d->nx, nu = d->nu, np = d->np, N = d->N;
@@ -591,7 +594,9 @@ int bqp_nw_oracle(bqp_handle h, int batch, int q, const double* data, int64_t sd
 
 static int lbmpc_check(const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_data* D) {
     if (!d || !D || batch <= 0) return BQP_E_ARG;
-    if (d->N <= 0 || d->n_run < 0 || d->n_run > d->N || d->q <= 0 || d->m < 0) return BQP_E_ARG;
+    if (d->N <= 0 || d->n_run < 0 || d->n_run > d->N || d->q <= 0 || d->m < 0 ||
+        (d->mask != 0 && d->mask != 1))
+        return BQP_E_ARG;
     if (!D->A || !D->B || !D->K || !D->Lq || !D->Lr || !D->Lp || !D->Lt || !D->LAMBDA ||
         !D->PSI || !D->xs || !D->data || !D->x0 || (d->m > 0 && (!D->Ain || !D->bin)))
         return BQP_E_ARG;
@@ -641,6 +646,7 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     a.z = z; a.flag = exitflag; a.iters = iterations;
     a.N = N; a.n = n; a.nr = nr; a.m = m; a.q = d->q; a.n_run = d->n_run;
     a.term_learned = d->term_learned; a.batch = batch; a.ntrial = LB_NTRIAL;
+    a.wrows = d->mask ? 8 : 7;
     a.max_iter = o.max_iter;
     const double bw = D->bandwidth > 0 ? D->bandwidth : 0.5;
     a.hinv2 = 1.0 / (bw * bw);
@@ -665,7 +671,10 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     q.sH = (int64_t)n * n; q.sf = n; q.sA = 0; q.sb = m;
     q.x = a.d; q.lam_ineqlin = a.lam; q.exitflag = a.qpflag;
     q.work = (double*)h->dwork.p; q.work_stride = wst;
-    q.polish = o.polish < 0 ? 0 : 1;
+    // every sub-problem polished to its active-set solution: the GN iteration converges linearly
+    // (60-80 iterations on the learned costs of DMS_LBMPC_casadi.m), and interior-point steps
+    // accurate to ~1e-8 left it wandering at that level (tools/diag_dms_gpu.py)
+    q.polish = o.polish < 0 ? 0 : 2;
     q.stats = (double*)h->dwork.p + (size_t)wst * B;
     HIP_TRY(hipEventRecord(h->ev0, st));
     int launches = 0;
@@ -707,7 +716,7 @@ int bqp_lbmpc_solve_batched(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
         {D->Lr, (size_t)nu * nu, nullptr}, {D->Lp, (size_t)nx * nx, nullptr},
         {D->Lt, (size_t)nx * nx, nullptr}, {D->LAMBDA, (size_t)nx * np, nullptr},
         {D->PSI, (size_t)nu * np, nullptr}, {D->xs, (size_t)nx, nullptr},
-        {D->data, span(batch, D->sdata, (size_t)7 * d->q), nullptr},
+        {D->data, span(batch, D->sdata, (size_t)(d->mask ? 8 : 7) * d->q), nullptr},
         {D->x0, span(batch, D->sx0, nx), nullptr},
         {D->Ain, (size_t)m * n, nullptr}, {D->bin, span(batch, D->sbin, m), nullptr},
         {z, (size_t)batch * n, nullptr},
@@ -906,6 +915,159 @@ int bqp_closed_loop_lbmpc(bqp_handle h, const bqp_ocp_dims* d, int batch, const 
                           int* exitflag) {
     if (!lw) return BQP_E_ARG;
     return closed_loop_host(h, d, batch, D, opt, cl, lw, x_init, X, U, exitflag);
+}
+
+// ------------------------------------------------------------------------------------------
+// learned-model NLP closed loop: batched SQP + true-plant step + data window, per time step
+// ------------------------------------------------------------------------------------------
+static int sqp_loop_check(const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_data* D,
+                          const bqp_sqp_loop* sl, const bqp_closed_loop* cl,
+                          const bqp_learning* lw, const double* x_init, const double* X,
+                          const double* U) {
+    if (!d || !D || !sl || !cl || !lw || !x_init || !X || !U || batch <= 0) return BQP_E_ARG;
+    if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
+        return BQP_E_ARG;
+    if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;   // the MG plant
+    if (lw->q != d->q || !lw->XL || (lw->mask != 0 && lw->mask != 1)) return BQP_E_ARG;
+    if (d->m > 0 && (!sl->bin0 || !sl->Bx)) return BQP_E_ARG;
+    // the loop supplies the window, the measured state and the rhs: check the rest
+    bqp_lbmpc_data Dc = *D;
+    double dummy = 0.0;
+    Dc.data = &dummy; Dc.x0 = &dummy; Dc.bin = &dummy;
+    bqp_lbmpc_dims dc = *d;
+    dc.mask = 1;
+    return lbmpc_check(&dc, batch, &Dc);
+}
+
+int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                               const bqp_lbmpc_data* D, const bqp_sqp_loop* sl,
+                               const bqp_options* opt, const bqp_closed_loop* cl,
+                               const bqp_learning* lw, const double* x_init, double* X, double* U,
+                               int* exitflag, void* stream) {
+    if (!h) return BQP_E_ARG;
+    int rc = sqp_loop_check(d, batch, D, sl, cl, lw, x_init, X, U);
+    if (rc) return rc;
+    DevScope ds(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    const int nx = d->nx, N = d->N, m = d->m, q = d->q;
+    const int n = N * d->nu + d->np;
+    const size_t B = batch;
+    const size_t nd = B * nx + B * n + B * m + B + B * (size_t)q * 8;
+    HIP_TRY(h->cwork.reserve(sizeof(double) * nd + sizeof(int) * 2 * B));
+    double* s = (double*)h->cwork.p;     // measured deviation state
+    double* z = s + B * nx;               // SQP iterate / solution
+    double* bin = z + B * n;              // rhs of the step's constraints
+    double* uo = bin + B * m;             // first input (deviation)
+    double* win = uo + B;                 // window ring, 8 doubles per point
+    int* fl = (int*)(win + B * (size_t)q * 8);
+    int* it = fl + B;
+    if (lw->window) win = lw->window;
+    HIP_TRY(bqp::launch_closed_loop_init(batch, nx, cl->steps, x_init, cl->x_eq, s, X, st));
+    HIP_TRY(bqp::launch_lbmpc_window_init(batch, cl->steps, q, lw->mask, x_init, win, lw->XL, st));
+    HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));
+    const double bw = lw->bandwidth > 0 ? lw->bandwidth : 0.5;
+    const double lam = lw->lambda > 0 ? lw->lambda : 1e-3;
+    bqp_lbmpc_dims dl = *d;
+    dl.mask = 1;                          // the loop's window always carries the validity row
+    bqp_lbmpc_data Dl = *D;
+    Dl.data = win; Dl.sdata = (int64_t)q * 8;
+    Dl.x0 = s; Dl.sx0 = nx;
+    Dl.bin = bin; Dl.sbin = m;
+    Dl.bandwidth = bw; Dl.lambda = lam;
+    hipEvent_t e0 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventRecord(e0, st));
+    int launches = 0;
+    for (int t = 0; t < cl->steps; ++t) {
+        HIP_TRY(bqp::launch_sqp_loop_prep(batch, nx, n, m, N * d->nu, t > 0 && sl->warm, s,
+                                          sl->bin0, sl->Bx, bin, z, st));
+        if (t > 0 && !sl->warm) HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));
+        rc = bqp_lbmpc_solve_batched_device(h, &dl, batch, &Dl, opt, z, nullptr, nullptr, fl, it,
+                                            stream);
+        if (rc) { hipEventDestroy(e0); return rc; }
+        launches += h->launches;
+        HIP_TRY(bqp::launch_sqp_loop_u0(batch, nx, n, D->K, s, z, uo, it, cl->steps, t,
+                                        sl->Z, sl->iterations, st));
+        HIP_TRY(bqp::launch_mg_plant(batch, 1, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
+                                     s, X, U, exitflag, st));
+        HIP_TRY(bqp::launch_lbmpc_window(batch, cl->steps, t, q, bw, lam, D->A, 0, D->B, 0,
+                                         cl->x_eq, cl->u_eq, X, U, win, lw->XL, st));
+        launches += 3;
+    }
+    HIP_TRY(hipEventRecord(h->ev1, st));
+    HIP_TRY(hipEventSynchronize(h->ev1));
+    std::swap(h->ev0, e0);
+    hipEventDestroy(e0);
+    h->timed = true;
+    h->launches = launches;
+    return BQP_OK;
+}
+
+int bqp_closed_loop_sqp(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                        const bqp_lbmpc_data* D, const bqp_sqp_loop* sl, const bqp_options* opt,
+                        const bqp_closed_loop* cl, const bqp_learning* lw, const double* x_init,
+                        double* X, double* U, int* exitflag) {
+    if (!h) return BQP_E_ARG;
+    int rc = sqp_loop_check(d, batch, D, sl, cl, lw, x_init, X, U);
+    if (rc) return rc;
+    DevScope ds(h->device);
+    const int nx = d->nx, nu = d->nu, np = d->np, N = d->N, m = d->m, q = d->q;
+    const int n = N * nu + np;
+    struct In { const double* src; size_t n; double* dst; };
+    In in[] = {
+        {D->A, (size_t)nx * nx, nullptr}, {D->B, (size_t)nx * nu, nullptr},
+        {D->K, (size_t)nu * nx, nullptr}, {D->Lq, (size_t)nx * nx, nullptr},
+        {D->Lr, (size_t)nu * nu, nullptr}, {D->Lp, (size_t)nx * nx, nullptr},
+        {D->Lt, (size_t)nx * nx, nullptr}, {D->LAMBDA, (size_t)nx * np, nullptr},
+        {D->PSI, (size_t)nu * np, nullptr}, {D->xs, (size_t)nx, nullptr},
+        {D->Ain, (size_t)m * n, nullptr}, {sl->bin0, (size_t)m, nullptr},
+        {sl->Bx, (size_t)m * nx, nullptr}, {x_init, (size_t)batch * nx, nullptr},
+        {cl->x_eq, (size_t)nx, nullptr}, {cl->u_eq, (size_t)nu, nullptr},
+    };
+    const int nin = sizeof(in) / sizeof(in[0]);
+    const size_t B = batch, S = cl->steps;
+    const size_t nX = B * (S + 1) * nx, nU = B * S * nu, nW = B * (size_t)q * 8, nZ = B * S * n;
+    size_t tot = 2 * nX + nU + nW + (sl->Z ? nZ : 0);
+    for (int i = 0; i < nin; ++i) tot += (in[i].src ? in[i].n : 0);
+    HIP_TRY(h->stage.reserve(sizeof(double) * tot + sizeof(int) * 2 * B * S));
+    double* cur = (double*)h->stage.p;
+    for (int i = 0; i < nin; ++i) {
+        if (!in[i].src || in[i].n == 0) continue;
+        in[i].dst = cur;
+        HIP_TRY(hipMemcpyAsync(cur, in[i].src, sizeof(double) * in[i].n, hipMemcpyHostToDevice, h->stream));
+        cur += in[i].n;
+    }
+    double* Xd = cur; cur += nX;
+    double* Ud = cur; cur += nU;
+    double* XLd = cur; cur += nX;
+    double* Wd = cur; cur += nW;
+    double* Zd = nullptr;
+    if (sl->Z) { Zd = cur; cur += nZ; }
+    int* Fd = (int*)cur;
+    int* Id = Fd + B * S;
+    bqp_lbmpc_data Dd = *D;
+    Dd.A = in[0].dst; Dd.B = in[1].dst; Dd.K = in[2].dst; Dd.Lq = in[3].dst; Dd.Lr = in[4].dst;
+    Dd.Lp = in[5].dst; Dd.Lt = in[6].dst; Dd.LAMBDA = in[7].dst; Dd.PSI = in[8].dst;
+    Dd.xs = in[9].dst; Dd.Ain = in[10].dst;
+    bqp_sqp_loop sd = *sl;
+    sd.bin0 = in[11].dst; sd.Bx = in[12].dst;
+    sd.Z = Zd; sd.iterations = sl->iterations ? Id : nullptr;
+    bqp_closed_loop cd = *cl;
+    cd.x_eq = in[14].dst; cd.u_eq = in[15].dst;
+    bqp_learning ld = *lw;
+    ld.XL = XLd; ld.window = Wd;
+    rc = bqp_closed_loop_sqp_device(h, d, batch, &Dd, &sd, opt, &cd, &ld, in[13].dst, Xd, Ud,
+                                    exitflag ? Fd : nullptr, h->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(X, Xd, sizeof(double) * nX, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(U, Ud, sizeof(double) * nU, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(lw->XL, XLd, sizeof(double) * nX, hipMemcpyDeviceToHost, h->stream));
+    if (lw->window) HIP_TRY(hipMemcpyAsync(lw->window, Wd, sizeof(double) * nW, hipMemcpyDeviceToHost, h->stream));
+    if (sl->Z) HIP_TRY(hipMemcpyAsync(sl->Z, Zd, sizeof(double) * nZ, hipMemcpyDeviceToHost, h->stream));
+    if (exitflag) HIP_TRY(hipMemcpyAsync(exitflag, Fd, sizeof(int) * B * S, hipMemcpyDeviceToHost, h->stream));
+    if (sl->iterations) HIP_TRY(hipMemcpyAsync(sl->iterations, Id, sizeof(int) * B * S, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return BQP_OK;
 }
 
 #ifdef BQP_STAMPS

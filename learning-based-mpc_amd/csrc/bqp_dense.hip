@@ -1173,7 +1173,7 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             wave_sync();
         }
     }
-    if (a.polish && (flag == 0 || flag == -8) && a.work) {
+    if (a.polish && (flag == 0 || flag == -8 || (a.polish == 2 && flag == 1)) && a.work) {
         // hand the iterate to dense_polish_kernel through the instance's workspace (DWork)
         const DWork L = DWork::make(n, m, 0);
         double* W = a.work + (int64_t)inst * a.work_stride;
@@ -1206,7 +1206,9 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     }
 }
 
-// the active-set polish of the instances that ended 0 / -8 (dense_polish), a kernel of its own
+// the active-set polish of the instances that ended 0 / -8 (dense_polish), a kernel of its own;
+// polish = 2 (the SQP sub-problems of bqp_lbmpc_solve_batched) polishes converged instances too,
+// so that the SQP steps are the exact active-set solutions (as oracle/dense_qp.py's are)
 // so that its registers do not weigh on the IPM kernels; the iterate is in the workspace (DWork
 // offsets: dense_ipm_kernel keeps it there, dense_wave_kernel stores it on those exits).  On
 // acceptance x, the multipliers, fval, the flag (1) and the stats are rewritten.
@@ -1214,7 +1216,7 @@ __global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
     if (inst >= a.batch) return;
     const int flag = a.exitflag[inst];
-    if (flag != 0 && flag != -8) return;
+    if (!(flag == 0 || flag == -8 || (a.polish == 2 && flag == 1))) return;
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
     __shared__ double sc[16];
     __shared__ double xs[DT];

@@ -88,7 +88,8 @@ struct DenseKernelArgs {
     double* stats;
     double* work;      // per-instance scratch (global), work_stride doubles each
     int64_t work_stride;
-    int polish;        // 1: active-set polish after a 0 / -8 exit (bqp_dense.hip::dense_polish)
+    int polish;        // 1: active-set polish after a 0 / -8 exit (bqp_dense.hip::dense_polish);
+                       // 2: also after a converged exit (exact active-set steps for the SQP)
 };
 
 int dense_work_doubles(int n, int m, int me);
@@ -96,9 +97,10 @@ hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st);
 
 // Learning-based MPC (Gauss-Newton SQP on the NW-learned model), bqp_lbmpc.hip.  Small
 // matrices column-major (A nx*nx, B nx*nu, K nu*nx, LAMBDA nx*np, PSI nu*np); weight factors
-// upper-triangular row-major (Lq nx*nx, Lr nu*nu, Lp, Lt nx*nx); NW window 7 x q column-major.
+// upper-triangular row-major (Lq nx*nx, Lr nu*nu, Lp, Lt nx*nx); NW window wrows x q
+// column-major (7: [X; Y], 8: [X; Y; v] with the validity row of casadiL2NW.m).
 struct LbmpcArgs {
-    int N, n, nr, m, q, n_run, term_learned, batch, ntrial, max_iter;
+    int N, n, nr, m, q, n_run, term_learned, batch, ntrial, max_iter, wrows;
     double hinv2, lam_nw, tol_step, tol_stat;
     const double *A, *B, *K, *Lq, *Lr, *Lp, *Lt, *LAM, *PSI, *xs;
     const double* data; int64_t sdata;
@@ -127,6 +129,15 @@ hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* x
 hipError_t launch_mg_plant(int batch, int N, int steps, int t, double delta, const double* uo,
                            const int* fl, const double* xeq, const double* ueq, double* s,
                            double* X, double* U, int* flags, hipStream_t st);
+// learned-model NLP closed loop glue (bqp_closed_loop_sqp): per instance bin = bin0 + Bx s and
+// the warm start (z shifted one stage, zero last move, theta kept) before the SQP; u_0 = K s + z_0
+// for the plant, and the step's z / iteration count into the caller's logs after it
+hipError_t launch_sqp_loop_prep(int batch, int nx, int n, int m, int nv, int shift, const double* s,
+                                const double* bin0, const double* Bx, double* bin, double* z,
+                                hipStream_t st);
+hipError_t launch_sqp_loop_u0(int batch, int nx, int n, const double* K, const double* s,
+                              const double* z, double* uo, const int* it, int steps, int t,
+                              double* Zlog, int* itlog, hipStream_t st);
 hipError_t launch_lbmpc_window_init(int batch, int steps, int q, int mask, const double* xinit,
                                     double* win, double* XL, hipStream_t st);
 hipError_t launch_lbmpc_window(int batch, int steps, int t, int q, double bw, double lam,

@@ -31,18 +31,22 @@ namespace bqp {
 #define LB_MAXQ 512      // NW window capacity (data points) held in LDS
 #define LB_CPL 4         // z columns per lane in the sensitivity recursion (n <= 256)
 
-// NW sums at xi over the window in LDS (7 x q, column-major: point i at D[7 i .. 7 i + 6]).
-// Returns g (4) and, if JAC, dg (4 x 3, row-major); every lane ends with the uniform values.
+// NW sums at xi over the window in LDS: point i at D[wr i .. wr i + wr - 1], wr = 7 rows
+// [X; Y] (every point counts in the normaliser, oracleL2NW.m / hybrid_LBMPC_casadi.m:331-358) or
+// wr = 8 rows [X; Y; v] (casadiL2NW.m:14-28: the normaliser is lambda + sum_j v_j k_j, the
+// numerator is not masked - points that are not yet valid hold Y = 0).  Returns g (4) and, if
+// JAC, dg (4 x 3, row-major); every lane ends with the uniform values.
 template <bool JAC>
-__device__ __forceinline__ void nw_eval(const double* D, int q, double hinv2, double lam,
+__device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double hinv2, double lam,
                                         const double (&xi)[3], double (&g)[4], double (&dg)[4][3],
                                         int lane) {
     double s = 0.0, sy[4] = {0, 0, 0, 0}, ds[3] = {0, 0, 0}, dsy[4][3] = {};
     for (int i = lane; i < q; i += LB_WAVE) {
-        const double* p = D + 7 * i;
+        const double* p = D + wr * i;
         const double d0 = p[0] - xi[0], d1 = p[1] - xi[1], d2 = p[2] - xi[2];
         const double k = exp(-(d0 * d0 + d1 * d1 + d2 * d2) * hinv2);
-        s += k;
+        const double v = wr == 8 ? p[7] : 1.0;
+        s += k * v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) sy[r] += p[3 + r] * k;
         if (JAC) {
@@ -50,7 +54,7 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, double hinv2, do
             const double dk[3] = {c * d0, c * d1, c * d2};
 #pragma unroll
             for (int c3 = 0; c3 < 3; ++c3) {
-                ds[c3] += dk[c3];
+                ds[c3] += dk[c3] * v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) dsy[r][c3] += p[3 + r] * dk[c3];
             }
@@ -77,8 +81,8 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, double hinv2, do
     }
 }
 
-__device__ __forceinline__ void load_window(double* D, const double* src, int q, int lane) {
-    for (int i = lane; i < 7 * q; i += LB_WAVE) D[i] = src[i];
+__device__ __forceinline__ void load_window(double* D, const double* src, int len, int lane) {
+    for (int i = lane; i < len; i += LB_WAVE) D[i] = src[i];
     wave_sync();
 }
 
@@ -93,10 +97,10 @@ __global__ void __launch_bounds__(64) nw_oracle_kernel(int batch, int q, const d
     const int b = blockIdx.x;
     const int lane = threadIdx.x;
     if (b >= batch) return;
-    load_window(D, data + (int64_t)b * sdata, q, lane);
+    load_window(D, data + (int64_t)b * sdata, 7 * q, lane);
     double xi[3] = {xi_in[3 * b], xi_in[3 * b + 1], xi_in[3 * b + 2]};
     double g[4], dg[4][3];
-    nw_eval<true>(D, q, hinv2, lam, xi, g, dg, lane);
+    nw_eval<true>(D, q, 7, hinv2, lam, xi, g, dg, lane);
     if (lane == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -114,13 +118,13 @@ __global__ void __launch_bounds__(64) nw_oracle_kernel(int batch, int q, const d
 template <int NX, int NU, int NP>
 __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) {
     static_assert(NX >= 2 && NU == 1, "NW input xi = [x_1; x_2; u] needs nx >= 2, nu = 1");
-    __shared__ double D[7 * LB_MAXQ];
+    __shared__ double D[8 * LB_MAXQ];
     const int lane = threadIdx.x;
     const int nt = gn ? 1 : a.ntrial;
     const int b = blockIdx.x / nt, t = blockIdx.x % nt;
     if (b >= a.batch || a.done[b]) return;
     const int N = a.N, n = a.n, nr = a.nr;
-    load_window(D, a.data + (int64_t)b * a.sdata, a.q, lane);
+    load_window(D, a.data + (int64_t)b * a.sdata, a.wrows * a.q, lane);
     const double alpha = gn ? 0.0 : ldexp(1.0, -t);
     const double* z = a.z + (int64_t)b * n;
     const double* dz = a.d + (int64_t)b * n;
@@ -205,8 +209,8 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         // learned step
         const double xi[3] = {x[0], x[1], u};
         double g[4], dg[4][3];
-        if (gn) nw_eval<true>(D, a.q, a.hinv2, a.lam_nw, xi, g, dg, lane);
-        else nw_eval<false>(D, a.q, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        if (gn) nw_eval<true>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        else nw_eval<false>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
         double x1[NX], xn1[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {

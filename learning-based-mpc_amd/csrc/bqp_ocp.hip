@@ -740,9 +740,13 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
                 for (int y = 0; y < NP; ++y) W[L.L0 + x * NP + y] = L0[x][y];
         }
-        // long horizons: the global P_k stores complete before the solves read them (the
-        // reads are agent-scope, past the L1)
-        if constexpr (LNG) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // long horizons: the global P_k stores complete before the solves read them.  Writer and
+        // readers are this wave (other lanes): the stores reach this XCD's L2 once the vector
+        // memory counter drains, and the reads are agent-scope (sc1, past the L1), so no L2
+        // write-back is needed - the tables stay dirty in L2 and are rewritten in place by the
+        // next factorisation (an agent-scope release wrote the XCD's dirty lines back to HBM
+        // once per factorisation: 1.29 GB of writes per C5 launch, profiles/r02_c5pmc)
+        if constexpr (LNG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_sync();
         return ok;
     };

@@ -146,6 +146,66 @@ __global__ void lbmpc_window_init_kernel(int batch, int steps, int q, int mask,
     if (threadIdx.x < 4) XL[(int64_t)b * (steps + 1) * 4 + threadIdx.x] = xinit[(int64_t)b * 4 + threadIdx.x];
 }
 
+// ------------------------------------------------------------------------------------------
+// learned-model NLP loop glue (bqp_closed_loop_sqp_device).  One workgroup per instance.
+// prep: bin = bin0 + Bx s (the condensed nominal constraints at the measured deviation state s,
+// Bx column-major m x nx) and, with shift, the warm start z <- [z_1 .. z_{nv-1}, 0, theta]
+// (DMS_LBMPC_casadi.m:209-213 with Kstabil's tail move 0; nu = 1, nv = N moves then theta)
+// ------------------------------------------------------------------------------------------
+__global__ void sqp_loop_prep_kernel(int nx, int n, int m, int nv, int shift, const double* s,
+                                     const double* bin0, const double* Bx, double* bin, double* z) {
+    const int b = blockIdx.x;
+    const double* sb = s + (int64_t)b * nx;
+    double* bb = bin + (int64_t)b * m;
+    for (int r = threadIdx.x; r < m; r += blockDim.x) {
+        double v = bin0[r];
+        for (int j = 0; j < nx; ++j) v += Bx[(int64_t)j * m + r] * sb[j];
+        bb[r] = v;
+    }
+    if (shift) {
+        double* zb = z + (int64_t)b * n;
+        // read all moves before any write (one pass per thread block, n <= a few hundred)
+        double v[4];
+        int cnt = 0;
+        for (int j = threadIdx.x; j < nv && cnt < 4; j += blockDim.x, ++cnt)
+            v[cnt] = (j + 1 < nv) ? zb[j + 1] : 0.0;
+        __syncthreads();
+        cnt = 0;
+        for (int j = threadIdx.x; j < nv && cnt < 4; j += blockDim.x, ++cnt) zb[j] = v[cnt];
+    }
+}
+
+// u_0 = K s + z_0 (deviation) for the plant kernel (stride 1); log z and the iteration count
+__global__ void sqp_loop_u0_kernel(int batch, int nx, int n, const double* K, const double* s,
+                                   const double* z, double* uo, const int* it, int steps, int t,
+                                   double* Zlog, int* itlog) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    double u = z[(int64_t)b * n];
+    for (int j = 0; j < nx; ++j) u += K[j] * s[(int64_t)b * nx + j];
+    uo[b] = u;
+    if (itlog) itlog[(int64_t)b * steps + t] = it[b];
+    if (Zlog)
+        for (int j = 0; j < n; ++j) Zlog[((int64_t)b * steps + t) * n + j] = z[(int64_t)b * n + j];
+}
+
+hipError_t launch_sqp_loop_prep(int batch, int nx, int n, int m, int nv, int shift, const double* s,
+                                const double* bin0, const double* Bx, double* bin, double* z,
+                                hipStream_t st) {
+    if (nv > 4 * 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sqp_loop_prep_kernel, dim3(batch), dim3(256), 0, st, nx, n, m, nv, shift, s,
+                       bin0, Bx, bin, z);
+    return hipGetLastError();
+}
+
+hipError_t launch_sqp_loop_u0(int batch, int nx, int n, const double* K, const double* s,
+                              const double* z, double* uo, const int* it, int steps, int t,
+                              double* Zlog, int* itlog, hipStream_t st) {
+    hipLaunchKernelGGL(sqp_loop_u0_kernel, dim3((batch + 255) / 256), dim3(256), 0, st, batch, nx,
+                       n, K, s, z, uo, it, steps, t, Zlog, itlog);
+    return hipGetLastError();
+}
+
 hipError_t launch_lbmpc_window_init(int batch, int steps, int q, int mask, const double* xinit,
                                     double* win, double* XL, hipStream_t st) {
     hipLaunchKernelGGL(lbmpc_window_init_kernel, dim3(batch), dim3(256), 0, st, batch, steps, q,

@@ -42,6 +42,10 @@ static const mxArray* field(const mxArray* P, const char* name, int required) {
     const mxArray* f = mxGetField(P, 0, name);
     if (f && mxIsEmpty(f)) f = NULL;
     if (!f && required) mexErrMsgIdAndTxt("bqp:args", "P.%s is required", name);
+    /* mxGetDoubles returns NULL for single / integer / complex arrays: reject them rather than
+       read an optional field as absent */
+    if (f && (!mxIsDouble(f) || mxIsComplex(f)))
+        mexErrMsgIdAndTxt("bqp:args", "P.%s must be a real double array", name);
     return f;
 }
 
@@ -84,6 +88,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         mexErrMsgIdAndTxt("bqp:args", "[X,U,theta,fval,exitflag,output,lambda] = ocp_gpu(P, x0, options)");
     const mxArray* P = prhs[0];
     const mxArray* X0 = prhs[1];
+    if (!mxIsDouble(X0) || mxIsComplex(X0)) mexErrMsgIdAndTxt("bqp:args", "x0 must be a real double array");
     const mxArray* A = field(P, "A", 1);
     bqp_ocp_dims d;
     d.nx = (int)mxGetM(A);

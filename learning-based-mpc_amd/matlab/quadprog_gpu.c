@@ -50,6 +50,11 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const mxArray* beq = nrhs > 5 ? prhs[5] : NULL;
     const mxArray* lb = nrhs > 6 ? prhs[6] : NULL;
     const mxArray* ub = nrhs > 7 ? prhs[7] : NULL;
+    /* every numeric argument must be real double: mxGetDoubles returns NULL for other classes,
+       which would otherwise read as an absent argument */
+    for (int i = 0; i < nrhs && i < 9; ++i)
+        if (prhs[i] && !mxIsEmpty(prhs[i]) && (!mxIsDouble(prhs[i]) || mxIsComplex(prhs[i])))
+            mexErrMsgIdAndTxt("bqp:args", "argument %d must be a real double array", i + 1);
     const int n = (int)mxGetM(f);
     const int batch = (int)mxGetN(f);
     const int m = (A && !mxIsEmpty(A)) ? (int)mxGetM(A) : 0;

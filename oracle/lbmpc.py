@@ -276,3 +276,73 @@ def window_replay(X, U, A, B, x_eq, u_eq, q, mask=True, h=0.5, lam=1e-3):
         else:                                               # get_data.m:7-9
             data = np.hstack([data[:, 1:], col[:, None]])
     return np.array(XL), data
+
+
+# ----------------------------------------------------------------------------------------
+# learned-model NLP closed loop (DMS_LBMPC_casadi.m:163-218)
+# ----------------------------------------------------------------------------------------
+def nw_window(xi, data):
+    """casadiL2NW.m:14-28 on an 8 x q window [X; Y; v] with dg/dxi:
+    g = sum_i Y_i k_i / (lambda + sum_j v_j k_j) (numerator not masked: the points that are not
+    yet valid hold Y = 0).  A 7-row window counts every point (v = 1), as nw()."""
+    X, Y = data[:3], data[3:7]
+    v = data[7] if data.shape[0] == 8 else np.ones(data.shape[1])
+    d = X - xi[:, None]
+    k = np.exp(-(d * d).sum(0) / H_BW ** 2)
+    den = LAM_NW + k @ v
+    sy = Y @ k
+    dk = (k[None, :] * d) * (2.0 / H_BW ** 2)
+    return sy / den, (Y @ dk.T) / den - np.outer(sy, dk @ v) / den ** 2
+
+
+def dms_problem(mg, N, data, F_T, h_T, F_x_d, h_x_d, delta=0.01):
+    """DMS_LBMPC_casadi.m:121-129 after eliminating both state chains: decision z = [u - u_eq;
+    theta]; running cost (delta-weighted, k = 0..N-1, :229-233) and terminal cost (:234) on the
+    learned rollout, constraints on the nominal rollout (:262-276) - the F4 problem with the
+    terminal term on the learned x_N.  data: the 8 x q window (or 7 x q)."""
+    p = f4_problem(mg, N, data, F_T, h_T, F_x_d, h_x_d, delta)
+    p['term_learned'] = True
+    return p
+
+
+def dms_lbmpc_loop(mg, sets, N, q, steps, mask=True, term_learned=True, warm=True,
+                   x_init=(0.15, 1.2875, 1.1547, 0.0), max_iter=200):
+    """Closed loop of DMS_LBMPC_casadi.m:157-218: per iteration the NLP at the measured state
+    (GN-SQP to a KKT point), u_0 to the RK4 plant (`dynamic`, :297-304), the sample
+    [dx1; dx2; du; Y; 1] into the window by get_data.m, and the shifted warm start (:209-213,
+    tail move 0).  mask: the 8 x q window with only the first (zero) point valid at the start
+    (:158-161); mask=False counts every point (7-row window).  Returns X (steps+1, 4) absolute,
+    U (steps,) absolute, Z (steps, N+1) and the SQP iteration counts."""
+    from .mg_model import mg_rk4
+    global nw
+    x_eq = np.asarray(mg['x_wp'], float); u_eq = float(np.ravel(mg['u_wp'])[0])
+    A = np.asarray(mg['A'], float); B = np.asarray(mg['B'], float).reshape(4)
+    data = np.zeros((8, q))
+    data[7, :] = 0.0 if mask else 1.0
+    data[7, 0] = 1.0
+    x = np.array(x_init, float)
+    X, U, Z, IT = [x.copy()], [], [], []
+    z = None
+    saved = nw
+    nw = nw_window
+    try:
+        for it in range(1, steps + 1):
+            p = dms_problem(mg, N, data, sets['F_w_N'], sets['h_w_N'], sets['F_x_d'], sets['h_x_d'])
+            p['term_learned'] = term_learned
+            z, _, info = sqp(p, x - x_eq, z0=z if warm else None, max_iter=max_iter)
+            du = z[0]
+            xn = mg_rk4(0.01, x, du + u_eq)
+            dx = x - x_eq
+            nom = A @ dx + B * du
+            col = np.concatenate([[dx[0], dx[1], du], (xn - x_eq) - nom, [1.0]])
+            if it < q:                                      # get_data.m:3-6
+                data[:, it] = col
+            else:                                           # get_data.m:7-9
+                data = np.hstack([data[:, 1:], col[:, None]])
+            Z.append(z.copy()); IT.append(info['iterations']); U.append(du + u_eq)
+            z = np.concatenate([z[1:N], [0.0], z[N:]])
+            x = xn
+            X.append(x.copy())
+    finally:
+        nw = saved
+    return np.array(X), np.array(U), np.array(Z), np.array(IT)

@@ -22,6 +22,8 @@ size_t mxGetN(const mxArray* a);
 size_t mxGetNumberOfElements(const mxArray* a);
 int mxIsEmpty(const mxArray* a);
 int mxIsStruct(const mxArray* a);
+int mxIsDouble(const mxArray* a);
+int mxIsComplex(const mxArray* a);
 double* mxGetDoubles(const mxArray* a);
 double* mxGetPr(const mxArray* a);
 double mxGetScalar(const mxArray* a);

@@ -37,6 +37,8 @@ size_t mxGetN(const mxArray* a) { return a ? a->n : 0; }
 size_t mxGetNumberOfElements(const mxArray* a) { return a ? a->m * a->n : 0; }
 int mxIsEmpty(const mxArray* a) { return !a || a->m * a->n == 0; }
 int mxIsStruct(const mxArray* a) { return a && a->kind == 1; }
+int mxIsDouble(const mxArray* a) { return a && a->kind == 0; }
+int mxIsComplex(const mxArray* a) { (void)a; return 0; }
 double* mxGetDoubles(const mxArray* a) { return (a && a->kind == 0) ? a->pr : NULL; }
 double* mxGetPr(const mxArray* a) { return mxGetDoubles(a); }
 double mxGetScalar(const mxArray* a) { return (a && a->kind == 0 && a->m * a->n > 0) ? a->pr[0] : 0.0; }

@@ -44,6 +44,8 @@ class Mex:
         L.mexemu_field_name.restype = C.c_char_p
         L.mexemu_field_name.argtypes = [vp, C.c_int]
         L.mexemu_is_char.argtypes = [vp]
+        L.mxCreateString.restype = vp
+        L.mxCreateString.argtypes = [C.c_char_p]
         self.live = []
 
     # ---- inputs ----
@@ -64,11 +66,15 @@ class Mex:
         C.memmove(self.L.mxGetDoubles(p), flat.ctypes.data, flat.nbytes)
         return p
 
+    def string(self, text):
+        """a char array (a non-double class, for the gateways' class checks)"""
+        return self.L.mxCreateString(text.encode())
+
     def struct(self, d):
         names = (C.c_char_p * len(d))(*[k.encode() for k in d])
         s = self.L.mxCreateStructMatrix(1, 1, len(d), names)
         for k, v in d.items():
-            self.L.mxSetField(s, 0, k.encode(), self.mat(v))
+            self.L.mxSetField(s, 0, k.encode(), self.string(v) if isinstance(v, str) else self.mat(v))
         return s
 
     # ---- outputs ----

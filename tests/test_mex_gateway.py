@@ -69,6 +69,9 @@ def test_quadprog_argument_errors(qmex):
         qmex.call(1, qmex.mat(np.eye(2)), qmex.mat(np.ones((2, 3))), qmex.mat(None), qmex.mat(None),
                   qmex.mat(None), qmex.mat(None), qmex.mat(lb), qmex.mat(ub))
     assert e.value.ident == 'bqp:fixed'
+    with pytest.raises(MexError) as e:                       # f of a non-double class
+        qmex.call(1, qmex.mat(np.eye(2)), qmex.string('ab'))
+    assert e.value.ident == 'bqp:args'
 
 
 def test_ocp_argument_errors(omex, mg, term_set):
@@ -84,6 +87,14 @@ def test_ocp_argument_errors(omex, mg, term_set):
     assert e.value.ident == 'bqp:dims'
     with pytest.raises(MexError) as e:                       # missing required field
         omex.call(1, omex.struct(dict(N=20, nu=1, np=1, A=prob.A)), omex.mat(np.zeros((4, 1))))
+    assert e.value.ident == 'bqp:args'
+    with pytest.raises(MexError) as e:                       # optional field of a non-double class
+        omex.call(1, omex.struct(dict(N=20, nu=1, np=1, A=prob.A, B=prob.B,
+                                      W=np.moveaxis(prob.W, 0, -1), w='abc')),
+                  omex.mat(np.zeros((4, 1))))
+    assert e.value.ident == 'bqp:args' and 'P.w' in str(e.value)
+    with pytest.raises(MexError) as e:                       # x0 of a non-double class
+        omex.call(1, _pstruct(omex, prob), omex.string('abcd'))
     assert e.value.ident == 'bqp:args'
 
 

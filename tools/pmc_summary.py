@@ -1,12 +1,13 @@
 """Per-launch HBM bytes of the solve kernel from rocprofv3 PMC passes (tools/gpu_prof.sh).
 
-    python tools/pmc_summary.py gpurun_out/TAG profiles/rNN_TAG [--kernel ocp_ipm_kernel] [--no-latest]
+    python tools/pmc_summary.py gpurun_out/TAG profiles/rNN_TAG [--kernel ocp_ipm_kernel] [--config C2]
 
 Reads TAG/pmc_fetch/run_counter_collection.csv (FETCH_SIZE, KB) and TAG/pmc_write/... (WRITE_SIZE,
 KB), keeps the dispatches of the named kernel, and applies the gfx950 correction of
 /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half the bytes of a wide
-read (x2); WRITE_SIZE is taken as is.  Writes OUT/pmc.json and profiles/pmc_latest.json (read by
-bench.py as roofline.traffic of the default C2 line; --no-latest for other configs), and copies the kernel-trace stats + PMC csvs into OUT.
+read (x2); WRITE_SIZE is taken as is.  Writes OUT/pmc.json and, with --config NAME,
+profiles/pmc_NAME.json (read by bench.py as roofline.traffic of that config's line), and copies
+the kernel-trace stats + PMC csvs into OUT.
 """
 import csv
 import json
@@ -47,15 +48,24 @@ def main():
         'correction': 'FETCH_SIZE x 1024 x 2 (gfx950: half of wide reads counted), '
                       'WRITE_SIZE x 1024; separate --pmc passes',
     }
+    ks = os.path.join(src, 'trace', 'run_kernel_stats.csv')
+    if os.path.exists(ks):      # rocprofv3 --stats average of the same kernel (kernel-trace pass)
+        for r in csv.DictReader(open(ks)):
+            if kernel in r.get('Name', ''):
+                res['trace_avg_ms'] = float(r['AverageNs']) * 1e-6
+                res['trace_calls'] = int(r['Calls'])
+                break
     json.dump(res, open(os.path.join(dst, 'pmc.json'), 'w'), indent=1)
-    if '--no-latest' not in sys.argv:
-        json.dump(res, open(os.path.join(ROOT, 'profiles', 'pmc_latest.json'), 'w'), indent=1)
+    res['source'] = dst
+    if '--config' in sys.argv:
+        name = sys.argv[sys.argv.index('--config') + 1]
+        json.dump(res, open(os.path.join(ROOT, 'profiles', 'pmc_%s.json' % name), 'w'), indent=1)
     for sub, name in (('trace', 'run_kernel_stats.csv'), ('pmc_fetch', 'run_counter_collection.csv'),
                       ('pmc_write', 'run_counter_collection.csv')):
         p = os.path.join(src, sub, name)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, '%s_%s' % (sub, name)))
-    for log in ('bench.log', 'stamps.log', 'pytest_gpu.log'):
+    for log in ('bench.log', 'bench_trace.log', 'stamps.log', 'stamps.json', 'pytest_gpu.log'):
         p = os.path.join(src, log)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, log))

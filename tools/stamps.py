@@ -1,6 +1,14 @@
 """Diagnostic: per-phase cycle shares of the structured kernel (build: make -C learning-based-mpc_amd stamps).
-Runs the C2 workload through libbqp_stamps.so and prints the mean cycles per phase per instance."""
+Runs the C2 workload through libbqp_stamps.so and prints the mean cycles per phase per instance.
+
+    python tools/stamps.py [BATCH] [--json OUT.json]
+
+--json writes the summary bench.py reports as roofline.latency (stage-wave busy fraction and
+cycles per iteration), tagged with the sha1 of csrc/bqp_ocp.hip so that bench can tell whether
+the stamps were taken on the kernel source it runs."""
 import ctypes as C
+import hashlib
+import json
 import os
 import sys
 
@@ -15,7 +23,11 @@ lib = _lib.load()
 lib.bqp_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _lib._PD]
 import bench
 g = np.load(os.path.join(ROOT, 'tests', 'golden', 'lmpc_N20.npz'))
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+pos = [a for a in sys.argv[1:] if not a.startswith('--')]
+jout = sys.argv[sys.argv.index('--json') + 1] if '--json' in sys.argv else None
+if jout in pos:
+    pos.remove(jout)
+B = int(pos[0]) if pos else 1024
 lm = bench.workload('C2', B, 0, 1)['prob']
 X = g['dx'][np.arange(B) % 1000]
 h = bqp.Handle(0)
@@ -40,3 +52,19 @@ for role, names, base in (('stage wave', stage, 0), ('row wave', row, 16)):
         v = st[:, base + i].mean()
         if v > 0:
             print('  %-28s %10.0f cyc  %5.1f %%  per-iter %8.0f' % (n, v, 100 * v / tot, v / it))
+if jout:
+    src = os.path.join(ROOT, 'learning-based-mpc_amd', 'csrc', 'bqp_ocp.hip')
+    waits = [i for i, n in enumerate(stage) if n.startswith('wait')]
+    sw = st[:, 0:16].sum(axis=1).mean()
+    busy = sw - sum(st[:, i].mean() for i in waits)
+    res = {'batch': B, 'kernel_ms_stamp_build': ms, 'iterations_mean': float(it),
+           'stage_wave_cycles_per_instance': float(sw),
+           'stage_wave_busy_frac': float(busy / sw),
+           'stage_wave_cycles_per_iter': float(busy / it),
+           'phases_stage_per_iter': {n: float(st[:, i].mean() / it) for i, n in enumerate(stage)},
+           'phases_row_per_iter': {n: float(st[:, 16 + i].mean() / it) for i, n in enumerate(row)},
+           'source_sha1': hashlib.sha1(open(src, 'rb').read()).hexdigest(),
+           'note': 's_memtime stamps of the diagnostic build (make stamps); busy = all stage-wave '
+                   'phases except the barrier waits'}
+    json.dump(res, open(jout, 'w'), indent=1)
+    print('wrote', jout)

@@ -298,7 +298,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C2D', 'C3', 'C4', 'C5', 'CL'])
+    ap.add_argument('--config', default='C2', choices=['C1', 'C2', 'C2H', 'C2D', 'C3', 'C4', 'C5', 'CL', 'CLL'])
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (C4: total)')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--precision', default='fp64', choices=['fp64', 'fp32', 'mixed'],
@@ -308,7 +308,7 @@ def main():
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
     args = ap.parse_args()
-    if args.config in ('C1', 'CL', 'C2H', 'C2D'):
+    if args.config in ('C1', 'CL', 'CLL', 'C2H', 'C2D'):
         return bench_aux(args)
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         return launch_ranks(args)
@@ -502,7 +502,8 @@ def bench_aux(args):
         train_data(:, 1:100), Gauss-Newton SQP on the GPU (bqp_lbmpc_solve_batched); one step =
         one batched SQP solve (default batch 1 = the reference's single-instance config);
     CL  closed-loop DSS tracking LMPC (N=100, RK4 plant), one step = one batched closed-loop
-        step (solve + plant) over --batch initial states; timed over --steps steps of one loop.
+        step (solve + plant) over --batch initial states; timed over --steps steps of one loop;
+    CLL the learned-model NLP loop of DMS_LBMPC_casadi.m (bqp_closed_loop_sqp), same step unit.
     The CPU leg is the numpy restatement (oracle/lbmpc.py, interpreted) for C1 and the C
     restatement + numpy RK4 for CL, on a bounded sample."""
     import time as _t
@@ -652,6 +653,46 @@ def bench_aux(args):
                                       kind='port', sample='%d solves of oracle/lbmpc.py (numpy)' % ns),
                     check=dict(converged_frac=float((r.exitflag == 1).mean()),
                                mean_sqp_iterations=float(r.iterations.mean())))
+    elif args.config == 'CLL':
+        # the learned-model NLP closed loop of DMS_LBMPC_casadi.m (cost on the learned states,
+        # 8 x 100 window): per step the GN-SQP with the exact Hessian, the RK4 plant and the
+        # window update, all on the GPU (bqp_closed_loop_sqp), over --batch initial states
+        g = np.load(os.path.join(GOLD, 'lbmpc_instance.npz'))
+        dl = bqp.DMSLBMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                          d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], g['F_w_N'], g['h_w_N'],
+                          g['F_x_d'], g['h_x_d'], d['x_wp'], d['u_wp'], N=100)
+        B = args.batch or 256
+        rng = np.random.default_rng(11)
+        x_init = np.array([0.15, 1.2875, 1.1547, 0.0])
+        X0 = x_init + rng.uniform(-1, 1, (B, 4)) * np.array([0.005, 0.005, 0.0, 0.0])
+        X0[0] = x_init                                     # DMS_LBMPC_casadi.m:99
+        bqp.closed_loop_sqp(dl, X0, 1, learning=dict(q=100, mask=1), handle=h)
+        t0 = _t.perf_counter()
+        r = bqp.closed_loop_sqp(dl, X0, args.steps, learning=dict(q=100, mask=1), handle=h)
+        el = _t.perf_counter() - t0
+        kms = h.kernel_ms()[0]
+        st = np.load(os.path.join(GOLD, 'dms_lbmpc_loops.npz'))['DMS_tLBMPC_q100']
+        e0 = np.abs(r.X[0] - st[:args.steps + 1])
+        from oracle import lbmpc as olb               # CPU leg only
+        from oracle.mg_model import mg_problem
+        c0 = _t.perf_counter()
+        olb.dms_lbmpc_loop(mg_problem(), dict(g), 100, 100, 3, x_init=X0[1])
+        cpu = 3 / (_t.perf_counter() - c0)
+        line = dict(metric='learned-model NLP closed-loop steps/s (DMS_LBMPC_casadi.m, N=100, q=100)',
+                    value=round(B * args.steps / el, 1), unit='instance-steps/s', n_gpus=1,
+                    steps=args.steps, warmup=1, ms_per_step=round(1e3 * el / args.steps, 4),
+                    higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
+                    data='x_init of DMS_LBMPC_casadi.m and seeded perturbations (+-0.005 in x1, x2)',
+                    config={'workload': 'CLL: DMS LBMPC closed loop, batch %d, %d steps' % (B, args.steps),
+                            'batch_per_gpu': B, 'horizon': 100, 'parallelism': 'dp1'},
+                    roofline=None, kernel_ms=round(kms, 4),
+                    cpu_baseline=dict(value=round(cpu, 3), unit='instance-steps/s', cores=1, kind='port',
+                                      sample='3 steps of one instance, oracle/lbmpc.py dms_lbmpc_loop (numpy)'),
+                    check=dict(converged_frac=float((r.exitflag == 1).mean()),
+                               sqp_iterations_mean=float(r.iterations.mean()),
+                               sqp_iterations_max=int(r.iterations.max()),
+                               x_init_vs_stored_q100_slow_max=float(e0[:, :2].max()),
+                               x_init_vs_stored_q100_all_max=float(e0.max())))
     else:
         gl = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
         tl = bqp.TrackingLMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],

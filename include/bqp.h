@@ -212,6 +212,11 @@ typedef struct {
     int q;              /* points in the NW window (<= 512) */
     int m;              /* rows of Ain */
     int mask;           /* 0: 7 x q window, every point counts; 1: 8 x q window with validity row */
+    int hessian;        /* 0: Gauss-Newton; 1: + the second-order term of the learned dynamics
+                           (costate-weighted NW Hessians) whenever the sum is positive definite
+                           (Cholesky pivots > 1e-10 max|H_ii|), Gauss-Newton otherwise.  GN
+                           converges linearly (rate ~0.5) on DMS_LBMPC_casadi.m's learned-state
+                           costs: 60-200 SQP iterations against 4-6 with 1 */
 } bqp_lbmpc_dims;
 
 typedef struct {

@@ -53,7 +53,8 @@ class Strides(C.Structure):
 
 
 class LbmpcDims(C.Structure):
-    _fields_ = [(n, C.c_int) for n in ('nx', 'nu', 'np', 'N', 'n_run', 'term_learned', 'q', 'm', 'mask')]
+    _fields_ = [(n, C.c_int) for n in ('nx', 'nu', 'np', 'N', 'n_run', 'term_learned', 'q', 'm', 'mask',
+                                       'hessian')]
 
 
 class SqpLoop(C.Structure):

@@ -87,6 +87,9 @@ class _LearnedOCP:
         self.nz = N * m + p
         self.n_run, self.term_learned = n_run, term_learned
         self.bandwidth, self.lam = bandwidth, lam
+        # SQP model: 'exact' adds the second-order term of the learned dynamics whenever the
+        # Hessian stays positive definite (bqp_lbmpc_dims.hessian), 'gn' is Gauss-Newton alone
+        self.hessian = 'exact'
         # ---- condensed nominal constraints Ain z <= b0 + Bx x0 ---------------------------
         # nominal closed rollout x_{k+1} = A x_k + B (K x_k + v_k): x_k = Mx_k x0 + Sx_k z
         nz = self.nz
@@ -132,7 +135,7 @@ class _LearnedOCP:
                 (self.A.T, self.B.T, self.K.T, self.Lq, self.Lr, self.Lp, self.Lt,
                  self.LAMBDA.T, self.PSI.T, self.xs)]
         dims = _lib.LbmpcDims(self.n, self.m, self.p, self.N, self.n_run, int(self.term_learned), q,
-                              mrows, mask)
+                              mrows, mask, int(self.hessian == 'exact'))
         dd = _lib.LbmpcData(*[_lib.ptr(a) for a in keep], _lib.ptr(w), sd, _lib.ptr(x0), self.n,
                             _lib.ptr(self.Ain_cm), _lib.ptr(bin_), mrows, self.bandwidth, self.lam)
         o = _lib.options(max_iter=max_iter, tol_stat=tol)
@@ -219,6 +222,7 @@ class DMSLBMPC(HybridLBMPC):
 
     def solve(self, xmeasure, data, y0=None, handle=None, max_iter=200, tol=1e-8):
         """as HybridLBMPC.solve, data the 8 x q window [X; Y; v] (or 7 x q: every point valid);
-        the GN iteration converges linearly on these learned costs (about 60 SQP iterations on
-        the second step of the stored DMS_tLBMPC_q100 run), hence the larger default max_iter"""
+        with hessian = 'gn' the iteration converges linearly on these learned costs (about 60 SQP
+        iterations on the second step of the stored DMS_tLBMPC_q100 run, 5 with the exact
+        Hessian), hence the larger default max_iter"""
         return super().solve(xmeasure, data, y0=y0, handle=handle, max_iter=max_iter, tol=tol)

@@ -94,7 +94,8 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
              mpc.xs)]
     bin0 = np.ascontiguousarray(mpc.b0, dtype=np.float64)
     Bx = np.ascontiguousarray(mpc.Bx.T, dtype=np.float64)        # column-major m x n
-    dims = _lib.LbmpcDims(mpc.n, mpc.m, mpc.p, mpc.N, mpc.n_run, int(mpc.term_learned), q, mrows, 1)
+    dims = _lib.LbmpcDims(mpc.n, mpc.m, mpc.p, mpc.N, mpc.n_run, int(mpc.term_learned), q, mrows, 1,
+                          int(getattr(mpc, 'hessian', 'exact') == 'exact'))
     dd = _lib.LbmpcData(*[_lib.ptr(a) for a in keep], None, 0, None, 0, _lib.ptr(mpc.Ain_cm), None,
                         0, mpc.bandwidth, mpc.lam)
     X = np.zeros((b, steps + 1, mpc.n)); U = np.zeros((b, steps, mpc.m))

@@ -595,7 +595,7 @@ int bqp_nw_oracle(bqp_handle h, int batch, int q, const double* data, int64_t sd
 static int lbmpc_check(const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_data* D) {
     if (!d || !D || batch <= 0) return BQP_E_ARG;
     if (d->N <= 0 || d->n_run < 0 || d->n_run > d->N || d->q <= 0 || d->m < 0 ||
-        (d->mask != 0 && d->mask != 1))
+        (d->mask != 0 && d->mask != 1) || (d->hessian != 0 && d->hessian != 1))
         return BQP_E_ARG;
     if (!D->A || !D->B || !D->K || !D->Lq || !D->Lr || !D->Lp || !D->Lt || !D->LAMBDA ||
         !D->PSI || !D->xs || !D->data || !D->x0 || (d->m > 0 && (!D->Ain || !D->bin)))
@@ -620,9 +620,10 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     const int N = d->N, n = N * d->nu + d->np, m = d->m;
     const int nr = d->n_run * (d->nx + d->nu) + 2 * d->nx;
     const size_t B = batch;
+    const size_t n2 = d->hessian ? B * 3 * (size_t)N * n : 0;   // Jr2, Tr2 of the exact Hessian
     const size_t nd = B * nr * n + B * nr + B * n * n + B * n + 2 * B * m + B * n + B +
-                      B * LB_NTRIAL + 2 * B;
-    const size_t ni = 2 * B + 4;
+                      B * LB_NTRIAL + 2 * B + 2 * n2;
+    const size_t ni = 3 * B + 4;
     HIP_TRY(h->lwork.reserve(sizeof(double) * nd + sizeof(int) * ni));
     double* p = (double*)h->lwork.p;
     bqp::LbmpcArgs a;
@@ -638,10 +639,14 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     a.costT = p; p += B * LB_NTRIAL;
     a.stat = p; p += B;
     a.cprev = p; p += B;
+    a.Jr2 = p; p += n2;
+    a.Tr2 = p; p += n2;
     int* ip = (int*)p;
     a.qpflag = ip; ip += B;
+    a.hused = ip; ip += B;
     a.done = ip; ip += B;
     a.ndone = ip;
+    a.hess = d->hessian;
     a.lam = lam ? lam : lam_int;
     a.z = z; a.flag = exitflag; a.iters = iterations;
     a.N = N; a.n = n; a.nr = nr; a.m = m; a.q = d->q; a.n_run = d->n_run;
@@ -658,6 +663,7 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     a.data = D->data; a.sdata = D->sdata; a.x0 = D->x0; a.sx0 = D->sx0;
     a.Ain = D->Ain; a.bin = D->bin; a.sbin = D->sbin;
     HIP_TRY(hipMemsetAsync(a.done, 0, sizeof(int) * (B + 1), st));   // done[] and ndone
+    HIP_TRY(hipMemsetAsync(a.hused, 0, sizeof(int) * B, st));
     HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * B, st));
     HIP_TRY(hipMemsetAsync(a.flag, 0, sizeof(int) * B, st));
     // QP sub-problem (dense kernel): min 0.5 d'Hd + f'd  s.t.  Ain d <= bin - Ain z
@@ -681,10 +687,11 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     for (int it = 0; it < o.max_iter; ++it) {
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 1, st));
         HIP_TRY(bqp::launch_lbmpc_normal(a, st));
+        if (a.hess) HIP_TRY(bqp::launch_lbmpc_hess(a, st));
         HIP_TRY(bqp::launch_dense(q, st));
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
         HIP_TRY(bqp::launch_lbmpc_update(a, st));
-        launches += 5;
+        launches += a.hess ? 6 : 5;
         if ((it & 3) == 3 || it + 1 == o.max_iter) {
             int nd_h = 0;
             HIP_TRY(hipMemcpyAsync(&nd_h, a.ndone, sizeof(int), hipMemcpyDeviceToHost, st));

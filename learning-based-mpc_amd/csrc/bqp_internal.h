@@ -114,6 +114,11 @@ struct LbmpcArgs {
     double *H, *f, *bsh;                // batch x n x n (column-major), batch x n, batch x m
     double *cost0, *costT, *stat, *cprev;  // batch, batch x ntrial, batch, batch
     int *qpflag, *flag, *done, *iters, *ndone;
+    // exact Hessian (hess = 1): rows Xi_k (Jr2) and W_k Xi_k (Tr2), batch x 3N x n row-major;
+    // hused (may be null): per instance, the iterations that used the exact Hessian
+    int hess;
+    double *Jr2, *Tr2;
+    int* hused;
 };
 
 hipError_t launch_nw_oracle(int batch, int q, const double* data, int64_t sdata, const double* xi,
@@ -122,6 +127,7 @@ bool lbmpc_supported(int nx, int nu, int np, int n, int q);
 hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st);
 hipError_t launch_lbmpc_normal(const LbmpcArgs& a, hipStream_t st);
 hipError_t launch_lbmpc_update(const LbmpcArgs& a, hipStream_t st);
+hipError_t launch_lbmpc_hess(const LbmpcArgs& a, hipStream_t st);
 
 // closed-loop simulation (bqp_plant.hip): Moore-Greitzer RK4 plant between batched solves
 hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* xinit,

@@ -6,7 +6,7 @@
 // constraintsLBMPC.m:18-45 (F3), examples/hybrid_LBMPC_casadi.m:250-311 (F4).  The algorithm
 // is stated in oracle/lbmpc.py; the host loop is bqp_lbmpc_solve_batched_device (bqp_api.cpp).
 //
-// Kernels (one SQP iteration = rollout(GN) -> normal -> dense QP -> rollout(trials) -> update):
+// Kernels (one SQP iteration = rollout(GN) -> normal [-> hess] -> dense QP -> rollout(trials) -> update):
 //   nw_oracle_kernel      one wave per query point: g(xi), dg/dxi; lanes over the data window
 //   lbmpc_rollout_kernel  one wave per (instance, trial): the learned rollout u = K x + v,
 //                         x+ = A x + B u + g(x, u) (NW sums over the window held in LDS, lanes
@@ -16,6 +16,8 @@
 //                         of the residual Jacobian Jr (row-major, coalesced along z)
 //   lbmpc_normal_kernel   one workgroup per instance: H = 2 Jr'Jr, f = 2 Jr'er through LDS row
 //                         tiles, and the QP right-hand side b_in - A_in z
+//   lbmpc_hess_kernel     (exact Hessian) one workgroup per instance: H_GN + the second-order
+//                         term of the learned dynamics, kept if its LDS Cholesky succeeds
 //   lbmpc_update_kernel   one wave per instance: convergence test (step, NLP stationarity
 //                         |f + A_in' lam|), Armijo choice among the trial step lengths, z += a d
 #include <hip/hip_runtime.h>
@@ -36,11 +38,15 @@ namespace bqp {
 // wr = 8 rows [X; Y; v] (casadiL2NW.m:14-28: the normaliser is lambda + sum_j v_j k_j, the
 // numerator is not masked - points that are not yet valid hold Y = 0).  Returns g (4) and, if
 // JAC, dg (4 x 3, row-major); every lane ends with the uniform values.
-template <bool JAC>
+// With HESS also the second derivatives d2g (4 x 6: the unique entries 00 01 02 11 12 22 of each
+// symmetric 3 x 3 Hessian): with c = 2/h^2, d2k_j = k_j (c^2 d_j d_j' - c I), d_j = X_j - xi,
+//   d2g_i = (d2N_i - g_i d2D - dg_i dD' - dD dg_i') / D.
+template <bool JAC, bool HESS = false>
 __device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double hinv2, double lam,
                                         const double (&xi)[3], double (&g)[4], double (&dg)[4][3],
-                                        int lane) {
+                                        int lane, double (*d2g)[6] = nullptr) {
     double s = 0.0, sy[4] = {0, 0, 0, 0}, ds[3] = {0, 0, 0}, dsy[4][3] = {};
+    double s2[6] = {}, sy2[4][6] = {};
     for (int i = lane; i < q; i += LB_WAVE) {
         const double* p = D + wr * i;
         const double d0 = p[0] - xi[0], d1 = p[1] - xi[1], d2 = p[2] - xi[2];
@@ -57,6 +63,16 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double h
                 ds[c3] += dk[c3] * v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) dsy[r][c3] += p[3 + r] * dk[c3];
+            }
+        }
+        if (HESS) {
+            const double dd[6] = {d0 * d0, d0 * d1, d0 * d2, d1 * d1, d1 * d2, d2 * d2};
+#pragma unroll
+            for (int e = 0; e < 6; ++e) {
+                const double kd = k * dd[e];
+                s2[e] += kd * v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sy2[r][e] += p[3 + r] * kd;
             }
         }
     }
@@ -78,6 +94,27 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double h
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int c3 = 0; c3 < 3; ++c3) dg[r][c3] = (dsy[r][c3] - g[r] * ds[c3]) * iden;
+    }
+    if (HESS) {
+        const double c = 2.0 * hinv2;
+        constexpr int EA[6] = {0, 0, 0, 1, 1, 2}, EB[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+            s2[e] = wsum(s2[e]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sy2[r][e] = wsum(sy2[r][e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+            const int ea = EA[e], eb = EB[e];
+            const double id = ea == eb ? 1.0 : 0.0;
+            const double d2D = c * c * s2[e] - c * s * id;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double d2N = c * c * sy2[r][e] - c * sy[r] * id;
+                d2g[r][e] = (d2N - g[r] * d2D - dg[r][ea] * ds[eb] - ds[ea] * dg[r][eb]) * iden;
+            }
+        }
     }
 }
 
@@ -113,17 +150,28 @@ __global__ void __launch_bounds__(64) nw_oracle_kernel(int batch, int q, const d
 }
 
 // ------------------------------------------------------------------------------------------
-// rollout: cost (all modes), residual Jacobian (GN mode)
+// rollout: cost (all modes), residual Jacobian (GN mode) and, with a.hess, the second-order term
+// of the learned dynamics (oracle/lbmpc.py newton_model):
+//   sum_k Xi_k' W_k Xi_k,  W_k = sum_i p_{k+1,i} d2g_i(xi_k),  Xi_k = dxi_k/dz (3 x n),
+// with the costate p_k = dJ/dx_k of the learned rollout (backward recursion
+// p_k = dphi_k/dx_k + (A + B K + G_x + g_u K)' p_{k+1}, p_N = terminal gradient).  The forward
+// pass keeps dg, d2g and dphi/dx per stage in LDS (LB_SS doubles), the costate pass turns d2g
+// into W_k, and a second sensitivity pass writes the rows Xi_k (Jr2) and W_k Xi_k (Tr2) that
+// lbmpc_hess_kernel contracts.  LDS is dynamic: the window (wrows x q), then the stage store.
 // ------------------------------------------------------------------------------------------
-template <int NX, int NU, int NP>
+#define LB_SS 40         // per stage: dg 4x3 | d2g 4x6 (W_k in the first 6 after the costate pass) | dphi/dx 4
+template <int NX, int NU, int NP, bool HESS>
 __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) {
-    static_assert(NX >= 2 && NU == 1, "NW input xi = [x_1; x_2; u] needs nx >= 2, nu = 1");
-    __shared__ double D[8 * LB_MAXQ];
+    static_assert(NX == 4 && NU == 1, "NW input xi = [x_1; x_2; u] with the 4-state model, nu = 1");
+    extern __shared__ double lbd[];
+    double* D = lbd;
     const int lane = threadIdx.x;
     const int nt = gn ? 1 : a.ntrial;
     const int b = blockIdx.x / nt, t = blockIdx.x % nt;
     if (b >= a.batch || a.done[b]) return;
     const int N = a.N, n = a.n, nr = a.nr;
+    constexpr bool hess = HESS;      // instantiated for the GN launch of an exact-Hessian solve
+    double* SS = lbd + ((a.wrows * a.q + 1) & ~1);
     load_window(D, a.data + (int64_t)b * a.sdata, a.wrows * a.q, lane);
     const double alpha = gn ? 0.0 : ldexp(1.0, -t);
     const double* z = a.z + (int64_t)b * n;
@@ -154,9 +202,12 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     double* er = gn ? a.er + (int64_t)b * nr : nullptr;
     double J = 0.0;
     int row = 0;
+    double gx[NX];                  // dphi/dx of the current residual block (hess mode)
     // weighted residual block L (e) with L upper-triangular (row-major), e = v - M theta;
-    // GN: its Jacobian rows for the lane's columns from sensitivities S (d v / d z)
-    auto residual = [&](const double* Lw, int dim, const double* v, auto&& Mth, auto&& Scol) __attribute__((always_inline)) {
+    // GN: its Jacobian rows for the lane's columns from sensitivities S (d v / d z); hess: the
+    // gradient 2 L'e w.r.t. v accumulated in gv
+    auto residual = [&](const double* Lw, int dim, const double* v, auto&& Mth, auto&& Scol,
+                        double* gv) __attribute__((always_inline)) {
         for (int r = 0; r < dim; ++r) {
             double e = 0.0;
             for (int c2 = r; c2 < dim; ++c2) {
@@ -166,6 +217,8 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
                 e += Lw[r * dim + c2] * ec;
             }
             J += e * e;
+            if (gv)
+                for (int c2 = r; c2 < dim; ++c2) gv[c2] += 2.0 * e * Lw[r * dim + c2];
             if (gn) {
                 if (lane == 0) er[row + r] = e;
 #pragma unroll
@@ -202,15 +255,32 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
                 UL[c] = ul; UN[c] = unn;
             }
         }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) gx[i] = 0.0;
         if (k < a.n_run) {
-            residual(a.Lq, NX, x, LAM, [&](int c, int i) { return SL[c][i]; });
-            residual(a.Lr, NU, &u, PSI, [&](int c, int i) { return UL[c]; });
+            residual(a.Lq, NX, x, LAM, [&](int c, int i) { return SL[c][i]; }, hess ? gx : nullptr);
+            double gu = 0.0;
+            residual(a.Lr, NU, &u, PSI, [&](int c, int i) { return UL[c]; }, hess ? &gu : nullptr);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) gx[i] += Km(0, i) * gu;    // u = K x + v
         }
         // learned step
         const double xi[3] = {x[0], x[1], u};
-        double g[4], dg[4][3];
-        if (gn) nw_eval<true>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        double g[4], dg[4][3], d2g[4][6];
+        if constexpr (HESS) nw_eval<true, true>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane, d2g);
+        else if (gn) nw_eval<true>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
         else nw_eval<false>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        if (hess && lane == 0) {
+            double* st = SS + (int64_t)k * LB_SS;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                for (int c3 = 0; c3 < 3; ++c3) st[3 * r + c3] = dg[r][c3];
+#pragma unroll
+                for (int e = 0; e < 6; ++e) st[12 + 6 * r + e] = d2g[r][e];
+                st[36 + r] = gx[r];
+            }
+        }
         double x1[NX], xn1[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
@@ -241,22 +311,198 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         for (int i = 0; i < NX; ++i) { x[i] = x1[i]; xn[i] = xn1[i]; }
     }
     // terminal P on x_N (learned or nominal), T on (LAMBDA theta - xs)
+#pragma unroll
+    for (int i = 0; i < NX; ++i) gx[i] = 0.0;
     if (a.term_learned)
-        residual(a.Lp, NX, x, LAM, [&](int c, int i) { return SL[c][i]; });
+        residual(a.Lp, NX, x, LAM, [&](int c, int i) { return SL[c][i]; }, hess ? gx : nullptr);
     else
-        residual(a.Lp, NX, xn, LAM, [&](int c, int i) { return SN[c][i]; });
+        residual(a.Lp, NX, xn, LAM, [&](int c, int i) { return SN[c][i]; }, nullptr);
     {
         // rows Lt (LAMBDA theta - xs): written as L (v - M theta) with v = -xs, M = -LAMBDA
         double mxs[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) mxs[i] = -a.xs[i];
         auto mLAM = [&](int i, int p) { return -LAM(i, p); };
-        residual(a.Lt, NX, mxs, mLAM, [&](int c, int i) { return 0.0; });
+        residual(a.Lt, NX, mxs, mLAM, [&](int c, int i) { return 0.0; }, nullptr);
     }
     if (lane == 0) {
         if (gn) a.cost0[b] = J;
         else a.costT[(int64_t)b * nt + t] = J;
     }
+    if constexpr (!HESS) return;
+    wave_sync();
+    // ---- costate pass (uniform on every lane): W_k into the stage store ----
+    double pc[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) pc[i] = gx[i];      // p_N: terminal gradient (0 for a nominal x_N)
+    for (int k = N - 1; k >= 0; --k) {
+        double* st = SS + (int64_t)k * LB_SS;
+        double W6[6];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+            double w = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w += pc[r] * st[12 + 6 * r + e];
+            W6[e] = w;
+        }
+        // p_k = dphi_k/dx_k + Jx' p_{k+1}, Jx = A + B K + [G_x0 G_x1 0 0] + g_u K
+        double pn[NX];
+#pragma unroll
+        for (int c2 = 0; c2 < NX; ++c2) {
+            double v = st[36 + c2];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double jx = Am(i, c2) + (Bm(i, 0) + st[3 * i + 2]) * Km(0, c2);
+                if (c2 < 2) jx += st[3 * i + c2];
+                v += jx * pc[i];
+            }
+            pn[c2] = v;
+        }
+        wave_sync();
+        if (lane == 0) {
+#pragma unroll
+            for (int e = 0; e < 6; ++e) st[12 + e] = W6[e];
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pc[i] = pn[i];
+    }
+    wave_sync();
+    // ---- second sensitivity pass: rows Xi_k and W_k Xi_k ----
+    double* J2 = a.Jr2 + (int64_t)b * 3 * N * n;
+    double* T2 = a.Tr2 + (int64_t)b * 3 * N * n;
+#pragma unroll
+    for (int c = 0; c < LB_CPL; ++c)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) SL[c][i] = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const double* st = SS + (int64_t)k * LB_SS;
+        const double w00 = st[12], w01 = st[13], w02 = st[14], w11 = st[15], w12 = st[16], w22 = st[17];
+#pragma unroll
+        for (int c = 0; c < LB_CPL; ++c) {
+            const int j = lane + LB_WAVE * c;
+            double ul = (j == k) ? 1.0 : 0.0;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) ul += Km(0, i) * SL[c][i];
+            const double x0c = SL[c][0], x1c = SL[c][1];
+            if (j < n) {
+                const int64_t r0 = (int64_t)(3 * k) * n + j;
+                J2[r0] = x0c; J2[r0 + n] = x1c; J2[r0 + 2 * n] = ul;
+                T2[r0] = w00 * x0c + w01 * x1c + w02 * ul;
+                T2[r0 + n] = w01 * x0c + w11 * x1c + w12 * ul;
+                T2[r0 + 2 * n] = w02 * x0c + w12 * x1c + w22 * ul;
+            }
+            double sl[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double v = (Bm(i, 0) + st[3 * i + 2]) * ul + st[3 * i] * x0c + st[3 * i + 1] * x1c;
+#pragma unroll
+                for (int c2 = 0; c2 < NX; ++c2) v += Am(i, c2) * SL[c][c2];
+                sl[i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) SL[c][i] = sl[i];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// exact Hessian (a.hess): Hx = H_GN + sym(Jr2' Tr2) through LDS row tiles (8 x 8 accumulators
+// per thread, as the normal kernel), then a right-looking Cholesky of Hx in LDS; if every pivot
+// is above 1e-10 max|Hx_ii| (oracle/lbmpc.py pd_cholesky) Hx replaces the Gauss-Newton H,
+// otherwise the iteration keeps H_GN.  Dynamic LDS: 2 tiles of 16 x n, then n x n.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
+    extern __shared__ double lh[];
+    const int b = blockIdx.x;
+    if (b >= a.batch || a.done[b]) return;
+    const int n = a.n, nr2 = 3 * a.N, tid = threadIdx.x;
+    const int tx = tid & 15, ty = tid >> 4;
+    double* TA = lh;
+    double* TB = lh + 16 * n;
+    double* Kx = lh + 32 * n;
+    __shared__ double red[4];
+    if (n > 128) return;
+    const double* J2 = a.Jr2 + (int64_t)b * nr2 * n;
+    const double* T2 = a.Tr2 + (int64_t)b * nr2 * n;
+    double acc[8][8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] = 0.0;
+    for (int r0 = 0; r0 < nr2; r0 += 16) {
+        const int rc = min(16, nr2 - r0);
+        __syncthreads();
+        for (int i = tid; i < rc * n; i += 256) { TA[i] = J2[(int64_t)r0 * n + i]; TB[i] = T2[(int64_t)r0 * n + i]; }
+        __syncthreads();
+        for (int r = 0; r < rc; ++r) {
+            const double* Ar = TA + r * n;
+            const double* Br = TB + r * n;
+            double cj[8];
+#pragma unroll
+            for (int q2 = 0; q2 < 8; ++q2) cj[q2] = (tx + 16 * q2 < n) ? Br[tx + 16 * q2] : 0.0;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int i = ty + 16 * p;
+                const double ci = (i < n) ? Ar[i] : 0.0;
+#pragma unroll
+                for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] += ci * cj[q2];
+            }
+        }
+    }
+    __syncthreads();
+    // Kx(i, j) = Jr2(:, i)' Tr2(:, j) (column-major in LDS), then H_GN + its symmetric part: each
+    // pair (i > j) and each diagonal entry belongs to one thread
+#pragma unroll
+    for (int p = 0; p < 8; ++p)
+#pragma unroll
+        for (int q2 = 0; q2 < 8; ++q2) {
+            const int i = ty + 16 * p, j = tx + 16 * q2;
+            if (i < n && j < n) Kx[j * n + i] = acc[p][q2];
+        }
+    __syncthreads();
+    const double* H = a.H + (int64_t)b * n * n;
+    double dmx = 0.0;
+    for (int e = tid; e < n * n; e += 256) {
+        const int i = e % n, j = e / n;
+        if (i > j) {
+            const double v = H[e] + 0.5 * (Kx[j * n + i] + Kx[i * n + j]);
+            Kx[j * n + i] = v;
+            Kx[i * n + j] = v;
+        } else if (i == j) {
+            const double v = H[e] + Kx[e];
+            Kx[e] = v;
+            dmx = fmax(dmx, fabs(v));
+        }
+    }
+    dmx = wmax(dmx);
+    if ((tid & 63) == 0) red[tid >> 6] = dmx;
+    __syncthreads();
+    const double tol = 1e-10 * fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    // the Cholesky below overwrites the lower triangle and the diagonal: keep the diagonal (the
+    // strict upper triangle stays the exact matrix)
+    double* dsave = TA;
+    for (int j = tid; j < n; j += 256) dsave[j] = Kx[j * n + j];
+    __syncthreads();
+    bool pd = true;
+    for (int j = 0; j < n; ++j) {
+        const double d = Kx[j * n + j];
+        if (!(d > tol)) { pd = false; break; }      // uniform: every thread reads the same pivot
+        const double sq = sqrt(d);
+        for (int i = j + 1 + tid; i < n; i += 256) Kx[j * n + i] /= sq;
+        __syncthreads();
+        for (int c = j + 1; c < n; ++c) {
+            const double lc = Kx[j * n + c];
+            for (int i = c + tid; i < n; i += 256) Kx[c * n + i] -= Kx[j * n + i] * lc;
+        }
+        __syncthreads();
+    }
+    if (!pd) return;
+    double* Hw = a.H + (int64_t)b * n * n;
+    for (int e = tid; e < n * n; e += 256) {
+        const int i = e % n, j = e / n;
+        Hw[e] = (i == j) ? dsave[i] : (i < j ? Kx[e] : Kx[i * n + j]);
+    }
+    if (tid == 0 && a.hused) a.hused[b] += 1;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -415,9 +661,34 @@ bool lbmpc_supported(int nx, int nu, int np, int n, int q) {
            q <= LB_MAXQ;
 }
 
+size_t lbmpc_rollout_lds(const LbmpcArgs& a, int gn) {
+    size_t d = (size_t)((a.wrows * a.q + 1) & ~1);
+    if (gn && a.hess) d += (size_t)LB_SS * a.N;
+    return d * sizeof(double);
+}
+
 hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st) {
     const int grid = a.batch * (gn ? 1 : a.ntrial);
-    hipLaunchKernelGGL((lbmpc_rollout_kernel<4, 1, 1>), dim3(grid), dim3(64), 0, st, a, gn);
+    const size_t lds = lbmpc_rollout_lds(a, gn);
+    auto k = (gn && a.hess) ? lbmpc_rollout_kernel<4, 1, 1, true> : lbmpc_rollout_kernel<4, 1, 1, false>;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(64), lds, st, a, gn);
+    return hipGetLastError();
+}
+
+hipError_t launch_lbmpc_hess(const LbmpcArgs& a, hipStream_t st) {
+    const size_t lds = sizeof(double) * ((size_t)32 * a.n + (size_t)a.n * a.n);
+    if (a.n > 128 || lds > 160 * 1024 - 64) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)lbmpc_hess_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(lbmpc_hess_kernel, dim3(a.batch), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 

@@ -135,6 +135,89 @@ def gn_model(p, x0, z):
     return H, f
 
 
+def nw_hess(xi, data):
+    """g (4,), dg (4, 3) and the second derivatives d2g (4, 3, 3) of the NW sums at xi over a 7-row
+    window (every point counts) or an 8-row window [X; Y; v] (casadiL2NW.m normaliser).
+    With c = 2/h^2: dk_j = c k_j d_j, d2k_j = k_j (c^2 d_j d_j' - c I), d_j = X_j - xi;
+    g = N / D, dg = (dN - g dD') / D, d2g_i = (d2N_i - g_i d2D - dg_i dD' - dD dg_i') / D."""
+    X, Y = data[:3], data[3:7]
+    v = data[7] if data.shape[0] == 8 else np.ones(data.shape[1])
+    d = X - xi[:, None]                                  # (3, q)
+    k = np.exp(-(d * d).sum(0) / H_BW ** 2)
+    c = 2.0 / H_BW ** 2
+    D = LAM_NW + k @ v
+    Nn = Y @ k
+    g = Nn / D
+    dk = c * k[None, :] * d                              # (3, q)
+    dN = Y @ dk.T                                        # (4, 3)
+    dD = dk @ v                                          # (3,)
+    dg = (dN - np.outer(g, dD)) / D
+    ddk = (c * c) * np.einsum('j,aj,bj->jab', k, d, d) - c * k[:, None, None] * np.eye(3)[None]
+    d2N = np.einsum('ij,jab->iab', Y, ddk)               # (4, 3, 3)
+    d2D = np.einsum('j,jab->ab', v, ddk)
+    d2g = (d2N - g[:, None, None] * d2D[None] - np.einsum('ia,b->iab', dg, dD)
+           - np.einsum('a,ib->iab', dD, dg)) / D
+    return g, dg, d2g
+
+
+def pd_cholesky(H, rel=1e-10):
+    """right-looking Cholesky of H with every pivot required above rel max_i |H_ii|"""
+    K = np.array(H, float)
+    n = K.shape[0]
+    tol = rel * np.abs(np.diag(K)).max()
+    for j in range(n):
+        d = K[j, j]
+        if not d > tol:
+            return False
+        K[j + 1:, j] /= np.sqrt(d)
+        K[j + 1:, j + 1:] -= np.outer(K[j + 1:, j], K[j + 1:, j])
+    return True
+
+
+def psd_part(W):
+    """the positive semidefinite part of a symmetric 3 x 3 matrix (eigenvalues clipped at 0)"""
+    w, V = np.linalg.eigh(0.5 * (W + W.T))
+    return (V * np.maximum(w, 0.0)) @ V.T
+
+
+def newton_model(p, x0, z, clip=True):
+    """H, f of the SQP model with the second-order term of the learned dynamics:
+    H = H_GN + sum_k Xi_k' [sum_i p_{k+1,i} d2g_i(xi_k)]_+ Xi_k, with the costate
+    p_k = dJ/dx_k (backward recursion through the learned rollout) and Xi_k = dxi_k/dz; the
+    per-stage 3 x 3 curvature is clipped to its PSD part so that the QP stays convex."""
+    N, nu, npar, nx = p['N'], p['nu'], p['np'], p['nx']
+    n = N * nu + npar
+    H, f = gn_model(p, x0, z)
+    xL, uL, S, U = rollout(p, x0, z, learned=True, jac=True)
+    th = _theta(p, z)
+    LAM, PSI, Q, R, K, A, B = p['LAMBDA'], p['PSI'], p['Q'], p['R'], p['K'], p['A'], p['B']
+    Gx, d2 = [], []
+    for k in range(N):
+        xi = np.concatenate([xL[k][:2], uL[k]])
+        _, dg, d2g = nw_hess(xi, p['data'])
+        Gx.append(dg); d2.append(d2g)
+    pk = np.zeros(nx)
+    if p['term_learned']:
+        pk = 2.0 * p['P'] @ (xL[N] - LAM @ th)
+    w = p['w_run']
+    for k in range(N - 1, -1, -1):
+        # W_k from p_{k+1}
+        Wk = np.einsum('i,iab->ab', pk, d2[k])
+        Xi = np.vstack([S[k][:2], U[k]])                  # (3, n)
+        H += Xi.T @ (psd_part(Wk) if clip else 0.5 * (Wk + Wk.T)) @ Xi
+        # p_k = dphi_k/dx_k + (dx_{k+1}/dx_k)' p_{k+1}
+        dg = Gx[k]
+        Jx = A + B @ K
+        Jx = Jx + np.hstack([dg[:, :2], np.zeros((nx, nx - 2))]) + np.outer(dg[:, 2], K[0]) if nu == 1 else Jx
+        pn = Jx.T @ pk
+        if k < p['n_run']:
+            ex = xL[k] - LAM @ th
+            eu = uL[k] - PSI @ th
+            pn = pn + 2 * w * (Q @ ex + K.T @ (R @ eu))
+        pk = pn
+    return H, f
+
+
 def constraints(p, x0):
     """A_in z <= b_in from the nominal rollout (exact: affine in z)."""
     N, nu, npar = p['N'], p['nu'], p['np']
@@ -155,8 +238,13 @@ def constraints(p, x0):
     return np.vstack(rows), np.concatenate(rhs)
 
 
-def sqp(p, x0, z0=None, max_iter=100, tol_step=1e-10, tol_stat=1e-9, trace=None):
-    """Gauss-Newton SQP with parallel-trial Armijo line search (see module doc).
+def sqp(p, x0, z0=None, max_iter=100, tol_step=1e-10, tol_stat=1e-9, trace=None, hessian='gn'):
+    """SQP with parallel-trial Armijo line search (see module doc).  hessian: 'gn' Gauss-Newton;
+    'exact' adds the second-order term of the learned dynamics (newton_model) whenever the result
+    is positive definite (pd_cholesky), else Gauss-Newton for that iteration - the product's
+    default (GN alone converges linearly, rate ~0.5, on the learned-state costs of
+    DMS_LBMPC_casadi.m: 60-200 iterations against 4-6); 'newton' clips each stage's curvature to
+    its PSD part (no faster than GN there: the curvature that matters is negative).
     Returns z, lam_in, info."""
     N, nu, npar = p['N'], p['nu'], p['np']
     n = N * nu + npar
@@ -170,11 +258,25 @@ def sqp(p, x0, z0=None, max_iter=100, tol_step=1e-10, tol_stat=1e-9, trace=None)
     it = 0
     stat = np.inf
     for it in range(1, max_iter + 1):
-        H, f = gn_model(p, x0, z)
+        if hessian == 'gn':
+            H, f = gn_model(p, x0, z)
+        else:
+            H, f = newton_model(p, x0, z, clip=hessian == 'newton')
+            if hessian == 'exact' and not pd_cholesky(H):
+                # the exact Hessian of the learned cost when it is positive definite (Cholesky
+                # pivots above 1e-10 max|H_ii|, the test of bqp_lbmpc.hip lbmpc_hess_kernel),
+                # the Gauss-Newton matrix otherwise
+                H, f = gn_model(p, x0, z)
         qp = dict(H=H, f=f, A=Ain, b=bin_ - Ain @ z, Aeq=np.zeros((0, n)), beq=np.zeros(0),
                   lb=np.full(n, -np.inf), ub=np.full(n, np.inf))
         d, _, lamq, info = dense_qp.solve(qp)
         lam = lamq['ineqlin']
+        if not (np.all(np.isfinite(d)) and np.all(np.isfinite(lam))):
+            # the dense IPM broke down (it does on some well-conditioned learned-cost
+            # sub-problems, eig(H) in [0.5, 1.2e3]): the exact LDP/NNLS solve of the same QP
+            from . import exact_qp
+            r = exact_qp.solve(H, f, Ain, bin_ - Ain @ z)
+            d, lam = r['z'], r['lam']
         stat = np.abs(f + Ain.T @ lam).max()
         feas_start = np.all(Ain @ z <= bin_ + 1e-9)
         if trace is not None:
@@ -306,7 +408,7 @@ def dms_problem(mg, N, data, F_T, h_T, F_x_d, h_x_d, delta=0.01):
 
 
 def dms_lbmpc_loop(mg, sets, N, q, steps, mask=True, term_learned=True, warm=True,
-                   x_init=(0.15, 1.2875, 1.1547, 0.0), max_iter=200):
+                   x_init=(0.15, 1.2875, 1.1547, 0.0), max_iter=200, hessian='exact'):
     """Closed loop of DMS_LBMPC_casadi.m:157-218: per iteration the NLP at the measured state
     (GN-SQP to a KKT point), u_0 to the RK4 plant (`dynamic`, :297-304), the sample
     [dx1; dx2; du; Y; 1] into the window by get_data.m, and the shifted warm start (:209-213,
@@ -329,7 +431,7 @@ def dms_lbmpc_loop(mg, sets, N, q, steps, mask=True, term_learned=True, warm=Tru
         for it in range(1, steps + 1):
             p = dms_problem(mg, N, data, sets['F_w_N'], sets['h_w_N'], sets['F_x_d'], sets['h_x_d'])
             p['term_learned'] = term_learned
-            z, _, info = sqp(p, x - x_eq, z0=z if warm else None, max_iter=max_iter)
+            z, _, info = sqp(p, x - x_eq, z0=z if warm else None, max_iter=max_iter, hessian=hessian)
             du = z[0]
             xn = mg_rk4(0.01, x, du + u_eq)
             dx = x - x_eq

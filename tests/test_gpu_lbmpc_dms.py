@@ -1,7 +1,14 @@
 """GPU learned-model NLP closed loop (bqp.closed_loop_sqp -> bqp_closed_loop_sqp: the GN-SQP
 kernels with the masked NW window, the RK4 plant kernel and get_data.m's window update per step)
 against the reference's stored runs of examples/DMS_LBMPC_casadi.m (tests/golden/
-dms_lbmpc_loops.npz) and against the oracle's restatement (oracle/lbmpc.py dms_lbmpc_loop)."""
+dms_lbmpc_loops.npz) and against the oracle's restatement of the loop (oracle/lbmpc.py
+dms_lbmpc_loop, fixture tests/golden/dms_lbmpc_oracle.npz from oracle/make_dms_oracle_fixture.py).
+
+Tolerances: the stored runs are IPOPT solutions (its default tol 1e-8 on the scaled NLP); the
+throttle-rate state x4 = 1000 delta u amplifies a first-move difference tenfold.  The GN-SQP stops
+at |d| <= tol (1 + |z|) with the KKT test, or once its step is below 1e-6 with the cost stagnant
+(bqp_lbmpc.hip lbmpc_update_kernel), so first moves agree with the oracle's tighter stop
+(|d| <= 1e-10) to ~1e-6."""
 import numpy as np
 import pytest
 
@@ -10,12 +17,13 @@ from conftest import golden
 pytestmark = pytest.mark.gpu
 
 
-def _dms(mg, N=100):
+def _mpc(mg, cls='DMSLBMPC', N=100):
     import bqp
     g = golden('lbmpc_instance.npz')
-    return bqp.DMSLBMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'], mg['LAMBDA'],
-                        mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'], g['F_w_N'],
-                        g['h_w_N'], g['F_x_d'], g['h_x_d'], mg['x_wp'], mg['u_wp'], N=N)
+    return getattr(bqp, cls)(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                             mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                             g['F_w_N'], g['h_w_N'], g['F_x_d'], g['h_x_d'], mg['x_wp'],
+                             mg['u_wp'], N=N)
 
 
 X_INIT = np.array([0.15, 1.2875, 1.1547, 0.0])
@@ -23,40 +31,58 @@ X_INIT = np.array([0.15, 1.2875, 1.1547, 0.0])
 
 def test_dms_lbmpc_loop_vs_stored_q100(mg):
     """DMS_LBMPC_casadi.m as written (q = 100, 8 x q window): the GPU loop regenerates the stored
-    plant trajectory DMS_tLBMPC_q100.mat"""
+    plant trajectory DMS_tLBMPC_q100.mat - the learned correction moves x4 at step 2 by 1.1 away
+    from the nominal (LMPC) loop, and the loop follows the stored run (measured: slow states
+    1.0e-8, all states 1.1e-5 over 25 steps, profiles/r03_learned/)"""
     import bqp
     st = golden('dms_lbmpc_loops.npz')['DMS_tLBMPC_q100']
-    T = 40
-    r = bqp.closed_loop_sqp(_dms(mg), X_INIT, T, learning=dict(q=100, mask=1))
+    T = 25
+    r = bqp.closed_loop_sqp(_mpc(mg), X_INIT, T, learning=dict(q=100, mask=1))
     assert (r.exitflag == 1).all(), r.exitflag
     e = np.abs(r.X[0] - st[:T + 1])
-    assert e[:4].max() < 5e-6, e[:4].max(axis=1)
-    assert e[:, :2].max() < 1e-4, e[:, :2].max()
+    assert e[:, :2].max() < 1e-7, e[:, :2].max()
+    assert e.max() < 3e-5, e.max(axis=1)
+    assert abs(r.X[0, 2, 3] - 3.0406) > 1.0
+    # the logged learned one-step predictions: x_eq + A dx + B du + g with the window before the
+    # update (DMS_LBMPC_casadi.m:199)
+    from oracle import lbmpc
+    XL, _ = lbmpc.window_replay(r.X[0], r.U[0, :, 0], mg['A'], mg['B'], mg['x_wp'], mg['u_wp'], 100)
+    assert np.abs(r.XL[0] - XL).max() < 1e-12
 
 
 def test_dms_lbmpc_loop_vs_oracle(mg):
-    """a batch of perturbed initial states: every instance's first moves equal the oracle's
-    restatement of the loop (same algorithm, GN-SQP to a KKT point)"""
+    """16 initial states around x_init: every instance's closed loop equals the oracle's
+    restatement of the loop (same GN-SQP; first moves to the SQP's stopping accuracy)"""
     import bqp
-    from oracle import lbmpc
-    sets = golden('lbmpc_instance.npz')
-    rng = np.random.default_rng(11)
-    B, T = 16, 3
-    X0 = X_INIT + rng.uniform(-1, 1, (B, 4)) * np.array([0.02, 0.02, 0.0, 0.0])
-    r = bqp.closed_loop_sqp(_dms(mg), X0, T, learning=dict(q=100, mask=1))
+    o = golden('dms_lbmpc_oracle.npz')
+    T = int(o['steps'])
+    r = bqp.closed_loop_sqp(_mpc(mg), o['x0'], T, learning=dict(q=100, mask=1))
     assert (r.exitflag == 1).all(), r.exitflag
-    for b in (0, 7):
-        Xo, Uo, _, _ = lbmpc.dms_lbmpc_loop(mg, sets, 100, 100, T, x_init=X0[b])
-        assert np.abs(r.U[b, :, 0] - Uo).max() < 1e-6, (b, r.U[b, :, 0] - Uo)
-        assert np.abs(r.X[b] - Xo).max() < 1e-7
+    du = np.abs(r.U[:, :, 0] - o['U'])
+    assert du.max() < 2e-6, du.max(axis=0)
+    assert np.median(du) < 5e-7
+    assert np.abs(r.X - o['X'])[:, :, :2].max() < 1e-8
+
+
+def test_hybrid_lbmpc_loop_vs_oracle(mg):
+    """the hybrid cost (hybrid_LBMPC_casadi.m:250-311: terminal term on the nominal x_N) in the
+    same loop with a 7-row window whose points all count (mask 0) vs the oracle's loop"""
+    import bqp
+    o = golden('dms_lbmpc_oracle.npz')
+    T = int(o['steps'])
+    r = bqp.closed_loop_sqp(_mpc(mg, 'HybridLBMPC'), X_INIT, T, learning=dict(q=100, mask=0))
+    assert (r.exitflag == 1).all(), r.exitflag
+    assert np.abs(r.U[0, :, 0] - o['hyb_U']).max() < 2e-6
+    assert np.abs(r.X[0] - o['hyb_X']).max() < 2e-5
 
 
 def test_dms_lbmpc_unmasked_window_vs_stored(mg):
-    """the same cost with a 7-row window whose zero points count (mask = 0, q = 10) reproduces
-    the stored DMS_tLBMPC.mat (its first learned move: x4 3.1073)"""
+    """the DMS cost with a 7-row window whose zero points count (mask = 0, q = 10) reproduces the
+    stored DMS_tLBMPC.mat (its first learned move: x4 3.1073)"""
     import bqp
     st = golden('dms_lbmpc_loops.npz')['DMS_tLBMPC']
-    T = 3
-    r = bqp.closed_loop_sqp(_dms(mg), X_INIT, T, learning=dict(q=10, mask=0))
+    T = 12
+    r = bqp.closed_loop_sqp(_mpc(mg), X_INIT, T, learning=dict(q=10, mask=0))
     assert (r.exitflag == 1).all(), r.exitflag
-    assert np.abs(r.X[0] - st[:T + 1]).max() < 5e-6, np.abs(r.X[0] - st[:T + 1]).max(axis=1)
+    e = np.abs(r.X[0] - st[:T + 1])
+    assert e[:, :2].max() < 1e-7 and e.max() < 3e-5, e.max(axis=1)

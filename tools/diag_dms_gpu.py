@@ -26,7 +26,7 @@ X0 = np.array([0.15, 1.2875, 1.1547, 0.0]) + rng.uniform(-1, 1, (B, 4)) * np.arr
 t0 = time.time()
 Uo = {b: lbmpc.dms_lbmpc_loop(mg, g, 100, 100, T, x_init=X0[b])[1] for b in (0, 8)}
 print('oracle loops %.1f s' % (time.time() - t0), flush=True)
-for tol, mi in ((1e-8, 200), (1e-10, 500)):
+for tol, mi in ((1e-8, 200),):
     t0 = time.time()
     r = bqp.closed_loop_sqp(dms, X0, T, learning=dict(q=100, mask=1), tol=tol, max_iter=mi)
     print('tol %.0e max_iter %d: %.2f s' % (tol, mi, time.time() - t0))
@@ -36,7 +36,7 @@ for tol, mi in ((1e-8, 200), (1e-10, 500)):
         print('  inst %d |U - U_oracle| per step' % b, np.abs(r.U[b, :, 0] - Uo[b]).tolist())
     sys.stdout.flush()
 st = golden('dms_lbmpc_loops.npz')['DMS_tLBMPC_q100']
-for tol in (1e-8, 1e-10):
+for tol in (1e-8,):
     r = bqp.closed_loop_sqp(dms, X0[:0].reshape(0, 4) if False else np.array([[0.15, 1.2875, 1.1547, 0.0]]),
                             25, learning=dict(q=100, mask=1), tol=tol, max_iter=500)
     e = np.abs(r.X[0] - st[:26])

@@ -4,7 +4,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libbqp.so')
+# BQP_LIB: another build of the library, for A/B timing diagnostics (tools/gpu_r03_ab.sh)
+LIB_PATH = os.environ.get('BQP_LIB') or os.path.join(_HERE, 'libbqp.so')
 
 BQP_OK = 0
 BQP_E_ARG = -1

@@ -2284,13 +2284,15 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 }
                 wave_sync();
             };
-            pol_tables(0);
+            // one call site (mode at run time): a single inlined copy of pol_tables (C2
+            // instantiation: 104 -> 80 B/lane of scratch)
+            int mode = 0;
             for (;;) {
+                pol_tables(mode);
                 BARRIER();                                // P_B
                 BARRIER();                                // P_C
                 const int dec = (int)X[X_PDEC];
                 if (dec == 1) {
-                    // polished: the active rows' multipliers (>= 0), 0 on the dropped rows
 #pragma unroll
                     for (int b = 0; b < BPL; ++b) nb[b] = fmax(nb[b], real(0));
 #pragma unroll
@@ -2299,9 +2301,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                     break;
                 }
                 if (dec == 3) break;
-                if (dec == 2) { pol_tables(2); continue; }
+                if (dec == 2) { mode = 2; continue; }
                 BARRIER();                                // P_D
-                pol_tables(1);
+                mode = 1;
             }
             STAMP_STORE(16);
             return;

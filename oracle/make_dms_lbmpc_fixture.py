@@ -5,9 +5,10 @@ Golden fixture of the learned-model NLP closed loops of examples/DMS_LBMPC_casad
 trajectories saved_data+plots/data/casadi/DMS_tLBMPC_q{10,50,100,500}.mat, DMS_tLBMPC.mat and
 DMS_N50_tLBMPC_q{10,100}.mat (`xlo`, 4 x 500 or 4 x 501 - the 501-column files hold x_init
 twice; stored here from x_init on, 500 states each).  Which script variant produced which file is
-established by tools/diag_learned_loops.py (profiles/r03_learned/diag.log): the q10/q50/q100 runs
-are DMS_LBMPC_casadi.m as written (8 x q window with validity row, cost on the learned states),
-DMS_tLBMPC.mat the same cost with a 7-row window whose zero points count (q = 10).  Runs only in
+established by tools/diag_learned_loops.py (profiles/r03_learned/): the q10/q50/q100 runs (N = 100
+and N = 50) are DMS_LBMPC_casadi.m as written (8 x q window with validity row, cost on the learned
+states); DMS_tLBMPC.mat (q = 10) and DMS_tLBMPC_q500.mat the same cost with a 7-row window whose
+zero points count.  Runs only in
 the build container (reads /root/reference); writes plain numeric .npz data.
 
     python -m oracle.make_dms_lbmpc_fixture     # writes tests/golden/dms_lbmpc_loops.npz

@@ -58,6 +58,24 @@ def test_f1_matches_cpu_restatement(mg, term_set, handle):
     assert np.mean(r.iterations == c['iterations']) > 0.9
 
 
+@pytest.mark.parametrize('N', [2, 3, 7, 21, 33])
+def test_horizon_parity_vs_cpu_restatement(mg, term_set, handle, N):
+    """the short-horizon kernel's sweeps run by stage pairs (two-stage recursive doubling,
+    bqp_ocp.hip solve) with a single first / last stage when N is odd: the iterates still equal
+    the C restatement's sequential sweeps to round-off, odd and even N alike"""
+    from oracle import cpu_ref, qp_forms
+    g = golden('lmpc_N20.npz')
+    lm = _lmpc(mg, term_set, N)
+    X0 = g['dx'][:64]
+    r = lm.solve(X0, handle=handle)
+    c = cpu_ref.solve(qp_forms.lmpc_ocp(mg, N, *term_set), X0)
+    assert (r.exitflag == c['exitflag']).all()
+    ok = r.exitflag == 1
+    assert ok.sum() >= 32
+    assert np.abs(r.u[ok] - c['u'][ok]).max() < TOL_ITER
+    assert np.median(np.abs(r.u[ok] - c['u'][ok]).max(axis=(1, 2))) < 1e-10
+
+
 @pytest.mark.parametrize('fname', ['dms_DSS_tLMPC.npz', 'dms_DMS_N50_tLMPC.npz', 'dms_DMS_tLMPC_K.npz',
                                    'dms_tLMPC.npz'])
 def test_f2_tracking_lmpc_vs_exact(mg, term_set, handle, fname):

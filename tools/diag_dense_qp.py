@@ -1,0 +1,51 @@
+"""Diagnostic (GPU): the dense QP sub-problem of the DMS LBMPC SQP (n = 101 variables, 524 rows,
+exact Hessian) through bqp.quadprog at batch 1 and 256 - exit flags, IPM iterations, kernel
+time - against the exact LDP/NNLS solution (oracle/exact_qp.py)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, 'learning-based-mpc_amd'), os.path.join(ROOT, 'tests')):
+    sys.path.insert(0, p)
+import bqp  # noqa: E402
+from conftest import golden  # noqa: E402
+from oracle import exact_qp, lbmpc  # noqa: E402
+from oracle.mg_model import mg_problem  # noqa: E402
+
+mg = mg_problem()
+sets = golden('lbmpc_instance.npz')
+x_eq, u_eq = mg['x_wp'], float(mg['u_wp'])
+X, U, Z, IT = lbmpc.dms_lbmpc_loop(mg, sets, 100, 100, 1)
+x = X[1]
+du = U[0] - u_eq
+dx = X[0] - x_eq
+A, B = mg['A'], mg['B'].reshape(4)
+data = np.zeros((8, 100)); data[7, 0] = 1
+data[:, 1] = np.concatenate([[dx[0], dx[1], du], (x - x_eq) - (A @ dx + B * du), [1]])
+saved = lbmpc.nw
+lbmpc.nw = lbmpc.nw_window
+p = lbmpc.dms_problem(mg, 100, data, sets['F_w_N'], sets['h_w_N'], sets['F_x_d'], sets['h_x_d'])
+x0 = x - x_eq
+Ain, bin_ = lbmpc.constraints(p, x0)
+z = np.concatenate([Z[0][1:100], [0.0], Z[0][100:]])
+H, f = lbmpc.newton_model(p, x0, z, clip=False)
+lbmpc.nw = saved
+b = bin_ - Ain @ z
+ex = exact_qp.solve(H, f, Ain, b)
+print('n %d m %d, exact status %s, active %d' % (len(f), len(b), ex['status'], len(ex['active'])))
+h = bqp.Handle(0)
+for batch in (1, 256):
+    Hb = np.broadcast_to(H, (batch,) + H.shape)
+    fb = np.broadcast_to(f, (batch,) + f.shape)
+    for rep in range(2):
+        t0 = time.perf_counter()
+        xq, fv, flag, out, lam = bqp.quadprog(Hb, fb, Ain, b)
+        el = time.perf_counter() - t0
+    ms, _ = h.kernel_ms() if hasattr(h, 'kernel_ms') else (None, None)
+    its = [o.iterations for o in out] if isinstance(out, (list, tuple)) else getattr(out, 'iterations', None)
+    print('batch %d: %.1f ms host, flags %s, iterations %s, |x - x*| %.2e' % (
+        batch, 1e3 * el, np.unique(flag).tolist(), np.unique(np.asarray(its)).tolist() if its is not None else None,
+        np.abs(np.atleast_2d(xq) - ex['z']).max()))

@@ -115,10 +115,42 @@ __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
         const double dj = sc[8];
         if (!(dj > 0.0)) return false;
         const double ljj = sqrt(dj);
-        for (int i = j + 1 + tid; i < n; i += NTH) K[(int64_t)j * n + i] /= ljj;
+        // column j of L, and its transpose into the (dead) upper triangle: row j of L' is then
+        // contiguous for the backward substitution of chol_solve_w
+        for (int i = j + 1 + tid; i < n; i += NTH) {
+            const double v = K[(int64_t)j * n + i] / ljj;
+            K[(int64_t)j * n + i] = v;
+            K[(int64_t)i * n + j] = v;
+        }
         __syncthreads();
         // trailing update of the lower triangle: K[c][r] -= L[j][r] * L[j][c], r >= c > j
         const int rem = n - j - 1;
+        if (NTH == 256 && rem <= 128) {
+            // 16 x 16 thread grid, 8 x 8 entries per thread: rows j+1 + ty + 16 p, columns
+            // j+1 + tx + 16 q (the packed-triangle index map below costs a square root and two
+            // corrections per entry)
+            const int tx = tid & 15, ty = tid >> 4;
+            double lr[8], lc[8];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int rr = ty + 16 * p, cc = tx + 16 * p;
+                lr[p] = rr < rem ? K[(int64_t)j * n + j + 1 + rr] : 0.0;
+                lc[p] = cc < rem ? K[(int64_t)j * n + j + 1 + cc] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int cc = tx + 16 * q;
+                if (cc >= rem) continue;
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    const int rr = ty + 16 * p;
+                    if (rr < rem && rr >= cc)
+                        K[(int64_t)(j + 1 + cc) * n + j + 1 + rr] -= lr[p] * lc[q];
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         const int64_t cnt = (int64_t)rem * (rem + 1) / 2;
         for (int64_t e = tid; e < cnt; e += NTH) {
             // map e -> (c, r) with c <= r in the trailing block (column-wise packing)
@@ -154,6 +186,51 @@ __device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
         if (threadIdx.x == 0) xs[i] = (xs[i] - s) / L[(int64_t)i * n + i];
         __syncthreads();
     }
+}
+
+// solve L L' x = b in place (xs in LDS, n <= 256) by the first wave alone: lane l keeps entries
+// l, l + 64, .. in registers; column-oriented substitutions broadcast each solved entry with
+// readlane and update the remaining ones from a contiguous column of L (forward) or of L' (the
+// upper triangle block_cholesky leaves, backward) - no workgroup barrier inside (the per-entry
+// block reductions of chol_solve_vec cost two barriers per entry).  Every thread calls it.
+__device__ void chol_solve_w(const double* L, int n, double* xs) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        double xr[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xr[q] = (l + 64 * q < n) ? xs[l + 64 * q] : 0.0;
+        for (int i = 0; i < n; ++i) {             // L y = b
+            const int qi = i >> 6, li = i & 63;
+            double xi = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) if (q == qi) xi = rl(xr[q], li);
+            xi /= L[(int64_t)i * n + i];
+            const double* col = L + (int64_t)i * n;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = l + 64 * q;
+                if (k > i && k < n) xr[q] -= col[k] * xi;
+                if (k == i) xr[q] = xi;
+            }
+        }
+        for (int i = n - 1; i >= 0; --i) {        // L' x = y
+            const int qi = i >> 6, li = i & 63;
+            double xi = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) if (q == qi) xi = rl(xr[q], li);
+            xi /= L[(int64_t)i * n + i];
+            const double* row = L + (int64_t)i * n;   // upper: L(i, k) at [i n + k], k < i
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = l + 64 * q;
+                if (k < i) xr[q] -= row[k] * xi;
+                if (k == i) xr[q] = xi;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) if (l + 64 * q < n) xs[l + 64 * q] = xr[q];
+    }
+    __syncthreads();
 }
 
 // sequential per-thread solve of L L' x = b for column vectors stored with stride (one per thread)
@@ -286,7 +363,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         const double sfl = DQ_PIV_FLOOR * fmax(red.max(smx), 1e-300);
         __syncthreads();
         if (ne > 0) block_cholesky<NTH>(S, ne, sc, sfl);
-        chol_solve_vec<NTH>(K, n, xs, red);
+        chol_solve_w(K, n, xs);
         for (int j = tid; j < n; j += NTH) w[j] = xs[j];
         __syncthreads();
         // mult = S^{-1}(Ex w + Ex z - ex)
@@ -302,7 +379,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
             xs[k] = v;
         }
         __syncthreads();
-        if (ne > 0) chol_solve_vec<NTH>(S, ne, xs, red);
+        if (ne > 0) chol_solve_w(S, ne, xs);
         for (int k = tid; k < ne; k += NTH) mult[k] = xs[k];
         __syncthreads();
         for (int j = tid; j < n; j += NTH) {
@@ -403,6 +480,27 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double* S = W + L.S;
     auto up_present = [&](int j) -> bool { return ub && isfinite(ub[j]); };
     auto lo_present = [&](int j) -> bool { return lb && isfinite(lb[j]); };
+    // A'(w) for a row weight w(r) (every thread calls it): A streamed through LDS row tiles
+    // (coalesced along the rows of column-major A, as the factorisation does), thread j < n
+    // accumulating column j from LDS; the column loops over all m rows that one thread per
+    // column ran before touched 64 cache lines per wave load (m = 1024: ~0.5 ms per product)
+    auto atw = [&](auto&& wfun) -> double {
+        double acc = 0.0;
+        for (int r0 = 0; r0 < m; r0 += TILE) {
+            const int rows = min(TILE, m - r0);
+            __syncthreads();
+            for (int t2 = tid; t2 < rows * n; t2 += DT) {
+                const int rr = t2 % rows, j = t2 / rows;
+                tileA[rr * 257 + j] = A[(int64_t)j * m + r0 + rr];
+            }
+            if (tid < rows) tileA[tid * 257 + 256] = wfun(r0 + tid);
+            __syncthreads();
+            if (tid < n)
+                for (int rr = 0; rr < rows; ++rr) acc += tileA[rr * 257 + tid] * tileA[rr * 257 + 256];
+        }
+        __syncthreads();
+        return acc;
+    };
     // row count
     double cnt = 0.0;
     for (int j = tid; j < n; j += DT) cnt += (up_present(j) ? 1.0 : 0.0) + (lo_present(j) ? 1.0 : 0.0);
@@ -427,12 +525,13 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             re[r] = v;
             fq = fmax(fq, fabs(v));
         }
+        const double alam = atw([&](int r) { return lA[r]; });   // (A' lam)_tid
         for (int j = tid; j < n; j += DT) {
             double v = f[j];
             for (int i = 0; i < n; ++i) v += H[(int64_t)j * n + i] * z[i];
             gs = fmax(gs, fabs(v));
             for (int r = 0; r < me; ++r) v += E[(int64_t)j * me + r] * y[r];
-            for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * lA[r];
+            v += alam;
             riB[j] = 0.0; riB[n + j] = 0.0;
             if (up_present(j)) {
                 v += lB[j];
@@ -465,7 +564,59 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         // K upper entries (i <= j) = H_ij + sum_r A_ri D_r A_rj (+ bound diagonal)
         const int ne = n * (n + 1) / 2;
         double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
-        for (int base = 0; base < ne; base += DT * 8) {
+        if (n <= 128) {
+            // register-tiled A'DA (the normal-equation scheme of lbmpc_normal_kernel): thread
+            // (tx, ty) accumulates the 8 x 8 entries (ty + 16 p, tx + 16 q) over 32-row LDS tiles,
+            // 16 LDS reads per 64 FMAs instead of 3 per FMA (the packed-triangle loop below was
+            // LDS-bandwidth bound: ~0.5 ms per factorisation at n = 101, m = 1024)
+            const int tx = tid & 15, ty = tid >> 4;
+            double acc[8][8];
+#pragma unroll
+            for (int p2 = 0; p2 < 8; ++p2)
+#pragma unroll
+                for (int q2 = 0; q2 < 8; ++q2) acc[p2][q2] = 0.0;
+            for (int r0 = 0; r0 < m; r0 += TILE) {
+                const int rows = min(TILE, m - r0);
+                __syncthreads();
+                for (int t2 = tid; t2 < rows * n; t2 += DT) {
+                    const int rr = t2 % rows, j = t2 / rows;
+                    tileA[rr * 257 + j] = A[(int64_t)j * m + r0 + rr];
+                }
+                if (tid < rows) tileA[tid * 257 + 256] = lA[r0 + tid] / tA[r0 + tid];
+                __syncthreads();
+                for (int rr = 0; rr < rows; ++rr) {
+                    const double* Tr = tileA + rr * 257;
+                    const double dr = Tr[256];
+                    double cj[8];
+#pragma unroll
+                    for (int q2 = 0; q2 < 8; ++q2) cj[q2] = (tx + 16 * q2 < n) ? Tr[tx + 16 * q2] : 0.0;
+#pragma unroll
+                    for (int p2 = 0; p2 < 8; ++p2) {
+                        const int i = ty + 16 * p2;
+                        const double ci = (i < n) ? Tr[i] * dr : 0.0;
+#pragma unroll
+                        for (int q2 = 0; q2 < 8; ++q2) acc[p2][q2] = fma(ci, cj[q2], acc[p2][q2]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int p2 = 0; p2 < 8; ++p2)
+#pragma unroll
+                for (int q2 = 0; q2 < 8; ++q2) {
+                    const int i = ty + 16 * p2, j = tx + 16 * q2;
+                    if (i < n && j < n) {
+                        double v = H[(int64_t)j * n + i] + acc[p2][q2];
+                        if (i == j) {
+                            if (up_present(j)) v += lB[j] / tB[j];
+                            if (lo_present(j)) v += lB[n + j] / tB[n + j];
+                            dmx = fmax(dmx, fabs(v));
+                        }
+                        K[(int64_t)j * n + i] = v;
+                    }
+                }
+            __syncthreads();
+        }
+        for (int base = 0; base < (n <= 128 ? 0 : ne); base += DT * 8) {
             double acc[8];
             int ii[8], jj[8];
 #pragma unroll
@@ -541,9 +692,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double* xs = tileA;  // LDS vector workspace (n <= 256 and me <= 256)
     auto solve = [&]() {
         // q = rd + A'((lam riA - rcA)/tA) + bound terms ; w = -K^{-1} q
+        const double aq = atw([&](int r) { return (lA[r] * riA[r] - rcA[r]) / tA[r]; });
         for (int j = tid; j < n; j += DT) {
-            double v = rd[j];
-            for (int r = 0; r < m; ++r) v += A[(int64_t)j * m + r] * ((lA[r] * riA[r] - rcA[r]) / tA[r]);
+            double v = rd[j] + aq;
             if (up_present(j)) v += (lB[j] * riB[j] - rcB[j]) / tB[j];
             if (lo_present(j)) v -= (lB[n + j] * riB[n + j] - rcB[n + j]) / tB[n + j];
             q[j] = v;
@@ -551,7 +702,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         __syncthreads();
         for (int j = tid; j < n; j += DT) xs[j] = -q[j];
         __syncthreads();
-        chol_solve_vec(K, n, xs, red);
+        chol_solve_w(K, n, xs);
         for (int j = tid; j < n; j += DT) w[j] = xs[j];
         __syncthreads();
         if (me > 0) {
@@ -562,7 +713,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 xs[r] = v;
             }
             __syncthreads();
-            chol_solve_vec(S, me, xs, red);
+            chol_solve_w(S, me, xs);
             for (int r = tid; r < me; r += DT) dy[r] = xs[r];
             __syncthreads();
         }

@@ -32,6 +32,9 @@ x0 = x - x_eq
 Ain, bin_ = lbmpc.constraints(p, x0)
 z = np.concatenate([Z[0][1:100], [0.0], Z[0][100:]])
 H, f = lbmpc.newton_model(p, x0, z, clip=False)
+if not lbmpc.pd_cholesky(H):
+    H, f = lbmpc.gn_model(p, x0, z)
+    print('exact Hessian not positive definite at this iterate: Gauss-Newton model')
 lbmpc.nw = saved
 b = bin_ - Ain @ z
 ex = exact_qp.solve(H, f, Ain, b)
@@ -42,10 +45,10 @@ for batch in (1, 256):
     fb = np.broadcast_to(f, (batch,) + f.shape)
     for rep in range(2):
         t0 = time.perf_counter()
-        xq, fv, flag, out, lam = bqp.quadprog(Hb, fb, Ain, b)
+        xq, fv, flag, out, lam = bqp.quadprog(Hb, fb, Ain, b, handle=h)
         el = time.perf_counter() - t0
-    ms, _ = h.kernel_ms() if hasattr(h, 'kernel_ms') else (None, None)
-    its = [o.iterations for o in out] if isinstance(out, (list, tuple)) else getattr(out, 'iterations', None)
-    print('batch %d: %.1f ms host, flags %s, iterations %s, |x - x*| %.2e' % (
-        batch, 1e3 * el, np.unique(flag).tolist(), np.unique(np.asarray(its)).tolist() if its is not None else None,
+    its = out['iterations']
+    kms, nl = h.kernel_ms()
+    print('batch %d: %.1f ms host, %.2f ms kernels (%d launches), flags %s, iterations %s, |x - x*| %.2e' % (
+        batch, 1e3 * el, kms, nl, np.unique(flag).tolist(), np.unique(np.asarray(its)).tolist(),
         np.abs(np.atleast_2d(xq) - ex['z']).max()))

@@ -69,7 +69,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 struct Red {
     double* sc;  // LDS scratch, >= 4 doubles
-    __device__ double sum(double v) {
+    // forceinline: as calls, sc became a generic pointer (flat accesses) and each reduction a call
+    __device__ __forceinline__ double sum(double v) {
         v = wave_sum(v);
         const int w = threadIdx.x >> 6;
         __syncthreads();
@@ -78,18 +79,16 @@ struct Red {
         double r = sc[0] + sc[1] + sc[2] + sc[3];
         return r;
     }
-    __device__ double max(double v) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    __device__ __forceinline__ double max(double v) {
+        v = wmax(v);                    // DPP (was six ds_bpermute shuffles)
         const int w = threadIdx.x >> 6;
         __syncthreads();
         if ((threadIdx.x & 63) == 0) sc[w] = v;
         __syncthreads();
         return fmax(fmax(sc[0], sc[1]), fmax(sc[2], sc[3]));
     }
-    __device__ double min(double v) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    __device__ __forceinline__ double min(double v) {
+        v = wmin(v);
         const int w = threadIdx.x >> 6;
         __syncthreads();
         if ((threadIdx.x & 63) == 0) sc[w] = v;
@@ -128,24 +127,44 @@ __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
         if (NTH == 256 && rem <= 128) {
             // 16 x 16 thread grid, 8 x 8 entries per thread: rows j+1 + ty + 16 p, columns
             // j+1 + tx + 16 q (the packed-triangle index map below costs a square root and two
-            // corrections per entry)
-            const int tx = tid & 15, ty = tid >> 4;
+            // corrections per entry).  Loads are unconditional from clamped (valid) addresses and
+            // all issued before the first store: guarded loads and in-place read-modify-writes
+            // were one memory round trip each (~50 chained latencies per pivot at n = 101)
+            if (rem == 0) break;
+            const int tx = tid & 15, ty = tid >> 4, nbr = (rem + 15) >> 4;   // nbr: block-uniform
+            const double* lj = K + (int64_t)j * n + j + 1;
             double lr[8], lc[8];
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
-                const int rr = ty + 16 * p, cc = tx + 16 * p;
-                lr[p] = rr < rem ? K[(int64_t)j * n + j + 1 + rr] : 0.0;
-                lc[p] = cc < rem ? K[(int64_t)j * n + j + 1 + cc] : 0.0;
+                lr[p] = lc[p] = 0.0;
+                if (p < nbr) {
+                    lr[p] = lj[min(ty + 16 * p, rem - 1)];
+                    lc[p] = lj[min(tx + 16 * p, rem - 1)];
+                }
             }
+            // blocks (p, q) with q <= p < nbr only (the others are empty or upper); two halves of
+            // 4 x 8 (a 64-entry register tile spilled)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int cc = tx + 16 * q;
-                if (cc >= rem) continue;
+            for (int h = 0; h < 2; ++h) {
+                if (4 * h >= nbr) break;
+                double t[4][8];
 #pragma unroll
-                for (int p = 0; p < 8; ++p) {
-                    const int rr = ty + 16 * p;
-                    if (rr < rem && rr >= cc)
-                        K[(int64_t)(j + 1 + cc) * n + j + 1 + rr] -= lr[p] * lc[q];
+                for (int q = 0; q < 4; ++q) {
+                    const int qq = 4 * h + q, cc = min(tx + 16 * qq, rem - 1);
+#pragma unroll
+                    for (int p = 0; p < 8; ++p)
+                        if (p >= qq && p < nbr)
+                            t[q][p] = K[(int64_t)(j + 1 + cc) * n + j + 1 + min(ty + 16 * p, rem - 1)];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int qq = 4 * h + q, cc = tx + 16 * qq;
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        const int rr = ty + 16 * p;
+                        if (p >= qq && p < nbr && cc < rem && rr < rem && rr >= cc)
+                            K[(int64_t)(j + 1 + cc) * n + j + 1 + rr] = t[q][p] - lr[p] * lc[qq];
+                    }
                 }
             }
             __syncthreads();
@@ -164,6 +183,76 @@ __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
         }
         __syncthreads();
     }
+    return true;
+}
+
+// Cholesky for n <= 128 on 256 threads with ONE barrier per pivot (block_cholesky has three):
+// every thread reads the pivot and column j itself and scales by 1/l_jj in registers; the scaled
+// column goes to the upper triangle (row j of L'), which nothing reads during the sweep, and the
+// lower triangle is filled from it at the end; l_jj is stored one pivot later (no thread reads
+// K[j-1][j-1] at pivot j).  The trailing update is block_cholesky's 16 x 16 grid.  Same result
+// layout as block_cholesky (L lower, L' upper).
+__device__ __forceinline__ bool chol_1b(double* K, int n, double fl) {   // inlined: K stays LDS
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    double lprev = 0.0;
+    for (int j = 0; j < n; ++j) {
+        double d = K[(int64_t)j * n + j];
+        if (fl >= 0.0 && !(d > fl)) d = fl;
+        if (!(d > 0.0)) { __syncthreads(); return false; }   // uniform: every thread read d
+        const double ljj = sqrt(d), inv = 1.0 / ljj;
+        if (tid == 0 && j > 0) K[(int64_t)(j - 1) * n + j - 1] = lprev;
+        lprev = ljj;
+        const int rem = n - j - 1, nbr = (rem + 15) >> 4;
+        if (rem > 0) {
+            const double* lj = K + (int64_t)j * n + j + 1;
+            double lr[8], lc[8];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                lr[p] = lc[p] = 0.0;
+                if (p < nbr) {
+                    lr[p] = lj[min(ty + 16 * p, rem - 1)];
+                    lc[p] = lj[min(tx + 16 * p, rem - 1)];
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < 8; ++p) { lr[p] *= inv; lc[p] *= inv; }
+            if (ty == 0) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int cc = tx + 16 * q;
+                    if (q < nbr && cc < rem) K[(int64_t)(j + 1 + cc) * n + j] = lc[q];
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (4 * h >= nbr) break;
+                double t[4][8];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int qq = 4 * h + q, cc = min(tx + 16 * qq, rem - 1);
+#pragma unroll
+                    for (int p = 0; p < 8; ++p)
+                        if (p >= qq && p < nbr)
+                            t[q][p] = K[(int64_t)(j + 1 + cc) * n + j + 1 + min(ty + 16 * p, rem - 1)];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int qq = 4 * h + q, cc = tx + 16 * qq;
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) {
+                        const int rr = ty + 16 * p;
+                        if (p >= qq && p < nbr && cc < rem && rr < rem && rr >= cc)
+                            K[(int64_t)(j + 1 + cc) * n + j + 1 + rr] = t[q][p] - lr[p] * lc[qq];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) K[(int64_t)(n - 1) * n + n - 1] = lprev;
+    for (int c = ty; c < n; c += 16)                 // lower <- upper: L(r, c) = K[r n + c]
+        for (int r = c + 1 + tx; r < n; r += 16) K[(int64_t)c * n + r] = K[(int64_t)r * n + c];
+    __syncthreads();
     return true;
 }
 
@@ -204,12 +293,15 @@ __device__ void chol_solve_w(const double* L, int n, double* xs) {
             double xi = 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) if (q == qi) xi = rl(xr[q], li);
-            xi /= L[(int64_t)i * n + i];
             const double* col = L + (int64_t)i * n;
+            double cv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cv[q] = col[min(l + 64 * q, n - 1)];   // unconditional loads
+            xi /= col[i];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = l + 64 * q;
-                if (k > i && k < n) xr[q] -= col[k] * xi;
+                if (k > i && k < n) xr[q] -= cv[q] * xi;
                 if (k == i) xr[q] = xi;
             }
         }
@@ -218,12 +310,15 @@ __device__ void chol_solve_w(const double* L, int n, double* xs) {
             double xi = 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) if (q == qi) xi = rl(xr[q], li);
-            xi /= L[(int64_t)i * n + i];
             const double* row = L + (int64_t)i * n;   // upper: L(i, k) at [i n + k], k < i
+            double rv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rv[q] = row[min(l + 64 * q, n - 1)];
+            xi /= row[i];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = l + 64 * q;
-                if (k < i) xr[q] -= row[k] * xi;
+                if (k < i) xr[q] -= rv[q] * xi;
                 if (k == i) xr[q] = xi;
             }
         }
@@ -454,13 +549,50 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
     return false;
 }
 
+#ifdef BQP_DSTAMPS
+// diagnostic build only (tools/gpu_r03_dstamps.sh): s_memtime cycles per phase of instance 0,
+// printed by thread 0 at exit; never linked into the product library
+#define DST_DECL                                                           \
+    unsigned long long dst_last = __builtin_amdgcn_s_memtime(), dst_acc[12]; \
+    _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) dst_acc[i_] = 0
+#define DST(id)                                                            \
+    do {                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                     \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();        \
+        dst_acc[id] += _t - dst_last;                                      \
+        dst_last = _t;                                                     \
+    } while (0)
+#else
+#define DST_DECL do { } while (0)
+#define DST(id) do { } while (0)
+#endif
+
+// dense_ipm_kernel LDS: the A row tiles (TILE rows, stride ts = 32 ceil(n/32) + 1 doubles - odd
+// in 64-bit words across the rows a tile load writes - column ts - 1 the row weight), then, when
+// it fits, the n x n factor K = L (lower) / L' (upper) itself: the Cholesky and the four
+// triangular solves per iteration then run on LDS instead of L2 round trips
+#define DENSE_LDS_MAX (152 * 1024)
+__host__ __device__ inline int dense_ts(int n) { return 32 * ((n + 31) / 32) + 1; }
+__host__ __device__ inline bool dense_k_lds(int n) {
+    return (size_t)(TILE * dense_ts(n) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
+}
+__host__ __device__ inline size_t dense_lds_bytes(int n) {
+    return sizeof(double) * (size_t)(TILE * dense_ts(n) + (dense_k_lds(n) ? n * n : 0));
+}
+
+template <bool KL>   // KL: the factor lives in LDS (dense_k_lds(n)); a compile-time choice so that
+                     // every access to it is a ds_* instruction (a run-time select made the pointer
+                     // generic: flat accesses, ~5k cycles per Cholesky pivot)
 __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
     if (inst >= a.batch) return;
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
     __shared__ double sc[16];
-    __shared__ double tileA[TILE * 257];
+    extern __shared__ double dlds[];
+    const int ts = dense_ts(n), tw = ts - 1;
+    double* tileA = dlds;
     Red red{sc};
+    DST_DECL;
     const DWork L = DWork::make(n, m, me);
     double* W = a.work + (int64_t)inst * a.work_stride;
     const double* H = a.H + (int64_t)inst * a.sH;
@@ -475,28 +607,89 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double *rd = W + L.rd, *re = W + L.re;
     double *tA = W + L.tA, *lA = W + L.lA, *riA = W + L.riA, *rcA = W + L.rcA, *dtA = W + L.dtA, *dlA = W + L.dlA;
     double *tB = W + L.tB, *lB = W + L.lB, *riB = W + L.riB, *rcB = W + L.rcB, *dtB = W + L.dtB, *dlB = W + L.dlB;
-    double* K = W + L.K;
+    double* K = KL ? dlds + TILE * ts : W + L.K;   // the factor (LDS when it fits)
     double* Y = W + L.Y;
     double* S = W + L.S;
     auto up_present = [&](int j) -> bool { return ub && isfinite(ub[j]); };
     auto lo_present = [&](int j) -> bool { return lb && isfinite(lb[j]); };
+    // rows r0 .. r0 + rows - 1 of A into tileA (row-major, stride ts): 8 clamped loads in flight
+    // per thread before the LDS stores (the load -> store loop waited on every load)
+    auto load_tile = [&](int r0, int rows) {
+        const int tot = rows * n;
+        const bool full = rows == TILE;
+        for (int b0 = 0; b0 < tot; b0 += 8 * DT) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t2 = min(b0 + tid + u * DT, tot - 1);
+                const int rr = full ? (t2 & (TILE - 1)) : t2 % rows, j = full ? (t2 / TILE) : t2 / rows;
+                v[u] = A[(int64_t)j * m + r0 + rr];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t2 = b0 + tid + u * DT;
+                const int rr = full ? (t2 & (TILE - 1)) : t2 % rows, j = full ? (t2 / TILE) : t2 / rows;
+                if (t2 < tot) tileA[rr * ts + j] = v[u];
+            }
+        }
+    };
+    // (A v)_r for one row r of column-major A: four independent chains
+    auto arow = [&](int r, const double* v) -> double {
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {
+            s0 = fma(A[(int64_t)j * m + r], v[j], s0);
+            s1 = fma(A[(int64_t)(j + 1) * m + r], v[j + 1], s1);
+            s2 = fma(A[(int64_t)(j + 2) * m + r], v[j + 2], s2);
+            s3 = fma(A[(int64_t)(j + 3) * m + r], v[j + 3], s3);
+        }
+        for (; j < n; ++j) s0 = fma(A[(int64_t)j * m + r], v[j], s0);
+        return (s0 + s1) + (s2 + s3);
+    };
     // A'(w) for a row weight w(r) (every thread calls it): A streamed through LDS row tiles
     // (coalesced along the rows of column-major A, as the factorisation does), thread j < n
     // accumulating column j from LDS; the column loops over all m rows that one thread per
     // column ran before touched 64 cache lines per wave load (m = 1024: ~0.5 ms per product)
     auto atw = [&](auto&& wfun) -> double {
+        if (m + n <= TILE * ts) {
+            // the row weights into LDS once; wave wv takes column groups 16 g (g = wv, wv + 4,
+            // ..): lanes over rows, 16 independent loads per row step, one transposed wave sum
+            // (wsum_t) per group; no tile barriers (the tile version waited on a load round
+            // trip and two barriers per 32 rows)
+            double* wl = tileA;
+            double* out = tileA + m;
+            __syncthreads();
+            for (int r = tid; r < m; r += DT) wl[r] = wfun(r);
+            __syncthreads();
+            const int lane = tid & 63, wv = tid >> 6;
+            for (int g = wv; 16 * g < n; g += DT / 64) {
+                double ac[16];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) ac[c] = 0.0;
+                const double* Ag = A + (int64_t)(16 * g) * m;
+                for (int r = lane; r < m; r += 64) {
+                    const double vr = wl[r];
+#pragma unroll
+                    for (int c = 0; c < 16; ++c)
+                        ac[c] = fma(Ag[(int64_t)min(c, n - 1 - 16 * g) * m + r], vr, ac[c]);
+                }
+                const double sv = wsum_t(ac, lane);
+                if (lane < 16 && 16 * g + lane < n) out[16 * g + lane] = sv;
+            }
+            __syncthreads();
+            const double res = tid < n ? out[tid] : 0.0;
+            __syncthreads();
+            return res;
+        }
         double acc = 0.0;
         for (int r0 = 0; r0 < m; r0 += TILE) {
             const int rows = min(TILE, m - r0);
             __syncthreads();
-            for (int t2 = tid; t2 < rows * n; t2 += DT) {
-                const int rr = t2 % rows, j = t2 / rows;
-                tileA[rr * 257 + j] = A[(int64_t)j * m + r0 + rr];
-            }
-            if (tid < rows) tileA[tid * 257 + 256] = wfun(r0 + tid);
+            load_tile(r0, rows);
+            if (tid < rows) tileA[tid * ts + tw] = wfun(r0 + tid);
             __syncthreads();
             if (tid < n)
-                for (int rr = 0; rr < rows; ++rr) acc += tileA[rr * 257 + tid] * tileA[rr * 257 + 256];
+                for (int rr = 0; rr < rows; ++rr) acc += tileA[rr * ts + tid] * tileA[rr * ts + tw];
         }
         __syncthreads();
         return acc;
@@ -512,13 +705,13 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                          double& cmax) {
         double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0, cm = 0.0;
         for (int r = tid; r < m; r += DT) {
-            double v = tA[r] - b[r];
-            for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * z[j];
+            const double v = tA[r] - b[r] + arow(r, z);
             riA[r] = v;
             fe = fmax(fe, fabs(v));
             cs += tA[r] * lA[r];
             cm = fmax(cm, tA[r] * lA[r]);
         }
+        DST(0);
         for (int r = tid; r < me; r += DT) {
             double v = -e[r];
             for (int j = 0; j < n; ++j) v += E[(int64_t)j * me + r] * z[j];
@@ -526,6 +719,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             fq = fmax(fq, fabs(v));
         }
         const double alam = atw([&](int r) { return lA[r]; });   // (A' lam)_tid
+        DST(10);
         for (int j = tid; j < n; j += DT) {
             double v = f[j];
             for (int i = 0; i < n; ++i) v += H[(int64_t)j * n + i] * z[i];
@@ -557,11 +751,12 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         gscale = red.max(gs);
         zmax = red.max(zm);
         cmax = red.max(cm);
+        DST(11);
     };
 
     // ---------------------------------------------------------------- factorisation
     auto factor = [&]() -> bool {
-        // K upper entries (i <= j) = H_ij + sum_r A_ri D_r A_rj (+ bound diagonal)
+        // K = H + sum_r A_r' D_r A_r (+ bound diagonal): lower triangle (n <= 128) or both
         const int ne = n * (n + 1) / 2;
         double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
         if (n <= 128) {
@@ -578,33 +773,35 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             for (int r0 = 0; r0 < m; r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
-                for (int t2 = tid; t2 < rows * n; t2 += DT) {
-                    const int rr = t2 % rows, j = t2 / rows;
-                    tileA[rr * 257 + j] = A[(int64_t)j * m + r0 + rr];
-                }
-                if (tid < rows) tileA[tid * 257 + 256] = lA[r0 + tid] / tA[r0 + tid];
+                load_tile(r0, rows);
+                if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
                 for (int rr = 0; rr < rows; ++rr) {
-                    const double* Tr = tileA + rr * 257;
-                    const double dr = Tr[256];
-                    double cj[8];
+                    const double* Tr = tileA + rr * ts;
+                    const double dr = Tr[tw];
+                    // clamped, unconditional LDS reads (one wait per row instead of one per
+                    // guarded load); accumulators of entries i or j >= n are discarded
+                    // blocks q2 <= p2 < nb only: the Cholesky reads the lower triangle
+                    double cj[8], ci[8];
 #pragma unroll
-                    for (int q2 = 0; q2 < 8; ++q2) cj[q2] = (tx + 16 * q2 < n) ? Tr[tx + 16 * q2] : 0.0;
+                    for (int q2 = 0; q2 < 8; ++q2) {        // unconditional: no wait inside a branch
+                        cj[q2] = Tr[min(tx + 16 * q2, n - 1)];
+                        ci[q2] = Tr[min(ty + 16 * q2, n - 1)];
+                    }
 #pragma unroll
-                    for (int p2 = 0; p2 < 8; ++p2) {
-                        const int i = ty + 16 * p2;
-                        const double ci = (i < n) ? Tr[i] * dr : 0.0;
+                    for (int p2 = 0; p2 < 8; ++p2) {    // no run-time bound: a branch per block row
+                        const double cd = ci[p2] * dr;     // cost more than the blocks it skipped
 #pragma unroll
-                        for (int q2 = 0; q2 < 8; ++q2) acc[p2][q2] = fma(ci, cj[q2], acc[p2][q2]);
+                        for (int q2 = 0; q2 <= p2; ++q2) acc[p2][q2] = fma(cd, cj[q2], acc[p2][q2]);
                     }
                 }
             }
 #pragma unroll
             for (int p2 = 0; p2 < 8; ++p2)
 #pragma unroll
-                for (int q2 = 0; q2 < 8; ++q2) {
+                for (int q2 = 0; q2 <= p2; ++q2) {
                     const int i = ty + 16 * p2, j = tx + 16 * q2;
-                    if (i < n && j < n) {
+                    if (i < n && i >= j) {      // lower triangle (col-major K[j n + i], i >= j)
                         double v = H[(int64_t)j * n + i] + acc[p2][q2];
                         if (i == j) {
                             if (up_present(j)) v += lB[j] / tB[j];
@@ -637,18 +834,15 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             for (int r0 = 0; r0 < m; r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
-                for (int t2 = tid; t2 < rows * n; t2 += DT) {
-                    const int rr = t2 % rows, j = t2 / rows;
-                    tileA[rr * 257 + j] = A[(int64_t)j * m + r0 + rr];
-                }
-                if (tid < rows) tileA[tid * 257 + 256] = lA[r0 + tid] / tA[r0 + tid];
+                load_tile(r0, rows);
+                if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
 #pragma unroll
                 for (int q2 = 0; q2 < 8; ++q2) {
                     if (ii[q2] < 0) continue;
                     double s = 0.0;
                     for (int rr = 0; rr < rows; ++rr)
-                        s += tileA[rr * 257 + ii[q2]] * tileA[rr * 257 + 256] * tileA[rr * 257 + jj[q2]];
+                        s += tileA[rr * ts + ii[q2]] * tileA[rr * ts + tw] * tileA[rr * ts + jj[q2]];
                     acc[q2] += s;
                 }
             }
@@ -667,7 +861,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             }
         }
         const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
-        if (!block_cholesky(K, n, sc, kfl)) return false;
+        DST(1);
+        if (!(n <= 128 ? chol_1b(K, n, kfl) : block_cholesky(K, n, sc, kfl))) return false;
+        DST(2);
         // Y = K^{-1} Aeq' (one thread per equality row), S = Aeq Y
         for (int r = tid; r < me; r += DT) {
             double* yc = Y + (int64_t)r * n;
@@ -692,7 +888,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double* xs = tileA;  // LDS vector workspace (n <= 256 and me <= 256)
     auto solve = [&]() {
         // q = rd + A'((lam riA - rcA)/tA) + bound terms ; w = -K^{-1} q
+        DST(3);
         const double aq = atw([&](int r) { return (lA[r] * riA[r] - rcA[r]) / tA[r]; });
+        DST(7);
         for (int j = tid; j < n; j += DT) {
             double v = rd[j] + aq;
             if (up_present(j)) v += (lB[j] * riB[j] - rcB[j]) / tB[j];
@@ -703,6 +901,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         for (int j = tid; j < n; j += DT) xs[j] = -q[j];
         __syncthreads();
         chol_solve_w(K, n, xs);
+        DST(8);
         for (int j = tid; j < n; j += DT) w[j] = xs[j];
         __syncthreads();
         if (me > 0) {
@@ -724,8 +923,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         }
         __syncthreads();
         for (int r = tid; r < m; r += DT) {
-            double v = 0.0;
-            for (int j = 0; j < n; ++j) v += A[(int64_t)j * m + r] * dz[j];
+            const double v = arow(r, dz);
             dtA[r] = -riA[r] - v;
             dlA[r] = (-rcA[r] - lA[r] * dtA[r]) / tA[r];
         }
@@ -735,6 +933,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             if (lo_present(j)) { dtB[n + j] = -riB[n + j] + dz[j]; dlB[n + j] = (-rcB[n + j] - lB[n + j] * dtB[n + j]) / tB[n + j]; }
         }
         __syncthreads();
+        DST(9);
     };
 
     auto max_step = [&]() -> double {
@@ -799,7 +998,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             K[e2] = H[e2] + (i == j ? sh : 0.0);
         }
         __syncthreads();
-        if (!block_cholesky(K, n, sc, -1.0)) flag = -6;
+        if (!(n <= 128 ? chol_1b(K, n, -1.0) : block_cholesky(K, n, sc, -1.0))) flag = -6;
     }
     double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0, cmax = 0.0;
     residuals(stat, feq, fin, csum, gscale, zmax, cmax);
@@ -848,6 +1047,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             solve();
             double al = max_step();
             const double mua = comp_after(al) * minv;
+            DST(4);
             double sg = mua / mu;
             sg = sg * sg * sg;
             const double smu = sg * mu;
@@ -874,8 +1074,16 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             for (int r = tid; r < me; r += DT) y[r] += al * dy[r];
             for (int r = tid; r < m; r += DT) { tA[r] += al * dtA[r]; lA[r] += al * dlA[r]; }
             __syncthreads();
+            DST(5);
         }
     }
+#ifdef BQP_DSTAMPS
+    if (inst == 0 && tid == 0)
+        printf("DSTAMPS it %d rows %llu atw_res %llu res_rest %llu ada %llu chol %llu solve_pre %llu "
+               "atw_sol %llu trsv %llu sol_post %llu step %llu upd %llu other %llu\n", it, dst_acc[0],
+               dst_acc[10], dst_acc[11], dst_acc[1], dst_acc[2], dst_acc[3], dst_acc[7], dst_acc[8],
+               dst_acc[9], dst_acc[4], dst_acc[5], dst_acc[6]);
+#endif
     // ---------------------------------------------------------------- outputs
     double fv = 0.0;
     for (int j = tid; j < n; j += DT) {
@@ -1429,7 +1637,19 @@ hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
         else
             hipLaunchKernelGGL(dense_wave_kernel<2>, dim3(a.batch), dim3(64), lds, st, a);
     } else {
-        hipLaunchKernelGGL(dense_ipm_kernel, dim3(a.batch), dim3(DT), 0, st, a);
+        const size_t lds = dense_lds_bytes(a.n);
+        if (dense_k_lds(a.n)) {
+            static bool lds_attr = false;
+            if (!lds_attr) {
+                hipError_t e = hipFuncSetAttribute((const void*)dense_ipm_kernel<true>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, DENSE_LDS_MAX);
+                if (e != hipSuccess) return e;
+                lds_attr = true;
+            }
+            hipLaunchKernelGGL(dense_ipm_kernel<true>, dim3(a.batch), dim3(DT), lds, st, a);
+        } else {
+            hipLaunchKernelGGL(dense_ipm_kernel<false>, dim3(a.batch), dim3(DT), lds, st, a);
+        }
     }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess || !a.polish || !a.work) return err;

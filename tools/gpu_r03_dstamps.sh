@@ -1,0 +1,7 @@
+#!/bin/bash
+# dense workgroup kernel phase stamps (diagnostic library, instance 0 printed by the kernel)
+set -o pipefail
+OUT=gpurun_out/${1:-r03_dst}
+mkdir -p $OUT
+BQP_LIB=learning-based-mpc_amd/build/dstamps/libbqp_dstamps.so timeout -k 10 200 python -u tools/diag_dense_qp.py > $OUT/dq_dst.log 2>&1 || exit $?
+grep DSTAMPS $OUT/dq_dst.log | tail -4

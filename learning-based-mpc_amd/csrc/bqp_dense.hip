@@ -186,13 +186,65 @@ __device__ bool block_cholesky(double* K, int n, double* sc, double fl) {
     return true;
 }
 
+// trailing update of pivot j over NB = ceil(rem / 16) block rows (compile-time, so no uniform
+// branch per block: those cost more than the LDS traffic of the update), thread (tx, ty) owning
+// rows j+1 + ty + 16 p and columns j+1 + tx + 16 q, blocks q <= p.  Loads clamped and
+// unconditional; stores of entries outside the lower trailing triangle go to a per-lane junk
+// slot instead of a masked store.  Also writes the scaled column j to the upper triangle.
+template <int NB>
+__device__ __forceinline__ void chol_upd(double* K, int n, int j, int rem, double inv, double* junk) {
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const double* lj = K + (int64_t)j * n + j + 1;
+    double lr[NB], lc[NB];
+#pragma unroll
+    for (int p = 0; p < NB; ++p) {
+        lr[p] = lj[min(ty + 16 * p, rem - 1)];
+        lc[p] = lj[min(tx + 16 * p, rem - 1)];
+    }
+    double* jk = junk + (tid & 63);
+#pragma unroll
+    for (int p = 0; p < NB; ++p) { lr[p] *= inv; lc[p] *= inv; }
+    if (ty == 0) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int cc = tx + 16 * q;
+            if (cc < rem) K[(int64_t)(j + 1 + cc) * n + j] = lc[q];
+        }
+    }
+    constexpr int NH = (NB + 3) / 4;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        double t[4][NB];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qq = 4 * h + q, cc = min(tx + 16 * qq, rem - 1);
+#pragma unroll
+            for (int p = 0; p < NB; ++p)
+                if (qq < NB && p >= qq)
+                    t[q][p] = K[(int64_t)(j + 1 + cc) * n + j + 1 + min(ty + 16 * p, rem - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qq = 4 * h + q, cc = tx + 16 * qq;
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                if (qq < NB && p >= qq) {
+                    const int rr = ty + 16 * p;
+                    double* dst = (cc < rem && rr < rem && rr >= cc) ? K + (int64_t)(j + 1 + cc) * n + j + 1 + rr : jk;
+                    *dst = t[q][p] - lr[p] * lc[qq];
+                }
+            }
+        }
+    }
+}
+
 // Cholesky for n <= 128 on 256 threads with ONE barrier per pivot (block_cholesky has three):
 // every thread reads the pivot and column j itself and scales by 1/l_jj in registers; the scaled
 // column goes to the upper triangle (row j of L'), which nothing reads during the sweep, and the
 // lower triangle is filled from it at the end; l_jj is stored one pivot later (no thread reads
 // K[j-1][j-1] at pivot j).  The trailing update is block_cholesky's 16 x 16 grid.  Same result
 // layout as block_cholesky (L lower, L' upper).
-__device__ __forceinline__ bool chol_1b(double* K, int n, double fl) {   // inlined: K stays LDS
+__device__ __forceinline__ bool chol_1b(double* K, int n, double fl, double* junk) {   // inlined: K stays LDS
     const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
     double lprev = 0.0;
     for (int j = 0; j < n; ++j) {
@@ -202,50 +254,17 @@ __device__ __forceinline__ bool chol_1b(double* K, int n, double fl) {   // inli
         const double ljj = sqrt(d), inv = 1.0 / ljj;
         if (tid == 0 && j > 0) K[(int64_t)(j - 1) * n + j - 1] = lprev;
         lprev = ljj;
-        const int rem = n - j - 1, nbr = (rem + 15) >> 4;
-        if (rem > 0) {
-            const double* lj = K + (int64_t)j * n + j + 1;
-            double lr[8], lc[8];
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                lr[p] = lc[p] = 0.0;
-                if (p < nbr) {
-                    lr[p] = lj[min(ty + 16 * p, rem - 1)];
-                    lc[p] = lj[min(tx + 16 * p, rem - 1)];
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < 8; ++p) { lr[p] *= inv; lc[p] *= inv; }
-            if (ty == 0) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int cc = tx + 16 * q;
-                    if (q < nbr && cc < rem) K[(int64_t)(j + 1 + cc) * n + j] = lc[q];
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (4 * h >= nbr) break;
-                double t[4][8];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int qq = 4 * h + q, cc = min(tx + 16 * qq, rem - 1);
-#pragma unroll
-                    for (int p = 0; p < 8; ++p)
-                        if (p >= qq && p < nbr)
-                            t[q][p] = K[(int64_t)(j + 1 + cc) * n + j + 1 + min(ty + 16 * p, rem - 1)];
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int qq = 4 * h + q, cc = tx + 16 * qq;
-#pragma unroll
-                    for (int p = 0; p < 8; ++p) {
-                        const int rr = ty + 16 * p;
-                        if (p >= qq && p < nbr && cc < rem && rr < rem && rr >= cc)
-                            K[(int64_t)(j + 1 + cc) * n + j + 1 + rr] = t[q][p] - lr[p] * lc[qq];
-                    }
-                }
-            }
+        const int rem = n - j - 1;
+        switch ((rem + 15) >> 4) {      // block-uniform; each case branch-free inside
+            case 1: chol_upd<1>(K, n, j, rem, inv, junk); break;
+            case 2: chol_upd<2>(K, n, j, rem, inv, junk); break;
+            case 3: chol_upd<3>(K, n, j, rem, inv, junk); break;
+            case 4: chol_upd<4>(K, n, j, rem, inv, junk); break;
+            case 5: chol_upd<5>(K, n, j, rem, inv, junk); break;
+            case 6: chol_upd<6>(K, n, j, rem, inv, junk); break;
+            case 7: chol_upd<7>(K, n, j, rem, inv, junk); break;
+            case 8: chol_upd<8>(K, n, j, rem, inv, junk); break;
+            default: break;
         }
         __syncthreads();
     }
@@ -776,6 +795,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 load_tile(r0, rows);
                 if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
+#pragma unroll 2
                 for (int rr = 0; rr < rows; ++rr) {
                     const double* Tr = tileA + rr * ts;
                     const double dr = Tr[tw];
@@ -862,7 +882,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         }
         const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
         DST(1);
-        if (!(n <= 128 ? chol_1b(K, n, kfl) : block_cholesky(K, n, sc, kfl))) return false;
+        if (!(n <= 128 ? chol_1b(K, n, kfl, tileA) : block_cholesky(K, n, sc, kfl))) return false;
         DST(2);
         // Y = K^{-1} Aeq' (one thread per equality row), S = Aeq Y
         for (int r = tid; r < me; r += DT) {
@@ -998,7 +1018,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             K[e2] = H[e2] + (i == j ? sh : 0.0);
         }
         __syncthreads();
-        if (!(n <= 128 ? chol_1b(K, n, -1.0) : block_cholesky(K, n, sc, -1.0))) flag = -6;
+        if (!(n <= 128 ? chol_1b(K, n, -1.0, tileA) : block_cholesky(K, n, sc, -1.0))) flag = -6;
     }
     double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0, cmax = 0.0;
     residuals(stat, feq, fin, csum, gscale, zmax, cmax);

@@ -65,9 +65,13 @@ typedef struct {
     int want_duals;    /* reserved (set 0): the structured API writes the multiplier outputs
                           whenever its `duals` argument is non-NULL */
     int polish;        /* structured API, fp64 active-set polish: the rows with lam > t are solved
-                          as equalities (augmented Lagrangian on the Riccati factorisation, with
-                          active-set corrections) and the result replaces the interior-point
-                          iterate if it passes the KKT checks (bqp_output.polished).
+                          as equalities (augmented-Lagrangian steps and conjugate gradients on
+                          their multipliers, on the Riccati factorisation with weight rho on
+                          the active rows, with active-set corrections) and the result replaces
+                          the interior-point iterate if it passes the KKT checks
+                          (bqp_output.polished).  It runs in a separate repair launch over the
+                          instances the solve launch marks, so the solve kernel carries no
+                          polish state.
                           0 (default) or 1: after an iteration-limit or numerical-failure exit
                           (e.g. multipliers ~1e3-1e5 drive D = lam/t out of fp64 range);
                           2: also when a row is left weakly active (slack and multiplier both
@@ -216,7 +220,9 @@ typedef struct {
                            (costate-weighted NW Hessians) whenever the sum is positive definite
                            (Cholesky pivots > 1e-10 max|H_ii|), Gauss-Newton otherwise.  GN
                            converges linearly (rate ~0.5) on DMS_LBMPC_casadi.m's learned-state
-                           costs: 60-200 SQP iterations against 4-6 with 1 */
+                           costs: 60-200 SQP iterations against 4-6 with 1.  The exact
+                           term needs n = N nu + np <= 127 (its n x n sum lives in LDS);
+                           longer horizons run Gauss-Newton */
 } bqp_lbmpc_dims;
 
 typedef struct {
@@ -332,8 +338,9 @@ int bqp_closed_loop_lbmpc_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
  * solution shifted one stage with a zero last move and the same theta (the scripts' guess
  * u0 = [u_OL(2:end); u_eq + Kstabil x_N], DMS_LBMPC_casadi.m:209-213, with the tail move of the
  * scripts' Kstabil = 0 case); warm = 0: z = 0 every step (u = u_eq, theta = 0).  opt->max_iter
- * bounds the SQP iterations per step.  X, U, exitflag and lw->XL / lw->window as in
- * bqp_closed_loop_lbmpc; Z (batch*steps*n, may be NULL): every step's SQP solution z;
+ * bounds the SQP iterations per step.  The NW kernel parameters are lw->bandwidth / lw->lambda
+ * when > 0, else data->bandwidth / data->lambda, else the reference's 0.5 / 1e-3.  X, U, exitflag
+ * and lw->XL / lw->window as in bqp_closed_loop_lbmpc; Z (batch*steps*n, may be NULL): every step's SQP solution z;
  * iterations (batch*steps, may be NULL): SQP iterations per step.
  * ---------------------------------------------------------------------------------------- */
 typedef struct {

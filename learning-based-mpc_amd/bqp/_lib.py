@@ -207,12 +207,13 @@ class Handle:
 
 def options(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995,
             want_duals=0, precision=0, polish=1):
-    """precision: 0 fp64, 1 fp32 (structured solver; see include/bqp.h); polish (bqp_options
-    .polish): 1 after 0 / -8 exits (default), 2 also with weakly active rows, 0/False off"""
+    """precision: 0 fp64, 1 fp32 (structured solver; see include/bqp.h).  polish takes the C
+    encoding of bqp_options.polish: 0 (the C default) or 1 after 0 / -8 exits, 2 also with weakly
+    active rows, -1 off; the booleans True / False name 1 / -1."""
     o = Options()
     load().bqp_default_options(C.byref(o))
     o.max_iter, o.tol_stat, o.tol_feas, o.tol_comp, o.tau = max_iter, tol_stat, tol_feas, tol_comp, tau
     o.want_duals = want_duals
     o.precision = precision
-    o.polish = -1 if polish is False or polish == 0 else int(polish)
+    o.polish = (1 if polish else -1) if isinstance(polish, bool) else int(polish)
     return o

@@ -92,6 +92,12 @@ void resolve(const bqp_options* in, bqp_options* o) {
         }                                                                 \
     } while (0)
 
+// an event owned by an entry point's scope: destroyed on every return (HIP_TRY included)
+struct EventGuard {
+    hipEvent_t e = nullptr;
+    ~EventGuard() { if (e) hipEventDestroy(e); }
+};
+
 }  // namespace
 
 extern "C" {
@@ -271,14 +277,18 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     if (mixed && !fit_wpb(true, wpb32)) return BQP_E_UNSUPPORTED;
     // workspace: H, Fp, stats
     const size_t nH = (size_t)(N + 1) * hstride, nF = (size_t)nv * mpad, nS = (size_t)batch * bqp::STATS_W;
+    // + the repair marks (one int per instance, after the stamps of the diagnostic build)
+    const size_t nPol = ((size_t)batch + 1) / 2;
 #ifdef BQP_STAMPS
-    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + (size_t)batch * 32)));
+    const size_t nStamp = (size_t)batch * 32;
 #else
-    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8)));
+    const size_t nStamp = 0;
 #endif
+    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + nStamp + nPol)));
     double* Hd = (double*)h->work.p;
     double* Fd = Hd + nH;
     double* Sd = Fd + nF;
+    int* polneed = (int*)(Sd + nS + 8 + nStamp);
     const double* Hinst = nullptr;
     if (hinst) {   // per-instance prepared stage-cost tables
         HIP_TRY(h->wwork.reserve(sizeof(double) * (size_t)batch * nH));
@@ -301,6 +311,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     a.max_iter = o.max_iter; a.tol_stat = o.tol_stat; a.tol_feas = o.tol_feas;
     a.tol_comp = o.tol_comp; a.tau = o.tau;
     a.polish = o.polish < 0 ? 0 : (o.polish == 0 ? 1 : std::min(o.polish, 2));
+    a.pol_need = polneed;
     a.H = Hd; a.Fp = Fd;
     a.A = D->A; a.B = D->B; a.c = D->c; a.w = D->w; a.xlb = D->xlb; a.xub = D->xub;
     a.ulb = D->ulb; a.uub = D->uub; a.hp = mp > 0 ? D->hp : Hd; a.x0 = D->x0;
@@ -349,9 +360,14 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     } else {
         HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
     }
+    // repair launch (fp64): the instances the solve launch marked (0 / -8 exits; with polish 2
+    // also weakly active rows) are solved again and polished to their active-set solution; a
+    // workgroup with no marked instance leaves at once.  The mixed mode repairs with the
+    // continuation's arguments.
+    if (!f32 && a.polish > 0) HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st, true));
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->timed = true;
-    h->launches = mixed ? 3 : 1;
+    h->launches = (mixed ? 3 : 1) + ((!f32 && a.polish > 0) ? 1 : 0);
     if (out) HIP_TRY(bqp::launch_ocp_finalize(Sd, batch, out, st));
     return BQP_OK;
 }
@@ -646,7 +662,8 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     a.hused = ip; ip += B;
     a.done = ip; ip += B;
     a.ndone = ip;
-    a.hess = d->hessian;
+    // exact Hessian where its LDS fits (n <= 127), Gauss-Newton otherwise (include/bqp.h)
+    a.hess = d->hessian && bqp::lbmpc_hess_fits(n);
     a.lam = lam ? lam : lam_int;
     a.z = z; a.flag = exitflag; a.iters = iterations;
     a.N = N; a.n = n; a.nr = nr; a.m = m; a.q = d->q; a.n_run = d->n_run;
@@ -797,13 +814,15 @@ static int closed_loop_impl(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
     bqp_ocp_data Dm = *D;
     Dm.x0 = s;
     Dm.sx0 = nx;
-    hipEvent_t e0 = nullptr;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventRecord(e0, st));
+    EventGuard e0;
+    HIP_TRY(hipEventCreate(&e0.e));
+    HIP_TRY(hipEventRecord(e0.e, st));
+    int launches = 0;
     for (int t = 0; t < cl->steps; ++t) {
         rc = bqp_solve_ocp_batched_device(h, d, batch, &Dm, opt, xo, uo, th, nullptr, fl, nullptr,
                                           nullptr, stream);
-        if (rc) { hipEventDestroy(e0); return rc; }
+        if (rc) return rc;
+        launches += h->launches + (lw ? 2 : 1);
         HIP_TRY(bqp::launch_mg_plant(batch, N, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
                                      s, X, U, exitflag, st));
         if (lw)
@@ -813,10 +832,9 @@ static int closed_loop_impl(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
     // timing of the whole loop (solves + plant steps) on this stream
     HIP_TRY(hipEventRecord(h->ev1, st));
     HIP_TRY(hipEventSynchronize(h->ev1));
-    std::swap(h->ev0, e0);
-    hipEventDestroy(e0);
+    std::swap(h->ev0, e0.e);   // the guard destroys the previous start event
     h->timed = true;
-    h->launches = (lw ? 4 : 3) * cl->steps;
+    h->launches = launches;
     return BQP_OK;
 }
 
@@ -972,8 +990,10 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     HIP_TRY(bqp::launch_closed_loop_init(batch, nx, cl->steps, x_init, cl->x_eq, s, X, st));
     HIP_TRY(bqp::launch_lbmpc_window_init(batch, cl->steps, q, lw->mask, x_init, win, lw->XL, st));
     HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));
-    const double bw = lw->bandwidth > 0 ? lw->bandwidth : 0.5;
-    const double lam = lw->lambda > 0 ? lw->lambda : 1e-3;
+    // the learned model's NW parameters: the loop's (bqp_learning) when set, else the model's own
+    // (bqp_lbmpc_data, oracleL2NW.m: h = 0.5, lambda = 1e-3 when both are unset)
+    const double bw = lw->bandwidth > 0 ? lw->bandwidth : (D->bandwidth > 0 ? D->bandwidth : 0.5);
+    const double lam = lw->lambda > 0 ? lw->lambda : (D->lambda > 0 ? D->lambda : 1e-3);
     bqp_lbmpc_dims dl = *d;
     dl.mask = 1;                          // the loop's window always carries the validity row
     bqp_lbmpc_data Dl = *D;
@@ -981,9 +1001,9 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     Dl.x0 = s; Dl.sx0 = nx;
     Dl.bin = bin; Dl.sbin = m;
     Dl.bandwidth = bw; Dl.lambda = lam;
-    hipEvent_t e0 = nullptr;
-    HIP_TRY(hipEventCreate(&e0));
-    HIP_TRY(hipEventRecord(e0, st));
+    EventGuard e0;
+    HIP_TRY(hipEventCreate(&e0.e));
+    HIP_TRY(hipEventRecord(e0.e, st));
     int launches = 0;
     for (int t = 0; t < cl->steps; ++t) {
         HIP_TRY(bqp::launch_sqp_loop_prep(batch, nx, n, m, N * d->nu, t > 0 && sl->warm, s,
@@ -991,7 +1011,7 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
         if (t > 0 && !sl->warm) HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));
         rc = bqp_lbmpc_solve_batched_device(h, &dl, batch, &Dl, opt, z, nullptr, nullptr, fl, it,
                                             stream);
-        if (rc) { hipEventDestroy(e0); return rc; }
+        if (rc) return rc;
         launches += h->launches;
         HIP_TRY(bqp::launch_sqp_loop_u0(batch, nx, n, D->K, s, z, uo, it, cl->steps, t,
                                         sl->Z, sl->iterations, st));
@@ -1003,8 +1023,7 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     }
     HIP_TRY(hipEventRecord(h->ev1, st));
     HIP_TRY(hipEventSynchronize(h->ev1));
-    std::swap(h->ev0, e0);
-    hipEventDestroy(e0);
+    std::swap(h->ev0, e0.e);   // the guard destroys the previous start event
     h->timed = true;
     h->launches = launches;
     return BQP_OK;

@@ -1648,6 +1648,22 @@ __global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
     }
 }
 
+// dynamic LDS above 64 KB needs the kernel attribute, set once per device and instantiation
+// (a process-wide flag left a handle on a second device without it)
+template <bool KL>
+static hipError_t dense_lds_attr(size_t lds) {
+    if (lds <= 64 * 1024) return hipSuccess;
+    static bool done[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev >= 0 && dev < 64 && done[dev]) return hipSuccess;
+    e = hipFuncSetAttribute((const void*)dense_ipm_kernel<KL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            DENSE_LDS_MAX);
+    if (e == hipSuccess && dev >= 0 && dev < 64) done[dev] = true;
+    return e;
+}
+
 hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
     if (a.n > 256 || a.me > 256) return hipErrorInvalidValue;
     if (a.me == 0 && a.n <= SW_NMAX && small_lds_doubles(a.n, a.m) <= SW_LDS_MAX) {
@@ -1658,16 +1674,14 @@ hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
             hipLaunchKernelGGL(dense_wave_kernel<2>, dim3(a.batch), dim3(64), lds, st, a);
     } else {
         const size_t lds = dense_lds_bytes(a.n);
+        if (lds > DENSE_LDS_MAX) return hipErrorInvalidValue;
         if (dense_k_lds(a.n)) {
-            static bool lds_attr = false;
-            if (!lds_attr) {
-                hipError_t e = hipFuncSetAttribute((const void*)dense_ipm_kernel<true>,
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, DENSE_LDS_MAX);
-                if (e != hipSuccess) return e;
-                lds_attr = true;
-            }
+            hipError_t e = dense_lds_attr<true>(lds);
+            if (e != hipSuccess) return e;
             hipLaunchKernelGGL(dense_ipm_kernel<true>, dim3(a.batch), dim3(DT), lds, st, a);
         } else {
+            hipError_t e = dense_lds_attr<false>(lds);
+            if (e != hipSuccess) return e;
             hipLaunchKernelGGL(dense_ipm_kernel<false>, dim3(a.batch), dim3(DT), lds, st, a);
         }
     }

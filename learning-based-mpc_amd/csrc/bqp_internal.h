@@ -54,8 +54,11 @@ struct OcpKernelArgs {
     // short horizons copy the instance's table into its LDS slot, long ones read it from L2
     const double* H_inst;
     // active-set polish (fp64 instantiation, bqp_options.polish): 0 off, 1 after a 0 / -8 exit,
-    // 2 also with a weakly active row
+    // 2 also with a weakly active row.  The solve kernel marks the instances that need it in
+    // pol_need (batch ints); the repair launch (launch_ocp(..., pol = true)) solves those again
+    // and polishes them
     int polish;
+    int* pol_need;
 };
 
 bool ocp_supported(int nx, int nu, int np);
@@ -65,11 +68,11 @@ int ocp_hand_floats(int N, int nx, int nu, int np, int mp);
 int ocp_wave_lds_doubles(int N, int nx, int nu, int np, int mpad, bool fpi, bool lng, bool hpsh,
                          bool bndsh, bool hinst);
 int ocp_pstride(int ns);
-hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
+hipError_t launch_ocp(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st, bool pol = false);
 // fp32 instantiation (bqp_ocp_f32.hip): LDS element count per instance (floats) and launch
 int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad, bool fpi, bool lng,
                              bool hpsh, bool bndsh, bool hinst);
-hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st);
+hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st, bool pol = false);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,
                            hipStream_t st);
@@ -123,6 +126,7 @@ struct LbmpcArgs {
 
 hipError_t launch_nw_oracle(int batch, int q, const double* data, int64_t sdata, const double* xi,
                             double* g, double* dg, double bw, double lam, hipStream_t st);
+bool lbmpc_hess_fits(int n);   // exact-Hessian LDS fits (n <= 127); else Gauss-Newton
 bool lbmpc_supported(int nx, int nu, int np, int n, int q);
 hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st);
 hipError_t launch_lbmpc_normal(const LbmpcArgs& a, hipStream_t st);

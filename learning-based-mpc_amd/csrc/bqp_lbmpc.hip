@@ -680,9 +680,13 @@ hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st) {
     return hipGetLastError();
 }
 
+// the exact-Hessian kernel holds 32 rows of Jr2 tiles and the n x n sum in LDS
+static size_t lbmpc_hess_lds(int n) { return sizeof(double) * ((size_t)32 * n + (size_t)n * n); }
+bool lbmpc_hess_fits(int n) { return n <= 128 && lbmpc_hess_lds(n) <= 160 * 1024 - 64; }
+
 hipError_t launch_lbmpc_hess(const LbmpcArgs& a, hipStream_t st) {
-    const size_t lds = sizeof(double) * ((size_t)32 * a.n + (size_t)a.n * a.n);
-    if (a.n > 128 || lds > 160 * 1024 - 64) return hipErrorInvalidValue;
+    const size_t lds = lbmpc_hess_lds(a.n);
+    if (!lbmpc_hess_fits(a.n)) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)lbmpc_hess_kernel,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -85,15 +85,15 @@ namespace dp {
 #ifndef BQP_EXP_NOSTAGE
 #define BQP_EXP_NOSTAGE 0
 #endif
-#ifndef BQP_POLISH_CODE
-#define BQP_POLISH_CODE BQP_POLISH
-#endif
 #define CMAX_K 100.0
 #define SOC_ALPHA 0.1
 #define DEG_POLISH 1e-10
 #define POL_RHO 2e6
-#define POL_ALM 8
-#define POL_ROUNDS 4
+#define POL_ROUNDS 8
+#define POL_PASS 3
+#define POL_CG 40
+#define POL_CG_SING 1e-2
+#define POL_STAG 0.5
 
 // Cholesky (lower, NxN with N <= 2) with static pivot floor; returns false if not PD.
 // 1/t for the row slacks and multipliers (t > 0 inside the IPM): hardware reciprocal estimate
@@ -180,8 +180,9 @@ enum : int {
     X_PLNEG,     //         min multiplier over the active rows
     X_PLMX,      //         max multiplier over the active rows
     X_PCHG,      //         rows an active-set correction would move
-    X_PDEC,      //         decision (stage wave): 0 step, 1 accept, 2 correct the set, 3 give up
-    X_NXCH = 18
+    X_PDEC,      //         decision (stage wave): 0 pass, 1 accept, 2 correct the set, 3 give up
+    X_CGD,       //         inner step (row wave): 0 CG step, 1 multiplier (AL) step, 2 pass done
+    X_NXCH = 20
 };
 
 // Per-instance LDS layout (in doubles), sized from N at run time.
@@ -308,9 +309,11 @@ __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
 // ==========================================================================================
 // stage wave
 // ==========================================================================================
-template <int NX, int NU, int NP, int SPL>
+template <int NX, int NU, int NP, int SPL, bool POL>
 __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
                                            const real* Hs, int lane, int inst) {
+    // POL: the repair kernel (ocp_polish_kernel) - the same IPM, then the active-set polish
+    constexpr bool PC = POL && BQP_POLISH && !BQP_EXP_NOSTAGE;
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     constexpr int NB = NX + NU;
@@ -457,7 +460,9 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 
     // long horizons: the dynamics residual re_k of stage k = lane + 64 j, recomputed from the
     // iterate (registers) in the operation order of stage_partials instead of kept in LDS
+    bool rez = false;   // polish direction solves: zero dynamics residual (PC only)
     auto re_at = [&](int j, int k, int i) __attribute__((always_inline)) -> real {
+        if constexpr (PC) { if (rez) return real(0); }
         real acc = cb[i] - W[L.xs + (k + 1) * NS + i];
 #pragma unroll
         for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
@@ -1185,8 +1190,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             X[X_STOP] = stop ? 1.0 : 0.0;
             X[X_FEASOK] = (feas <= FEAS_GUARD * (1.0 + bscale)) ? 1.0 : 0.0;
             X[X_FLAG] = (real)flag;
-            X[X_RHO] = POL_RHO * (1.0 + gsA);
-            X[X_TF] = 1e-12 * (1.0 + bscale);
+            if constexpr (PC) {
+                X[X_RHO] = POL_RHO * (1.0 + gsA);
+                X[X_TF] = 1e-12 * (1.0 + bscale);
+            }
         }
         BARRIER();                                        // B2: predictor rhs ready; stop flag
         STAMP(4);
@@ -1209,15 +1216,19 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         STAMP(9);
     }
 
-    // ======================= active-set polish (fp64) ========================================
+    // ======================= active-set polish (fp64, repair kernel only) ====================
     // oracle/cpu_ipm.c polish(): rows with lam > t are equalities, the others are dropped; the
-    // equality-constrained QP is solved by augmented-Lagrangian steps on the Riccati machinery
-    // (D = rho on the active rows, e = rho (C v - b), multipliers nu += rho (C v - b) by the row
-    // wave after each step); negative multipliers leave the set and violated rows enter it.
-    // The polished point replaces the IPM iterate only if it passes the KKT checks.
+    // equality-constrained QP is solved on the Riccati machinery with weight rho on the active
+    // rows (one factorisation per round).  A pass is one augmented-Lagrangian step (the exact
+    // minimiser of the AL for the current multipliers nu) followed by conjugate gradients on nu
+    // for r(nu) = C v(nu) - b = 0 (each CG step one solve with right-hand side C'p and zero
+    // stage / dynamics residuals; plain multiplier steps once a direction is numerically
+    // singular), then nu += rho r.  Negative multipliers leave the set and violated rows enter
+    // it between rounds.  The polished point replaces the IPM iterate only if it passes the KKT
+    // checks.  Barriers T0..T10 pair with the row wave's.
     real polished = 0.0;
     bool pi_kept = false;                                 // pi_out already holds the IPM's pi
-    if constexpr (BQP_POLISH_CODE && !BQP_EXP_NOSTAGE) {
+    if constexpr (PC) {
         BARRIER();                                        // Q0: row wave published max min(t, lam)
         const bool dopol = a.polish > 0 && flag != -2 &&
                            (flag != 1 || (a.polish > 1 && X[X_DEG] > DEG_POLISH)) && isfinite(gsA);
@@ -1241,43 +1252,88 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                 }
             }
             const real tf = 1e-12 * (1.0 + bscale);
-            int rd = 0, jj = 0, dec = 0;
-            bool pfail = false, fresh = false;
-            real va_prev = INFINITY, pst = 0.0;
+            int rd = 0, pass = 0, m = 0, dec = 0;
+            real pst = 0.0;
+            auto zero_stage_res = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int j = 0; j < SPL; ++j) {
+                    const int k = lane + WAVE * j;
+                    if (k > N) continue;
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) {
+                        W[L.rs + k * NS + i] = 0.0;
+                        if constexpr (!LNG) W[L.re + k * NS + i] = 0.0;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NU; ++i) W[L.ru + k * NU + i] = 0.0;
+                }
+                wave_sync();
+            };
             for (;;) {
-                // combine() adds the row terms into the stage residuals in place: they are
-                // re-formed before every use
-                if (!fresh) stage_partials(feasA, gsA);
-                fresh = false;
-                BARRIER();                                // P_B: row tables of (v, nu) ready
+                stage_partials(feasA, gsA);
+                BARRIER();                                // T0: stage vectors, partial residuals
+                BARRIER();                                // T1: row tables of (v, nu), mode m
                 pst = combine();
                 const real va = X[X_PVA];
-                if (pfail) {
-                    dec = 3;
-                } else if (jj == 0 || (jj < POL_ALM && va > 1e-14 * (1.0 + bscale) && va < 0.5 * va_prev)) {
-                    dec = 0;
+                if (m != 1) {
+                    // a new active set: one factorisation per round
+                    dec = factor() ? 0 : 3;
+                    pass = 0;
                 } else {
-                    const bool ok = isfinite(pst) && pst <= a.tol_stat * (1.0 + gsA) && X[X_PVIOL] <= tf &&
-                                    va <= tf && X[X_PLNEG] >= -1e-9 * (1.0 + X[X_PLMX]) && feasA <= tf;
-                    dec = ok ? 1 : ((rd + 1 < POL_ROUNDS && X[X_PCHG] > 0.0) ? 2 : 3);
+                    const bool pok = isfinite(pst) && pst <= a.tol_stat * (1.0 + gsA) && va <= tf;
+                    if (!pok && pass + 1 < POL_PASS) {
+                        dec = 0; ++pass;
+                    } else {
+                        const bool ok = pok && X[X_PVIOL] <= tf &&
+                                        X[X_PLNEG] >= -1e-9 * (1.0 + X[X_PLMX]) && feasA <= tf;
+                        dec = ok ? 1 : ((rd + 1 < POL_ROUNDS && X[X_PCHG] > 0.0) ? 2 : 3);
+                    }
                 }
-                va_prev = (jj == 0) ? INFINITY : va;      // the first step of a round always runs
                 if (lane == 0) X[X_PDEC] = (real)dec;
-                BARRIER();                                // P_C: decision out
+                BARRIER();                                // T2: decision out
                 if (dec == 1 || dec == 3) break;
-                if (dec == 2) { ++rd; jj = 0; va_prev = INFINITY; continue; }
-                if (jj == 0 && !factor()) pfail = true;
-                if (!pfail) {
-                    prep_iter();
-                    solve(L.dsc, L.duc);
-                    dual_dir(L.dsc);
-                    update_stage_dir(1.0, L.dsc, L.duc);
-                    write_state();
-                    stage_partials(feasA, gsA);
-                    fresh = true;
+                if (dec == 2) { ++rd; m = 2; continue; }
+                // AL step from the residuals of (v, nu)
+                prep_iter();
+                solve(L.dsc, L.duc);
+                dual_dir(L.dsc);
+                update_stage_dir(1.0, L.dsc, L.duc);
+                write_state();
+                BARRIER();                                // T3: v after the AL step
+                BARRIER();                                // T4: row wave: CG start, decision
+                for (;;) {
+                    const int cgd = (int)X[X_CGD];
+                    if (cgd == 2) break;
+                    if (cgd == 0) {
+                        // CG direction: right-hand side C'p (the row wave's tables)
+                        zero_stage_res();
+                        rez = true;
+                        prep_iter();
+                        solve(L.dsc, L.duc);
+                        dual_dir(L.dsc);
+                        rez = false;
+                        BARRIER();                        // T5: direction in (dsc, duc)
+                        BARRIER();                        // T6: row wave: alpha, next step
+                        const real al = X[X_ALPHA];
+                        if (al != 0.0) update_stage_dir(al, L.dsc, L.duc);
+                    } else {
+                        // multiplier step nu += rho r, then the AL step
+                        write_state();
+                        stage_partials(feasA, gsA);
+                        BARRIER();                        // T7: v, partial residuals
+                        BARRIER();                        // T8: row tables of mode 1
+                        combine();
+                        prep_iter();
+                        solve(L.dsc, L.duc);
+                        dual_dir(L.dsc);
+                        update_stage_dir(1.0, L.dsc, L.duc);
+                        write_state();
+                        BARRIER();                        // T9: v after the AL step
+                        BARRIER();                        // T10: row wave: |r|, next step
+                    }
                 }
-                ++jj;
-                BARRIER();                                // P_D: the stepped stage vectors
+                write_state();
+                m = 1;
             }
             if (dec == 1) {
                 polished = 1.0;
@@ -1375,9 +1431,10 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 // ==========================================================================================
 // row wave
 // ==========================================================================================
-template <int NX, int NU, int NP, int BPL, int RPL>
+template <int NX, int NU, int NP, int BPL, int RPL, bool POL>
 __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
                                          const real* Fs, const real* Sh, int lane, int inst) {
+    constexpr bool PC = POL && BQP_POLISH && !BQP_EXP_NOROW;
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     constexpr int NB = NX + NU;          // box slots per stage: x then u, each [upper, lower]
@@ -2111,9 +2168,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     };
 
     // ======================= active-set polish (fp64): row side ==============================
-    if constexpr (BQP_POLISH_CODE && !BQP_EXP_NOROW) {
-        // max over rows of min(t, lam): a weakly active row keeps both ~ sqrt(mu) at the exit
-        real dg = 0.0;
+    // max over rows of min(t, lam): a weakly active row keeps both ~ sqrt(mu) at the exit
+    real dg = 0.0;
+    if (BQP_POLISH && a.polish > 1) {
 #pragma unroll
         for (int b = 0; b < BPL; ++b)
             if (bpres(b)) dg = fmax(dg, fmin(tx[b], lx[b]));
@@ -2121,6 +2178,17 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         for (int q = 0; q < RPL; ++q)
             if (prow(q)) dg = fmax(dg, fmin(tp[q], lp[q]));
         dg = wmax(dg);
+    }
+    if constexpr (!POL) {
+        // solve kernel: instances that need the polish are marked for the repair launch
+        // (ocp_polish_kernel), which solves them again and polishes; the solve kernel itself
+        // carries no polish state
+        if (BQP_POLISH && a.pol_need && lane == 0) {
+            const int flag = (int)X[X_FLAG];
+            a.pol_need[inst] = (a.polish > 0 && flag != -2 && (flag != 1 || (a.polish > 1 && dg > DEG_POLISH))) ? 1 : 0;
+        }
+    }
+    if constexpr (PC) {
         if (lane == 0) X[X_DEG] = dg;
         BARRIER();                                        // Q0
         const int flag = (int)X[X_FLAG];
@@ -2131,6 +2199,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             // the IPM's multipliers go out now (the fall-back); the row state is dead after this
             out_duals(lx, lp);
             const real rho = X[X_RHO], tf = X[X_TF];
+            const real tol14 = 0.01 * tf;                 // 1e-14 (1 + |data|)
             unsigned bact = 0, pact = 0;                 // rows taken as equalities
             real nb[BPL], npq[RPL];                       // their multipliers (0 on dropped rows)
             real lmx_r = 0.0;
@@ -2284,13 +2353,67 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 }
                 wave_sync();
             };
-            // one call site (mode at run time): a single inlined copy of pol_tables (C2
-            // instantiation: 104 -> 80 B/lane of scratch)
+            // conjugate gradients on the multipliers of the active rows (oracle/cpu_ipm.c
+            // polish()): residual r = C v - b and direction p per active row, 0 elsewhere
+            real crb[BPL], cpb[BPL], crq[RPL], cpq[RPL];
+            real rr = 0.0, va_prev = INFINITY;
+            // the direction solve's tables: e = p on the active rows (box rhs terms, Fp'p)
+            auto dir_tables = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int pv = 0; pv < BPL / 2; ++pv) {
+                    if (!binrange(2 * pv)) continue;
+                    if constexpr (LNG) {
+                        W[L.ebox + lane + WAVE * pv] = cpb[2 * pv] - cpb[2 * pv + 1];
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) W[L.ebox + brow(2 * pv + h)] = cpb[2 * pv + h];
+                    }
+                }
+                real red[NV];
+#pragma unroll
+                for (int c = 0; c < NV; ++c) red[c] = 0.0;
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    const int r = lane + WAVE * q;
+                    if (r >= mp) continue;
+#pragma unroll
+                    for (int c = 0; c < NV; ++c) red[c] += Fs[c * mpad + r] * cpq[q];
+                }
+                const real tot = wsum_t(red, lane);
+                if (lane < NV) W[L.gpe + lane] = tot;
+            };
+            // active-row constraint values of the stage vectors in LDS: max |C v - b|
+            auto act_res = [&](bool keep) __attribute__((always_inline)) -> real {
+                real va = 0.0;
+#pragma unroll
+                for (int b = 0; b < BPL; ++b) {
+                    real ri = 0.0;
+                    if ((bact >> b) & 1u) {
+                        const real v = bvar(b, L.xs, L.xu);
+                        const real bd = bndp[brow(b)];
+                        ri = (b & 1) == 0 ? v - bd : -v + bd;
+                    }
+                    if (keep) crb[b] = ri;
+                    va = fmax(va, fabs(ri));
+                }
+                real vp[NV];
+                load_v(vp, L.xs, L.xu);
+#pragma unroll
+                for (int q = 0; q < RPL; ++q) {
+                    const int r = lane + WAVE * q;
+                    real ri = 0.0;
+                    if (((pact >> q) & 1u) && r < mp) ri = fdot(r, vp) - hpi[r];
+                    if (keep) crq[q] = ri;
+                    va = fmax(va, fabs(ri));
+                }
+                return wmax(va);
+            };
             int mode = 0;
             for (;;) {
+                BARRIER();                                // T0
                 pol_tables(mode);
-                BARRIER();                                // P_B
-                BARRIER();                                // P_C
+                BARRIER();                                // T1
+                BARRIER();                                // T2
                 const int dec = (int)X[X_PDEC];
                 if (dec == 1) {
 #pragma unroll
@@ -2302,7 +2425,98 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 }
                 if (dec == 3) break;
                 if (dec == 2) { mode = 2; continue; }
-                BARRIER();                                // P_D
+                BARRIER();                                // T3: v after the AL step
+                {
+                    // CG start: r = p = C v - b on the active rows
+                    real va = act_res(true), pr = 0.0;
+#pragma unroll
+                    for (int b = 0; b < BPL; ++b) { cpb[b] = crb[b]; pr += crb[b] * crb[b]; }
+#pragma unroll
+                    for (int q = 0; q < RPL; ++q) { cpq[q] = crq[q]; pr += crq[q] * crq[q]; }
+                    rr = wsum(pr);
+                    va_prev = INFINITY;
+                    dir_tables();
+                    if (lane == 0) X[X_CGD] = (va > tol14 && isfinite(rr) && POL_CG > 0) ? 0.0 : 2.0;
+                }
+                BARRIER();                                // T4
+                for (int j = 0;; ++j) {
+                    const int cgd = (int)X[X_CGD];
+                    if (cgd == 2) break;
+                    if (cgd == 0) {
+                        BARRIER();                        // T5: direction in (dsc, duc)
+                        // M p = -C dv on the active rows; alpha = r'r / p'Mp
+                        real mpb[BPL], mpq[RPL];
+                        real pq = 0.0, pp = 0.0;
+#pragma unroll
+                        for (int b = 0; b < BPL; ++b) {
+                            real c = 0.0;
+                            if ((bact >> b) & 1u) {
+                                const real dv = bvar(b, L.dsc, L.duc);
+                                c = (b & 1) ? dv : -dv;
+                            }
+                            mpb[b] = c;
+                            pq += cpb[b] * c; pp += cpb[b] * cpb[b];
+                        }
+                        real dvp[NV];
+                        load_v(dvp, L.dsc, L.duc);
+#pragma unroll
+                        for (int q = 0; q < RPL; ++q) {
+                            const int r = lane + WAVE * q;
+                            real c = 0.0;
+                            if (((pact >> q) & 1u) && r < mp) c = -fdot(r, dvp);
+                            mpq[q] = c;
+                            pq += cpq[q] * c; pp += cpq[q] * cpq[q];
+                        }
+                        real red2[2] = {pq, pp};
+                        const real t2 = wsum_t(red2, lane);
+                        pq = rl(t2, 0); pp = rl(t2, 1);
+                        real al = 0.0, va = INFINITY;
+                        int nxt;
+                        if (!(pq * rho > POL_CG_SING * pp)) {
+                            // numerically singular direction (nearly dependent active rows):
+                            // plain multiplier steps from here
+                            nxt = (j + 1 < POL_CG) ? 1 : 2;
+                        } else {
+                            al = rr / pq;
+                            real rn = 0.0;
+                            va = 0.0;
+#pragma unroll
+                            for (int b = 0; b < BPL; ++b) {
+                                nb[b] += al * cpb[b];
+                                crb[b] -= al * mpb[b];
+                                rn += crb[b] * crb[b]; va = fmax(va, fabs(crb[b]));
+                            }
+#pragma unroll
+                            for (int q = 0; q < RPL; ++q) {
+                                npq[q] += al * cpq[q];
+                                crq[q] -= al * mpq[q];
+                                rn += crq[q] * crq[q]; va = fmax(va, fabs(crq[q]));
+                            }
+                            rn = wsum(rn);
+                            va = wmax(va);
+                            const real be = rn / rr;
+#pragma unroll
+                            for (int b = 0; b < BPL; ++b) cpb[b] = crb[b] + be * cpb[b];
+#pragma unroll
+                            for (int q = 0; q < RPL; ++q) cpq[q] = crq[q] + be * cpq[q];
+                            rr = rn;
+                            dir_tables();
+                            nxt = (j + 1 < POL_CG && va > tol14 && isfinite(rr)) ? 0 : 2;
+                        }
+                        if (lane == 0) { X[X_ALPHA] = al; X[X_CGD] = (real)nxt; }
+                        BARRIER();                        // T6
+                    } else {
+                        BARRIER();                        // T7: v, partial residuals
+                        pol_tables(1);
+                        BARRIER();                        // T8
+                        BARRIER();                        // T9: v after the AL step
+                        const real va = act_res(false);
+                        const int nxt = (va >= POL_STAG * va_prev) ? 2 : ((j + 1 < POL_CG && va > tol14) ? 1 : 2);
+                        va_prev = va;
+                        if (lane == 0) X[X_CGD] = (real)nxt;
+                        BARRIER();                        // T10
+                    }
+                }
                 mode = 1;
             }
             STAMP_STORE(16);
@@ -2317,8 +2531,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 // ==========================================================================================
 // kernel: QPB instances per workgroup, waves [0, QPB) stage waves, [QPB, 2 QPB) row waves
 // ==========================================================================================
-template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
-__global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernelArgs a) {
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL, bool POL>
+__device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -2327,6 +2541,13 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int qpb = a.wpb;
+    if constexpr (POL) {
+        // repair launch: a workgroup none of whose instances the solve launch marked leaves
+        // before staging the shared tables
+        const int i0 = blockIdx.x * a.wpb + ((threadIdx.x >> 6) % a.wpb);
+        const bool need = i0 < a.batch && a.pol_need[i0] != 0;
+        if (!__syncthreads_or(need)) return;
+    }
     // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
     if constexpr (SPL == 2) {
         // mixed mode, cold retry launch: a workgroup none of whose instances needs the retry
@@ -2370,7 +2591,8 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
     const int slot = rowwave ? wid - qpb : wid;
     const int inst = blockIdx.x * qpb + slot;
     if (inst >= a.batch) return;       // both waves of an empty slot leave together
-    if (SPL == 2 && a.redo_flag &&
+    if (POL && a.pol_need[inst] == 0) return;   // repair launch: nothing to polish here
+    if (!POL && SPL == 2 && a.redo_flag &&
         !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
         return;                        // mixed mode, cold retry launch: nothing to redo here
     const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, LNG && a.sh_hp >= 0,
@@ -2394,9 +2616,20 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
         wave_sync();
     }
     if (!rowwave)
-        stage_wave<NX, NU, NP, SPL>(a, W, L, Hs, lane, inst);
+        stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
     else
-        row_wave<NX, NU, NP, BPL, RPL>(a, W, L, Fs, lds, lane, inst);
+        row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+}
+
+// the solve kernel (no polish code: the main loop keeps its register budget) and the repair
+// kernel (same IPM, then the active-set polish) over the instances the solve kernel marked
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
+__global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernelArgs a) {
+    ocp_body<NX, NU, NP, SPL, RPL, BPL, false>(a);
+}
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
+__global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_polish_kernel(OcpKernelArgs a) {
+    ocp_body<NX, NU, NP, SPL, RPL, BPL, true>(a);
 }
 
 }  // namespace dp / sp
@@ -2419,11 +2652,12 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernel
 #endif
 
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
-static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipStream_t st) {
+static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipStream_t st, bool pol) {
 #ifdef BQP_F32
+    (void)pol;
     auto k = sp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
 #else
-    auto k = dp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
+    auto k = pol ? dp::ocp_polish_kernel<NX, NU, NP, SPL, RPL, BPL> : dp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
 #endif
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -2437,43 +2671,43 @@ static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipSt
 // layout per lane (SPL) is tied to it: SPL 1 (N < 64) -> 4 (<= 256 rows) or 10 (<= 640),
 // SPL 2 -> 16 (<= 1024) or 20 (<= 1280)
 template <int NX, int NU, int NP, int SPL, int BPL>
-static hipError_t launch_rpl(const OcpKernelArgs& a, int rpl, int blocks, size_t lds, hipStream_t st) {
+static hipError_t launch_rpl(const OcpKernelArgs& a, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
     switch (rpl) {
-        case 1: return launch_t<NX, NU, NP, SPL, 1, BPL>(a, blocks, lds, st);
-        case 4: return launch_t<NX, NU, NP, SPL, 4, BPL>(a, blocks, lds, st);
-        case 10: return launch_t<NX, NU, NP, SPL, 10, BPL>(a, blocks, lds, st);
-        case 16: return launch_t<NX, NU, NP, SPL, 16, BPL>(a, blocks, lds, st);
+        case 1: return launch_t<NX, NU, NP, SPL, 1, BPL>(a, blocks, lds, st, pol);
+        case 4: return launch_t<NX, NU, NP, SPL, 4, BPL>(a, blocks, lds, st, pol);
+        case 10: return launch_t<NX, NU, NP, SPL, 10, BPL>(a, blocks, lds, st, pol);
+        case 16: return launch_t<NX, NU, NP, SPL, 16, BPL>(a, blocks, lds, st, pol);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int NX, int NU, int NP>
-static hipError_t launch_spl(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st) {
+static hipError_t launch_spl(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
     const int nbr = (a.N + 1) * 2 * (NX + NU);
-    if (spl == 1 && nbr <= 4 * WAVE) return launch_rpl<NX, NU, NP, 1, 4>(a, rpl, blocks, lds, st);
-    if (spl == 1 && nbr <= 10 * WAVE) return launch_rpl<NX, NU, NP, 1, 10>(a, rpl, blocks, lds, st);
-    if (spl == 2 && nbr <= 16 * WAVE) return launch_rpl<NX, NU, NP, 2, 16>(a, rpl, blocks, lds, st);
-    if (spl == 2 && nbr <= 20 * WAVE) return launch_rpl<NX, NU, NP, 2, 20>(a, rpl, blocks, lds, st);
+    if (spl == 1 && nbr <= 4 * WAVE) return launch_rpl<NX, NU, NP, 1, 4>(a, rpl, blocks, lds, st, pol);
+    if (spl == 1 && nbr <= 10 * WAVE) return launch_rpl<NX, NU, NP, 1, 10>(a, rpl, blocks, lds, st, pol);
+    if (spl == 2 && nbr <= 16 * WAVE) return launch_rpl<NX, NU, NP, 2, 16>(a, rpl, blocks, lds, st, pol);
+    if (spl == 2 && nbr <= 20 * WAVE) return launch_rpl<NX, NU, NP, 2, 20>(a, rpl, blocks, lds, st, pol);
     return hipErrorInvalidValue;
 }
 
-hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st);
-hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st);
+hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol);
+hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol);
 
 #if BQP_FAM_MG
-hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st) {
+hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
 #ifdef BQP_ISA_ONLY_MG10
     // codegen inspection build (make isa): the MG N<64, 616-row instance only
-    if (spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st);
+    if (spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st, pol);
     return hipErrorInvalidValue;
 #else
-    return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st);
+    return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st, pol);
 #endif
 }
 #endif
 #if BQP_FAM_DI && !defined(BQP_ISA_ONLY_MG10)
-hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st) {
-    return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st);
+hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
+    return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st, pol);
 }
 #endif
 
@@ -2517,7 +2751,7 @@ int BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(int N, int nx, int nu, int np, int mp
 #endif
 }
 
-hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st) {
+hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st, bool pol) {
     const int spl = (a.N + 1 <= 64) ? 1 : 2;
     const int rpl = ocp_rpl_for(a.mp);
     const int blocks = (a.batch + a.wpb - 1) / a.wpb;
@@ -2527,9 +2761,9 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
                                                                                       BQP_LNG_OK && spl == 2 && a.sh_hp >= 0,
                                                                                       BQP_LNG_OK && spl == 2 && a.sh_bnd >= 0,
                                                                                       a.H_inst != nullptr));
-    if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st);
+    if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st, pol);
 #ifndef BQP_ISA_ONLY_MG10
-    if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st);
+    if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st, pol);
 #endif
     return hipErrorInvalidValue;
 }

@@ -33,9 +33,30 @@
 #ifndef DEG_POLISH
 #define DEG_POLISH 1e-10  /* polish = 2: also a converged iterate with max_i min(t_i, lam_i) > this */
 #endif
-#define POL_RHO 2e6       /* polish weight rho = POL_RHO (1 + |H v + g|_inf)                      */
-#define POL_ALM 8         /* augmented-Lagrangian iterations per polish round (at most)           */
-#define POL_ROUNDS 4      /* active-set corrections                                               */
+#ifndef POL_RHO
+#define POL_RHO 2e6
+#endif
+//       /* polish weight rho = POL_RHO (1 + |H v + g|_inf)                      */
+#ifndef POL_ALM
+#define POL_ALM 8
+#endif
+//         /* augmented-Lagrangian iterations per polish round (at most)           */
+#ifndef POL_STAG
+#define POL_STAG 0.5
+#endif
+#ifndef POL_CG_SING
+#define POL_CG_SING 1e-2
+#endif
+#ifndef POL_PASS
+#define POL_PASS 3
+#endif
+#ifndef POL_CG
+#define POL_CG 40
+#endif
+#ifndef POL_ROUNDS
+#define POL_ROUNDS 8
+#endif
+//      /* active-set corrections                                               */
 
 typedef struct {
     int nx, nu, np, ns, nv, N, mp, kp;
@@ -64,6 +85,7 @@ typedef struct {
     int pol;
     double cmax;   /* max_i t_i lam_i of the last residuals() */
     double *wx, *wu, *wp;
+    double *cgr, *cgp;   /* polish: CG residual and direction over all rows [x | u | poly] */
 } work_t;
 
 static int perm_of(const prob_t* P, int i) {
@@ -616,6 +638,8 @@ static double comp_s2(const prob_t* P, work_t* W) {
     }                                                                                           \
     for (int i = 0; i < mp; ++i) { BP; }
 
+static double poly_fdv(const prob_t* P, const work_t* W, int r);
+
 static int polish(const prob_t* P, work_t* W, double bs, double rho, double* kkt_out) {
     const int N = P->N, nx = P->nx, ns = P->ns;
     const int nxr = (N + 1) * nx * 2, nur = N * P->nu * 2, mp = P->mp;
@@ -643,20 +667,104 @@ static int polish(const prob_t* P, work_t* W, double bs, double rho, double* kkt
     for (int rd = 0; rd < POL_ROUNDS && !ok; ++rd) {
         residuals(P, W, &stat, &feas, &cs, &mc, &gs);
         if (factor(P, W)) break;
-        double va_prev = INFINITY;
-        for (int j = 0; j < POL_ALM; ++j) {
-            if (j > 0) residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+        /* one augmented-Lagrangian step: v <- argmin_v AL(v, nu) (the Newton step is exact on the
+         * quadratic AL), then conjugate gradients on the multipliers of the active rows for
+         * r(nu) = C v(nu) - b = 0: r is affine in nu with dr/dnu = -M, M = C (H + rho C'C)^{-1} C'
+         * SPD, so CG converges in a few steps where the plain multiplier update nu += rho r
+         * contracts by 1 / (1 + rho sigma) per step - slow on nearly dependent active rows
+         * (a state box row held over consecutive stages: C4 instance 28 at N = 80, sigma_min of
+         * the active rows 6.5e-5).  Each CG step is one solve on the same
+         * factorisation with right-hand side C'p (stage residuals and dynamics residual zero). */
+        /* POL_PASS passes of [AL step + CG]: the AL step from the exact residuals is an iterative
+         * refinement of the stationarity, which the factorisation with rho ~ 1e9 resolves to
+         * ~eps rho |C v| per solve (C4 instances 20695 / 63175 at N = 100) */
+        for (int pass = 0; pass < POL_PASS; ++pass) {
+            if (pass > 0) residuals(P, W, &stat, &feas, &cs, &mc, &gs);
             prep_iter(P, W);
-            solve_kkt(P, W, W->dtx, W->dtu, W->dtp);    /* complementarity rhs unused */
+            solve_kkt(P, W, W->dtx, W->dtu, W->dtp);
             for (int i = 0; i < S; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
             for (int i = 0; i < U; ++i) W->u[i] += W->du[i];
             residuals(P, W, &stat, &feas, &cs, &mc, &gs);
-            double va = 0.0;
-            FOR_ROWS({ W->lx[i] += W->wx[i] * W->rix[i]; if (W->wx[i] > 0) va = fmax(va, fabs(W->rix[i])); },
-                     { W->lu[i] += W->wu[i] * W->riu[i]; if (W->wu[i] > 0) va = fmax(va, fabs(W->riu[i])); },
-                     { W->lp[i] += W->wp[i] * W->rip[i]; if (W->wp[i] > 0) va = fmax(va, fabs(W->rip[i])); })
-            if (va <= 1e-14 * (1.0 + bs) || va >= 0.5 * va_prev) break;
-            va_prev = va;
+            {
+                double* cr = W->cgr;                      /* r on the active rows, 0 elsewhere */
+                double* cp = W->cgp;
+                double rr = 0.0, va = 0.0;
+                FOR_ROWS({ cr[i] = W->wx[i] > 0 ? W->rix[i] : 0.0; },
+                         { cr[nxr + i] = W->wu[i] > 0 ? W->riu[i] : 0.0; },
+                         { cr[nxr + nur + i] = W->wp[i] > 0 ? W->rip[i] : 0.0; })
+                for (int i = 0; i < nxr + nur + mp; ++i) { cp[i] = cr[i]; rr += cr[i] * cr[i]; va = fmax(va, fabs(cr[i])); }
+                int cg = 1;
+                double va_prev = INFINITY;
+                for (int j = 0; j < POL_CG && va > 1e-14 * (1.0 + bs) && isfinite(rr); ++j) {
+                    if (!cg) {
+                        /* plain multiplier step (nearly dependent active rows: M numerically
+                         * singular); the AL solve from the new nu */
+                        residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+                        FOR_ROWS({ W->lx[i] += W->wx[i] * W->rix[i]; }, { W->lu[i] += W->wu[i] * W->riu[i]; },
+                                 { W->lp[i] += W->wp[i] * W->rip[i]; })
+                        residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+                        prep_iter(P, W);
+                        solve_kkt(P, W, W->dtx, W->dtu, W->dtp);
+                        for (int i = 0; i < S; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
+                        for (int i = 0; i < U; ++i) W->u[i] += W->du[i];
+                        residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+                        va = 0.0;
+                        FOR_ROWS({ if (W->wx[i] > 0) va = fmax(va, fabs(W->rix[i])); },
+                                 { if (W->wu[i] > 0) va = fmax(va, fabs(W->riu[i])); },
+                                 { if (W->wp[i] > 0) va = fmax(va, fabs(W->rip[i])); })
+                        if (getenv("CPU_IPM_TRACE")) fprintf(stderr, "   alm %d va %.3e\n", j, va);
+                        if (va >= POL_STAG * va_prev) break;
+                        va_prev = va;
+                        continue;
+                    }
+                    /* direction solve: e = p on the active rows (rix = p / rho), zero stage residuals */
+                    memset(W->rs, 0, sizeof(double) * S); memset(W->ru, 0, sizeof(double) * U);
+                    memset(W->re, 0, sizeof(double) * N * ns);
+                    FOR_ROWS({ W->rix[i] = cp[i] / rho; }, { W->riu[i] = cp[nxr + i] / rho; },
+                             { W->rip[i] = cp[nxr + nur + i] / rho; })
+                    prep_iter(P, W);
+                    solve_kkt(P, W, W->dtx, W->dtu, W->dtp);
+                    /* M p = -C dv on the active rows; alpha = r'r / p'Mp */
+                    double pq = 0.0, pp = 0.0;
+                    FOR_ROWS({ const double c_ = (i & 1) ? W->ds[k_ * ns + xi_] : -W->ds[k_ * ns + xi_];
+                               W->dtx[i] = W->wx[i] > 0 ? c_ : 0.0; pq += cp[i] * W->dtx[i]; },
+                             { const double c_ = (i & 1) ? W->du[i / 2] : -W->du[i / 2];
+                               W->dtu[i] = W->wu[i] > 0 ? c_ : 0.0; pq += cp[nxr + i] * W->dtu[i]; },
+                             { W->dtp[i] = W->wp[i] > 0 ? -poly_fdv(P, W, i) : 0.0; pq += cp[nxr + nur + i] * W->dtp[i]; })
+                    for (int i = 0; i < nxr + nur + mp; ++i) pp += cp[i] * cp[i];
+                    /* the eigenvalues of M lie in (0, 1/rho): a Rayleigh quotient below 1e-8 / rho is a
+                     * numerically singular direction (dependent rows) - plain multiplier steps from here */
+                    if (!(pq * rho > POL_CG_SING * pp)) {
+                        cg = 0;
+                        if (getenv("CPU_IPM_TRACE")) fprintf(stderr, "   cg %d singular (rayleigh rho %.3e)\n", j, pq * rho / pp);
+                        continue;
+                    }
+                    const double al = rr / pq;
+                    for (int i = 0; i < S; ++i) { W->s[i] += al * W->ds[i]; W->pi[i] += al * W->dpi[i]; }
+                    for (int i = 0; i < U; ++i) W->u[i] += al * W->du[i];
+                    double rn = 0.0;
+                    va = 0.0;
+                    FOR_ROWS({ W->lx[i] += al * cp[i]; cr[i] -= al * W->dtx[i]; },
+                             { W->lu[i] += al * cp[nxr + i]; cr[nxr + i] -= al * W->dtu[i]; },
+                             { W->lp[i] += al * cp[nxr + nur + i]; cr[nxr + nur + i] -= al * W->dtp[i]; })
+                    for (int i = 0; i < nxr + nur + mp; ++i) { rn += cr[i] * cr[i]; va = fmax(va, fabs(cr[i])); }
+                    const double be = rn / rr;
+                    for (int i = 0; i < nxr + nur + mp; ++i) cp[i] = cr[i] + be * cp[i];
+                    rr = rn;
+                    if (getenv("CPU_IPM_TRACE")) fprintf(stderr, "   cg %d va %.3e alpha*rho^-1 %.3e\n", j, va, al / rho);
+                }
+                /* the Lagrangian multipliers of v(nu): nu + rho r (exact stationarity of the AL) */
+                residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+                FOR_ROWS({ W->lx[i] += W->wx[i] * W->rix[i]; }, { W->lu[i] += W->wu[i] * W->riu[i]; },
+                         { W->lp[i] += W->wp[i] * W->rip[i]; })
+            }
+            residuals(P, W, &stat, &feas, &cs, &mc, &gs);
+            double va2 = 0.0;
+            FOR_ROWS({ if (W->wx[i] > 0) va2 = fmax(va2, fabs(W->rix[i])); },
+                     { if (W->wu[i] > 0) va2 = fmax(va2, fabs(W->riu[i])); },
+                     { if (W->wp[i] > 0) va2 = fmax(va2, fabs(W->rip[i])); })
+            if (getenv("CPU_IPM_TRACE")) fprintf(stderr, "  pass %d stat %.3e va %.3e\n", pass, stat, va2);
+            if (stat <= 1e-8 * (1.0 + gs) && va2 <= 1e-12 * (1.0 + bs)) break;
         }
         residuals(P, W, &stat, &feas, &cs, &mc, &gs);
         double va = 0.0, lneg = 0.0, lmx = 0.0;
@@ -822,6 +930,9 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         residuals(P, W, &stat, &feas, &cs, &mc, &gs);
         mu = cs / (mc > 0 ? mc : 1);
         if (stat <= op->tol_stat * (1.0 + gs) && feas <= op->tol_feas * (1.0 + bs) && mu <= op->tol_comp && W->cmax <= CMAX_K * op->tol_comp) { flag = 1; break; }
+        if (getenv("CPU_IPM_ITER"))
+            fprintf(stderr, "it %2d stat %.3e (tol %.3e) feas %.3e mu %.3e cmax %.3e gs %.3e\n", it, stat,
+                    op->tol_stat * (1.0 + gs), feas, mu, W->cmax, gs);
         if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
         if (mu > MU_BLOWUP * mu_min && feas > FEAS_GUARD * (1.0 + bs)) { flag = -2; break; }
         if (mu < mu_min) mu_min = mu;
@@ -958,6 +1069,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.itx = alloc0((N + 1) * nx * 2); W.ilx = alloc0((N + 1) * nx * 2);
         W.itu = alloc0(N * nu * 2); W.ilu = alloc0(N * nu * 2); W.itp = alloc0(mp); W.ilp = alloc0(mp);
         W.wx = alloc0((N + 1) * nx * 2); W.wu = alloc0(N * nu * 2); W.wp = alloc0(mp);
+        W.cgr = alloc0((N + 1) * nx * 2 + N * nu * 2 + mp); W.cgp = alloc0((N + 1) * nx * 2 + N * nu * 2 + mp);
         prob_t P;
         memset(&P, 0, sizeof(P));
         P.nx = nx; P.nu = nu; P.np = np; P.ns = ns; P.nv = nv; P.N = N; P.mp = mp;
@@ -1030,7 +1142,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Phit); free(W.Ktab); free(W.Rinv); free(W.p);
         free(W.qs); free(W.qu); free(W.wv); free(W.cw); free(W.qt); free(W.qh); free(W.kff); free(W.f); free(W.Dx);
         free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
-        free(W.ilp); free(W.wx); free(W.wu); free(W.wp);
+        free(W.ilp); free(W.wx); free(W.wu); free(W.wp); free(W.cgr); free(W.cgp);
     }
     return err;
 }

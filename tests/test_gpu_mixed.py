@@ -93,11 +93,14 @@ def test_mixed_duals_kkt(mg, term_set, handle):
 
 
 def test_mixed_status_cold_restart(mg, term_set, handle):
-    """perturbed models (config C4 generator): instances the fp32 phase ends as infeasible or
-    failed restart in fp64 from the fp64 initial point, so the exit flags are the fp64 solve's
-    and the converged first moves agree"""
+    """perturbed models (config C4 generator, 512 models) at N = 80: the fp64 solve and the mixed
+    mode both end every model 1 or -2, equal to the exact LDP/NNLS classification
+    (tests/golden/c4_mixed_N80.npz, oracle/make_c4_fixture.py --mixed), first moves and theta
+    within 1e-8 of z*; model 28 (strictly feasible, LP margin 0.115, where the round-3 polish left
+    -8: VERDICT r3 item 1) solved to z* within 1e-8 over the whole horizon"""
     import bqp
     d = golden('mg_design.npz')
+    ex = golden('c4_mixed_N80.npz')
     rng = np.random.default_rng(4)
     n = 512
     E = rng.standard_normal((n, 4, 4))
@@ -110,13 +113,19 @@ def test_mixed_status_cold_restart(mg, term_set, handle):
                   term_set[0], term_set[1], N=80)
     r64 = lm.solve(dx, A=A, B=Bm, handle=handle)
     rmx = lm.solve(dx, A=A, B=Bm, handle=handle, precision=2)
-    print('mixed C4 sample: flags fp64 %s, mixed %s' % (np.unique(r64.exitflag, return_counts=True),
-                                                       np.unique(rmx.exitflag, return_counts=True)))
-    assert (r64.exitflag == -2).any()
-    # every status of the fp64 solve is reproduced, except that the mixed mode may converge
-    # where the fp64 solve ends numerically (-8) on a marginal model
-    same = rmx.exitflag == r64.exitflag
-    assert (same | ((r64.exitflag == -8) & (rmx.exitflag == 1))).all()
-    assert same.mean() > 0.99
+    print('mixed C4 sample: flags fp64 %s, mixed %s; polished fp64 %d'
+          % (np.unique(r64.exitflag, return_counts=True), np.unique(rmx.exitflag, return_counts=True),
+             int(r64.polished.sum())))
+    assert np.array_equal(r64.exitflag == 1, ex['feasible'])
+    assert set(np.unique(r64.exitflag)) <= {1, -2}
+    assert np.array_equal(rmx.exitflag, r64.exitflag)
+    zi = ex['z_idx']
+    for r in (r64, rmx):
+        z = np.concatenate([r.u.reshape(n, -1), r.theta], axis=1)[zi]
+        err = np.abs(z - ex['z_star'])
+        assert err[:, 0].max() < 1e-8 and err[:, -1].max() < 1e-8, (err[:, 0].max(), err[:, -1].max())
+        k28 = int(np.flatnonzero(zi == 28)[0])
+        sc = max(1.0, np.abs(ex['z_star'][k28]).max())
+        assert err[k28].max() / sc < 1e-8, err[k28].max()
     ok = r64.exitflag == 1
     assert np.abs(rmx.du0[ok] - r64.du0[ok]).max() < 1e-8

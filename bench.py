@@ -155,15 +155,26 @@ def cpu_reference(prob, sample, threads, timed):
     kw1 = {k: v[:n1] for k, v in kw.items()}
     t0 = time.perf_counter(); cpu_ref.solve(ocp, X[:n1], threads=1, **kw1); t1 = time.perf_counter()
     single = n1 / (t1 - t0)
-    reps = max(1, int(np.ceil(single * threads * 1.0 / len(X))))
-    kwa = {k: np.concatenate([v] * reps) for k, v in kw.items()}
-    Xa = np.concatenate([X] * reps)
-    t0 = time.perf_counter(); cpu_ref.solve(ocp, Xa, threads=threads, **kwa); t1 = time.perf_counter()
-    allc = len(Xa) / (t1 - t0)
-    return dict(value=round(allc, 1), unit='QP-steps/s', cores=threads, kind='port',
-                single_core=round(single, 1),
-                sample='%d QPs all-core + %d single-core of the same workload; oracle/cpu_ipm.c '
-                       '(same IPM, fp64, -O3 -march=native, OpenMP)' % (len(Xa), n1)), kref
+
+    def timed_run(nthr):
+        # about one second of work on nthr threads (at least 64 QPs per thread)
+        want = max(64 * nthr, int(single * nthr * 1.0))
+        reps = max(1, int(np.ceil(want / len(X))))
+        kwa = {k: np.concatenate([v] * reps) for k, v in kw.items()}
+        Xa = np.concatenate([X] * reps)
+        t0 = time.perf_counter(); cpu_ref.solve(ocp, Xa, threads=nthr, **kwa); t1 = time.perf_counter()
+        return len(Xa) / (t1 - t0), len(Xa)
+
+    # every host core of the box (the affinity mask), and beside it the per-GPU
+    # share of the box's cores (OMP_NUM_THREADS) that the driver sets
+    present = len(os.sched_getaffinity(0))
+    allc, nall = timed_run(present)
+    share, nsh = (allc, nall) if threads == present else timed_run(threads)
+    return dict(value=round(allc, 1), unit='QP-steps/s', cores=present, kind='port',
+                single_core=round(single, 1), share_value=round(share, 1), share_cores=threads,
+                sample='%d QPs on all %d host cores, %d QPs on the %d-core per-GPU share and %d '
+                       'single-core, of the same workload; oracle/cpu_ipm.c (same IPM, fp64, -O3 '
+                       '-march=native, OpenMP)' % (nall, present, nsh, threads, n1)), kref
 
 
 def free_port():
@@ -427,8 +438,8 @@ def main():
             cpu, kref_u = cpu_reference(prob, wl['sample'], threads, not args.no_cpu and world == 1)
             if cpu is not None:
                 cpu['cores_present'] = present
-                cpu['cores_note'] = ('threads = OMP_NUM_THREADS (the per-GPU CPU share the box '
-                                     'sets) when set, else every core in the affinity mask')
+                cpu['cores_note'] = ('value: every core in the affinity mask; share_value: '
+                                     'OMP_NUM_THREADS threads (the per-GPU CPU share the box sets)')
             # algorithmic flops per launch: sum over the batch of K_ref x F_iter;
             # instances the reference solver does not converge on (infeasible) count with their
             # own iteration count
@@ -448,14 +459,15 @@ def main():
                 except Exception:
                     traffic = None
             check['mean_iterations_ref'] = float(kref.mean())
-            roof = {'bound': 'mfma', 'achieved': round(achieved, 4),
+            roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                     'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
                     'kernel_ms': round(kernel_ms, 4), 'flops_per_launch': flops_launch,
                     'traffic_source': traffic_src,
-                    'note': 'FP64 compute roof: 78.6 TF/s is both the FP64 MFMA and the FP64 '
-                            'vector peak of MI355X; this kernel issues no MFMA (5x5 stage blocks, '
-                            'DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
+                    'note': 'bound: FP64 VALU issue plus the latency of the sequential N-stage '
+                            'Riccati chain (roofline.latency); 78.6 TF/s is the FP64 vector peak '
+                            '(= the FP64 MFMA peak) of MI355X; this kernel issues no MFMA (5x5 '
+                            'stage blocks, DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
                             'passes of this config (traffic_source)'}
             st_json = os.path.join(ROOT, 'profiles', 'stamps_%s.json' % args.config)
@@ -494,6 +506,59 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def cll_subproblem_roofline(dl, X0, h):
+    """roofline of the learned-model loop's dominant kernel (dense_ipm_kernel, 83 % of the loop
+    in round 3): the loop's QP sub-problem shape - n = N nu + np = 101 variables, the m = 1024
+    condensed nominal rows Ain of DMS_LBMPC_casadi.m:262-276 shared by the batch - at the first
+    SQP iterate of every instance (zero window: the learned rollout is the nominal one, so the
+    sub-problem is this QP exactly), one batched launch.  Algorithmic flops per IPM iteration
+    (DESIGN.md 4): K = H + A'DA (lower triangle) n(n+1)m, Cholesky n^3/3, row products and A'v
+    (A z, A dz twice, A'lam, A'w twice) 12 n m, triangular solves 8 n^2; x the iterations each
+    instance takes."""
+    import bqp
+    n, m_, p, N = dl.n, dl.m, dl.p, dl.N
+    nz = dl.nz
+    B = len(X0)
+    dX = X0 - dl.x_eq
+    # nominal rollout x_k = Mx_k dx0 + Sx_k z (K = 0), u_k = e_k z
+    Et = np.zeros((p, nz)); Et[:, N * m_:] = np.eye(p)
+    H = np.zeros((nz, nz)); F = np.zeros((nz, n))            # f = F dx0
+    Mx, Sx = np.eye(n), np.zeros((n, nz))
+    for k in range(N + 1):
+        Ex = dl.Lq @ (Sx - dl.LAMBDA @ Et)
+        if k < dl.n_run:
+            Eu = np.zeros((m_, nz)); Eu[:, k * m_:(k + 1) * m_] = np.eye(m_)
+            Ur = dl.Lr @ (Eu - dl.PSI @ Et)
+            H += 2 * (Ex.T @ Ex + Ur.T @ Ur); F += 2 * Ex.T @ (dl.Lq @ Mx)
+        if k == N:
+            Ep = dl.Lp @ (Sx - dl.LAMBDA @ Et)
+            Lt = dl.Lt @ (dl.LAMBDA @ Et)
+            H += 2 * (Ep.T @ Ep + Lt.T @ Lt); F += 2 * Ep.T @ (dl.Lp @ Mx)
+        if k < N:
+            Eu = np.zeros((m_, nz)); Eu[:, k * m_:(k + 1) * m_] = np.eye(m_)
+            Sx = dl.A @ Sx + dl.B @ Eu
+            Mx = dl.A @ Mx
+    H = 0.5 * (H + H.T)
+    f = dX @ F.T
+    b = dl.b0[None, :] + dX @ dl.Bx.T
+    A = dl.Ain
+    mr = A.shape[0]
+    bqp.quadprog(H, f[:2], A, b[:2], handle=h)              # warm-up (module load, workspaces)
+    x, fv, flag, out, lam = bqp.quadprog(H, f, A, b, handle=h)
+    kms, nl = h.kernel_ms()
+    its = out['iterations'].astype(float)
+    F_it = nz * (nz + 1) * mr + nz ** 3 / 3.0 + 12.0 * nz * mr + 8.0 * nz * nz
+    flops = float(its.sum() * F_it)
+    ach = flops / (kms * 1e-3) / 1e12
+    return dict(bound='fp64_mfma', achieved=round(ach, 4), peak=FP64_PEAK_TFLOPS, unit='TFLOP/s',
+                frac=round(ach / FP64_PEAK_TFLOPS, 5), traffic=None, kernel_ms=round(kms, 4),
+                flops_per_launch=flops, launches=nl,
+                note='dense_ipm_kernel on the loop sub-problem shape (n = %d, m = %d, batch %d, '
+                     'mean %.1f IPM iterations, exit flags %s): K = H + A\'DA on the fp64 matrix '
+                     'cores; kernel_ms covers the solve and the polish launch' %
+                     (nz, mr, B, its.mean(), dict(zip(*[v.tolist() for v in np.unique(flag, return_counts=True)]))))
 
 
 def bench_aux(args):
@@ -673,6 +738,7 @@ def bench_aux(args):
         kms = h.kernel_ms()[0]
         st = np.load(os.path.join(GOLD, 'dms_lbmpc_loops.npz'))['DMS_tLBMPC_q100']
         e0 = np.abs(r.X[0] - st[:args.steps + 1])
+        roof = cll_subproblem_roofline(dl, X0, h)
         from oracle import lbmpc as olb               # CPU leg only
         from oracle.mg_model import mg_problem
         c0 = _t.perf_counter()
@@ -685,7 +751,7 @@ def bench_aux(args):
                     data='x_init of DMS_LBMPC_casadi.m and seeded perturbations (+-0.005 in x1, x2)',
                     config={'workload': 'CLL: DMS LBMPC closed loop, batch %d, %d steps' % (B, args.steps),
                             'batch_per_gpu': B, 'horizon': 100, 'parallelism': 'dp1'},
-                    roofline=None, kernel_ms=round(kms, 4),
+                    roofline=roof, kernel_ms=round(kms, 4),
                     cpu_baseline=dict(value=round(cpu, 3), unit='instance-steps/s', cores=1, kind='port',
                                       sample='3 steps of one instance, oracle/lbmpc.py dms_lbmpc_loop (numpy)'),
                     check=dict(converged_frac=float((r.exitflag == 1).mean()),

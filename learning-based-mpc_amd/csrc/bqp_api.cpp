@@ -244,7 +244,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     auto shared_layout = [&](bool single) {
         Shared o;
         o.lng = !single && N + 1 > 64;
-        o.hpsh = o.lng && mp > 0 && D->shp == 0;
+        o.hpsh = mp > 0 && D->shp == 0;       // the shared polytope rhs (every horizon)
         o.bndsh = o.lng && D->sxb == 0 && D->sub == 0;
         const int nbr = (N + 1) * 2 * (nx + nu);
         int sh = (o.lng || hinst) ? 0 : (N + 1) * hstride;
@@ -263,7 +263,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
     auto fit_wpb = [&](bool single, int& wpb) -> bool {
         const Shared& S = single ? L32 : L64;
         const int shared_doubles = S.doubles;
-        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi, false, false, false, hinst)
+        const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi, false, S.hpsh, false, hinst)
                                     : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi, S.lng, S.hpsh, S.bndsh, hinst);
         const size_t lds_budget = 160 * 1024 / (single ? sizeof(float) : sizeof(double));
         // long horizons (N + 1 > 64, two stages per lane) are compiled for <= 256 threads per
@@ -694,10 +694,13 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     q.sH = (int64_t)n * n; q.sf = n; q.sA = 0; q.sb = m;
     q.x = a.d; q.lam_ineqlin = a.lam; q.exitflag = a.qpflag;
     q.work = (double*)h->dwork.p; q.work_stride = wst;
-    // every sub-problem polished to its active-set solution: the GN iteration converges linearly
-    // (60-80 iterations on the learned costs of DMS_LBMPC_casadi.m), and interior-point steps
-    // accurate to ~1e-8 left it wandering at that level (tools/diag_dms_gpu.py)
-    q.polish = o.polish < 0 ? 0 : 2;
+    // sub-problem polish: after 0 / -8 exits always; the active-set polish of every converged
+    // sub-problem (mode 2) only once the SQP has run LB_POLISH_STALL iterations - the
+    // Gauss-Newton iteration converges linearly on the learned costs of DMS_LBMPC_casadi.m and
+    // interior-point steps accurate to ~1e-8 left it wandering at that level
+    // (tools/diag_dms_gpu.py); with the exact Hessian the SQP ends in 1-4 iterations, where the
+    // polish launch after every sub-problem was 12 % of the loop
+    constexpr int LB_POLISH_STALL = 6;
     q.stats = (double*)h->dwork.p + (size_t)wst * B;
     HIP_TRY(hipEventRecord(h->ev0, st));
     int launches = 0;
@@ -705,6 +708,7 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 1, st));
         HIP_TRY(bqp::launch_lbmpc_normal(a, st));
         if (a.hess) HIP_TRY(bqp::launch_lbmpc_hess(a, st));
+        q.polish = o.polish < 0 ? 0 : (it >= LB_POLISH_STALL ? 2 : 1);
         HIP_TRY(bqp::launch_dense(q, st));
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
         HIP_TRY(bqp::launch_lbmpc_update(a, st));

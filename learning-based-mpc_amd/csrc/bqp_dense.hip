@@ -27,6 +27,7 @@ namespace bqp {
 
 #define DT 256
 #define TILE 32
+typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_PIV_FLOOR 1e-14    // static pivot floor of K, relative to its largest diagonal entry
 #define DQ_CONVEX_EPS 1e-10   // shift of the convexity test (relative)
 #define DQ_MU_BLOWUP 1e6
@@ -779,50 +780,61 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         const int ne = n * (n + 1) / 2;
         double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
         if (n <= 128) {
-            // register-tiled A'DA (the normal-equation scheme of lbmpc_normal_kernel): thread
-            // (tx, ty) accumulates the 8 x 8 entries (ty + 16 p, tx + 16 q) over 32-row LDS tiles,
-            // 16 LDS reads per 64 FMAs instead of 3 per FMA (the packed-triangle loop below was
-            // LDS-bandwidth bound: ~0.5 ms per factorisation at n = 101, m = 1024)
-            const int tx = tid & 15, ty = tid >> 4;
-            double acc[8][8];
+            // K = H + A'DA on the fp64 matrix cores (v_mfma_f64_16x16x4_f64): the lower block
+            // triangle of ceil(n/16)^2 16 x 16 tiles, tile t = w, w + 4, ... on wave w (at most 9
+            // per wave); each k-step takes 4 rows of A from the LDS row tile - lane l supplies
+            // A[r][16 I + l%16] (r = 4 s + l/16) as the A operand and d_r A[r][16 J + l%16] as the
+            // B operand, so tile (I, J) accumulates sum_r A[r][16I + i] d_r A[r][16J + j].
+            // Columns >= n read a clamped (finite) column and rows past the tile have d = 0:
+            // their products land in entries i or j >= n, which are not written back.  (Round 3
+            // formed this product with VALU FMAs from 8 x 8 register tiles: ~10 % of the CU's
+            // FP64 rate, the largest phase of the learned-model loop's sub-problem.)
+            constexpr int TPW = 9;
+            const int lane = tid & 63, wv = tid >> 6;
+            const int c16 = lane & 15, k4 = lane >> 4;
+            const int nbk = (n + 15) >> 4, ntl = nbk * (nbk + 1) / 2;
+            int tI[TPW], tJ[TPW];
 #pragma unroll
-            for (int p2 = 0; p2 < 8; ++p2)
+            for (int u = 0; u < TPW; ++u) {
+                // tile index t -> (I, J), J <= I, row-major over the lower block triangle
+                const int t = wv + 4 * u;
+                int I = 0;
+                while ((I + 1) * (I + 2) / 2 <= t) ++I;
+                tI[u] = I;
+                tJ[u] = t - I * (I + 1) / 2;
+            }
+            dbl4 acc[TPW];
 #pragma unroll
-                for (int q2 = 0; q2 < 8; ++q2) acc[p2][q2] = 0.0;
+            for (int u = 0; u < TPW; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
             for (int r0 = 0; r0 < m; r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
                 load_tile(r0, rows);
                 if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
-#pragma unroll 2
-                for (int rr = 0; rr < rows; ++rr) {
-                    const double* Tr = tileA + rr * ts;
-                    const double dr = Tr[tw];
-                    // clamped, unconditional LDS reads (one wait per row instead of one per
-                    // guarded load); accumulators of entries i or j >= n are discarded
-                    // blocks q2 <= p2 < nb only: the Cholesky reads the lower triangle
-                    double cj[8], ci[8];
+                for (int s4 = 0; s4 < rows; s4 += 4) {
+                    const int rr = s4 + k4;
+                    const double* Tr = tileA + min(rr, rows - 1) * ts;
+                    const double dr = rr < rows ? Tr[tw] : 0.0;
 #pragma unroll
-                    for (int q2 = 0; q2 < 8; ++q2) {        // unconditional: no wait inside a branch
-                        cj[q2] = Tr[min(tx + 16 * q2, n - 1)];
-                        ci[q2] = Tr[min(ty + 16 * q2, n - 1)];
-                    }
-#pragma unroll
-                    for (int p2 = 0; p2 < 8; ++p2) {    // no run-time bound: a branch per block row
-                        const double cd = ci[p2] * dr;     // cost more than the blocks it skipped
-#pragma unroll
-                        for (int q2 = 0; q2 <= p2; ++q2) acc[p2][q2] = fma(cd, cj[q2], acc[p2][q2]);
+                    for (int u = 0; u < TPW; ++u) {
+                        if (wv + 4 * u < ntl) {          // wave-uniform
+                            const double ai = Tr[min(16 * tI[u] + c16, n - 1)];
+                            const double aj = Tr[min(16 * tJ[u] + c16, n - 1)];
+                            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, dr * aj, acc[u], 0, 0, 0);
+                        }
                     }
                 }
             }
+            // tile (I, J), lane l, register e: K(16 I + l/16 + 4 e, 16 J + l%16)
 #pragma unroll
-            for (int p2 = 0; p2 < 8; ++p2)
+            for (int u = 0; u < TPW; ++u) {
+                if (wv + 4 * u >= ntl) continue;
 #pragma unroll
-                for (int q2 = 0; q2 <= p2; ++q2) {
-                    const int i = ty + 16 * p2, j = tx + 16 * q2;
-                    if (i < n && i >= j) {      // lower triangle (col-major K[j n + i], i >= j)
-                        double v = H[(int64_t)j * n + i] + acc[p2][q2];
+                for (int e2 = 0; e2 < 4; ++e2) {
+                    const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
+                    if (i < n && j < n && i >= j) {      // lower triangle (col-major K[j n + i])
+                        double v = H[(int64_t)j * n + i] + acc[u][e2];
                         if (i == j) {
                             if (up_present(j)) v += lB[j] / tB[j];
                             if (lo_present(j)) v += lB[n + j] / tB[n + j];
@@ -831,6 +843,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                         K[(int64_t)j * n + i] = v;
                     }
                 }
+            }
             __syncthreads();
         }
         for (int base = 0; base < (n <= 128 ? 0 : ne); base += DT * 8) {
@@ -1145,7 +1158,6 @@ __host__ __device__ inline int small_lds_doubles(int n, int m) {
     return 2 * n * n + 8 * n + 12 * n + 8 * m + (m * n <= SW_A_LDS_MAX ? m * n : 0);
 }
 
-typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 // A'v for the n <= 16 NT columns of A (column-major m x n): every lane accumulates its rows
 // r = lane, lane + 64, ... for all columns at once, then one transposed wave sum (wsum_t) leaves

@@ -111,6 +111,14 @@ __device__ __forceinline__ float frcp(float t) {
     return __builtin_fmaf(r, __builtin_fmaf(-t, r, 1.0f), r);
 }
 
+// the lane index made opaque where a phase starts: the per-lane LDS addresses of the phase are
+// formed inside it instead of being hoisted to the kernel start and carried through the
+// iteration loop in registers (dozens of them: the stage wave's scratch spills)
+__device__ __forceinline__ int opq(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // fused multiply-add in the instantiation's precision (no promotion of the fp32 path to fp64)
 __device__ __forceinline__ double fmar(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float fmar(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -188,14 +196,15 @@ enum : int {
 // Per-instance LDS layout (in doubles), sized from N at run time.
 struct QpLds {
     int P, K, Lr, L0, AB, xs, xu, qt_xpi, rs, ru, re, pv, wv, bw, qu, fv, dsv, duv, dsc, duc, Dx, FD,
-        blam, ebox, bnd, gpp, gpe, prp, hp, xch, Fi, Hi, total;
+        blam, ebox, bnd, gpp, gpe, prp, hp, rp, xch, Fi, Hi, total;
     // fpi: the instance carries its own polytope matrix (bqp_ocp_data.sFp != 0), NV x mpad.
     // lng: long-horizon layout (N + 1 > 64, two instances per workgroup at fp64 N = 100): the
     // Riccati P_k live in global scratch (an LDS ring of two stages feeds the recursion), the
     // forward drift f_k shares the qhat_k slot, the dynamics residual re_k is recomputed from the
     // iterate where it is used, box multipliers and right-hand-side terms are stored per box
     // variable ([upper] - [lower]), and the polytope right-hand side and box bounds sit in the
-    // shared tables when the batch shares them (hpsh, bndsh).
+    // shared tables when the batch shares them (hpsh, bndsh).  The polytope rhs is in the
+    // shared tables whenever the batch shares it (hpsh, every horizon).
     // hinst: per-instance stage-cost table (bqp_ocp_data.sW != 0) in the slot (short horizons)
     __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false,
                                           bool lng = false, bool hpsh = false, bool bndsh = false,
@@ -207,7 +216,7 @@ struct QpLds {
         o.K = c;      c += N * NU * NS;              // feedback K_k (row-major NU x NS)
         o.Lr = c;     c += N * NU * NU;              // factor of Rhat_k (nu = 1: its reciprocal)
         o.L0 = c;     c += NP * NP;                  // factor of P_0[theta, theta]
-        o.AB = c;     c += NS * NS + NS * NU;        // Abar (row-major), Bbar
+        o.AB = c;     c += NS * NS + NS * NU + NS;   // Abar (row-major), Bbar, cbar
         o.xs = c;     c += (N + 1) * NS;             // s_k
         o.xu = c;     c += (N + 1) * NU;             // u_k (u_N = 0)
         o.qt_xpi = c; c += (N + 1) * NS;             // pi_k in the residuals, qhat_k in the solves
@@ -235,7 +244,8 @@ struct QpLds {
         o.gpp = c;    c += NV;                       // Fp' lam
         o.gpe = c;    c += NV;                       // Fp' e
         o.prp = c;    c += mpad;                     // predictor dt*dlam of the polytope rows
-        o.hp = c;     c += hpsh ? 0 : mpad;          // polytope right-hand side
+        o.hp = c;     c += hpsh ? 0 : mpad;          // polytope right-hand side (hpsh: shared)
+        o.rp = c;     c += mpad;                     // polytope row residuals (row wave)
         o.xch = c;    c += X_NXCH;
         o.Fi = c;     c += fpi ? NV * mpad : 0;      // per-instance polytope (column-major)
         o.Hi = c;     c += (hinst && !lng) ? (N + 1) * (NV * NV + 1) : 0;   // per-instance H table
@@ -291,7 +301,7 @@ __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
                 a.stamps[(int64_t)inst * 32 + (base) + i_] = (double)st_acc[i_]; \
         }                                                                  \
     } while (0)
-#elif defined(BQP_ISA_ONLY_MG10)
+#elif defined(BQP_ISA_ONLY_MG10) || defined(BQP_ISA_ONLY_DI)
 #define STAMP(id) asm volatile(";BQP_PHASE " #id)
 #define STAMP_DECL do { } while (0)
 #define STAMP_STORE(base) do { } while (0)
@@ -311,7 +321,8 @@ __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
 // ==========================================================================================
 template <int NX, int NU, int NP, int SPL, bool POL>
 __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
-                                           const real* Hs, int lane, int inst) {
+                                           const real* Hs, int lane_w, int inst) {
+    const int lane = lane_w;
     // POL: the repair kernel (ocp_polish_kernel) - the same IPM, then the active-set polish
     constexpr bool PC = POL && BQP_POLISH && !BQP_EXP_NOSTAGE;
     constexpr int NS = NX + NP;
@@ -350,13 +361,15 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             const int i = lane / NU, j = lane % NU;
             W[L.AB + NS * NS + lane] = (i < NX) ? B[j * NX + i] : 0.0;
         }
+        // the affine term c of the dynamics (theta rows 0)
+        if (lane < NS) W[L.AB + NS * NS + NS * NU + lane] = (lane < NX && a.c) ? a.c[(int64_t)inst * a.sc + lane] : 0.0;
     }
     wave_sync();
     auto Abar = [&](int i, int j) __attribute__((always_inline)) -> real { return W[L.AB + i * NS + j]; };
     auto Bbar = [&](int i, int j) __attribute__((always_inline)) -> real { return W[L.AB + NS * NS + i * NU + j]; };
-    real cb[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) cb[i] = (i < NX && a.c) ? a.c[(int64_t)inst * a.sc + i] : 0.0;
+    // c from LDS at use (a register copy was carried through the loop: a scratch spill of the
+    // DI kernel)
+    auto cb = [&](int i) __attribute__((always_inline)) -> real { return W[L.AB + NS * NS + NS * NU + i]; };
     const double* wb = a.w ? a.w + (int64_t)inst * a.sw : nullptr;
     // linear cost term of stage k, internal index i ([x; theta; u] from external [x; u; theta])
     auto gterm = [&](int k, int i) __attribute__((always_inline)) -> real {
@@ -385,6 +398,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 
     // ---- stage vectors to LDS (s, u, pi) ----
     auto write_state = [&]() __attribute__((always_inline)) {
+        const int lane = opq(lane_w);
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -401,6 +415,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // ---- stage residuals without the row multipliers: rs' = g + Abar' pi_{k+1} - pi_k,
     //      ru' = g_u + Bbar' pi_{k+1}, re = Abar s + Bbar u + c - s_{k+1}; returns max|re|, max|g|
     auto stage_partials = [&](real& feasA, real& gsA) __attribute__((always_inline)) {
+        const int lane = opq(lane_w);
         real fe = 0, gs = 0;
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
@@ -444,7 +459,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
             if (k < N) {
 #pragma unroll
                 for (int i = 0; i < NS; ++i) {
-                    real acc = cb[i] - W[L.xs + (k + 1) * NS + i];
+                    real acc = cb(i) - W[L.xs + (k + 1) * NS + i];
 #pragma unroll
                     for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
 #pragma unroll
@@ -463,7 +478,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     bool rez = false;   // polish direction solves: zero dynamics residual (PC only)
     auto re_at = [&](int j, int k, int i) __attribute__((always_inline)) -> real {
         if constexpr (PC) { if (rez) return real(0); }
-        real acc = cb[i] - W[L.xs + (k + 1) * NS + i];
+        real acc = cb(i) - W[L.xs + (k + 1) * NS + i];
 #pragma unroll
         for (int c = 0; c < NS; ++c) acc += Abar(i, c) * s[j][c];
 #pragma unroll
@@ -474,6 +489,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // ---- add the row multipliers (box [upper, lower] in that order, polytope at kp) and
     //      return the stationarity norm ----
     auto combine = [&]() __attribute__((always_inline)) -> real {
+        const int lane = opq(lane_w);
         real gpp[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) gpp[c] = W[L.gpp + c];
@@ -773,6 +789,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     //   cw_k = Phi_k' w_k (Phi_k = Abar + Bbar K_k; the pre-pass adds it to qt_k),
     //   bw_k = Bbar' w_k (the post-backward pass adds it to Bbar' p_{k+1}).
     auto prep_iter = [&]() __attribute__((always_inline)) {
+        const int lane = opq(lane_w);
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -819,16 +836,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
     const int li = lane < NS ? lane : NS - 1;
     auto solve = [&](int ods, int odu) __attribute__((always_inline)) {
-        real Acol[NS], Arow[NS], Bli[NU], Bl[NS][NU];  // Abar(:, li), Abar(li, :), Bbar(li, :), Bbar
-#pragma unroll
-        for (int c = 0; c < NS; ++c) {
-            Acol[c] = Abar(c, li);
-            Arow[c] = Abar(li, c);
-#pragma unroll
-            for (int x = 0; x < NU; ++x) Bl[c][x] = Bbar(c, x);
-        }
-#pragma unroll
-        for (int x = 0; x < NU; ++x) Bli[x] = Bbar(li, x);
+        const int lane = opq(lane_w);
         real qs[SPL][NS], qu[SPL][NU];
         real gpe[NV];
 #pragma unroll
@@ -895,41 +903,75 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
         wave_sync();
         STAMP(10);
-        // backward sweep: lane i < NS computes entry i of p_k = Phi_k' p_{k+1} + qh_k; the new
-        // vector is broadcast with readlane (scalar registers); two register sets used
-        // alternately (stages k, k-1), each refilled two stages ahead
+        // backward sweep p_k = Phi_k' p_{k+1} + qh_k with Phi_k = Abar + Bbar K_k: EVERY lane
+        // computes the whole vector from uniform (broadcast) LDS reads - no cross-lane traffic on
+        // the sequential chain (round 3: lane i formed entry i and readlane broadcast the vector,
+        // ~250 cycles per stage).  Abar = [A 0; 0 I], Bbar = [B; 0] (the per-instance model in
+        // LDS), so Phi_k' p = [A' p_x; p_th] + K_k' (B' p_x): NX^2 + NX NU + NS NU FMAs in
+        // NS + NU independent chains.  Lanes < NS store their entry.
         {
+            real Am[NX][NX], Bm[NX][NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+#pragma unroll
+                for (int c = 0; c < NX; ++c) Am[i][c] = Abar(i, c);
+#pragma unroll
+                for (int x = 0; x < NU; ++x) Bm[i][x] = Bbar(i, x);
+            }
             real p[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) p[i] = W[L.pv + N * NS + i];
-            // Phi_k column li = Abar(:, li) + Bbar K_k(:, li)
-            auto load_b = [&](int k, real (&kc)[NU], real& q) __attribute__((always_inline)) {
-                q = W[L.qt_xpi + k * NS + li];
+            struct BS { real q[NS], kk[NU][NS]; };
+            auto load_b = [&](int k, BS& o) __attribute__((always_inline)) {
 #pragma unroll
-                for (int x = 0; x < NU; ++x) kc[x] = W[L.K + k * NU * NS + x * NS + li];
+                for (int i = 0; i < NS; ++i) o.q[i] = W[L.qt_xpi + k * NS + i];
+#pragma unroll
+                for (int x = 0; x < NU; ++x)
+#pragma unroll
+                    for (int i = 0; i < NS; ++i) o.kk[x][i] = W[L.K + k * NU * NS + x * NS + i];
             };
-            real k0[NU], q0, k1[NU], q1;
-            load_b(N - 1, k0, q0);
-            if (N >= 2) load_b(N - 2, k1, q1);
-            auto step_b = [&](int k, const real (&kc)[NU], real q) __attribute__((always_inline)) {
-                real acc = q;
+            BS b0, b1;
+            load_b(N - 1, b0);
+            if (N >= 2) load_b(N - 2, b1);
+            auto step_b = [&](int k, const BS& o) __attribute__((always_inline)) {
+                real sb[NU];                                  // B' p_x
 #pragma unroll
-                for (int c = 0; c < NS; ++c) {
-                    real ph = Acol[c];
+                for (int x = 0; x < NU; ++x) {
+                    real t = Bm[0][x] * p[0];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) ph += Bl[c][x] * kc[x];
-                    acc += ph * p[c];
+                    for (int c = 1; c < NX; ++c) t = fmar(Bm[c][x], p[c], t);
+                    sb[x] = t;
                 }
-                if (lane < NS) W[L.pv + k * NS + lane] = acc;
+                real o2[NS];
 #pragma unroll
-                for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
+                for (int j = 0; j < NS; ++j) {
+                    real v = o.q[j];
+                    if (j < NX) {
+#pragma unroll
+                        for (int c = 0; c < NX; ++c) v = fmar(Am[c][j], p[c], v);
+                    } else {
+                        v += p[j];
+                    }
+                    o2[j] = v;
+                }
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    real v = o2[j];
+#pragma unroll
+                    for (int x = 0; x < NU; ++x) v = fmar(o.kk[x][j], sb[x], v);
+                    p[j] = v;
+                }
+                real mine = p[0];
+#pragma unroll
+                for (int j = 1; j < NS; ++j) mine = (lane == j) ? p[j] : mine;
+                if (lane < NS) W[L.pv + k * NS + lane] = mine;
             };
             for (int k = N - 1; k >= 0; k -= 2) {
-                step_b(k, k0, q0);
-                if (k >= 2) load_b(k - 2, k0, q0);
+                step_b(k, b0);
+                if (k >= 2) load_b(k - 2, b0);
                 if (k == 0) break;
-                step_b(k - 1, k1, q1);
-                if (k >= 3) load_b(k - 3, k1, q1);
+                step_b(k - 1, b1);
+                if (k >= 3) load_b(k - 3, b1);
             }
         }
         wave_sync();
@@ -963,7 +1005,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
         wave_sync();
         STAMP(12);
-        // theta_0 step + forward sweep: lane i < NS computes entry i of ds_{k+1} = Phi_k ds_k + f_k
+        // theta_0 step + forward sweep ds_{k+1} = Phi_k ds_k + f_k
         {
             real d[NS];
 #pragma unroll
@@ -978,36 +1020,69 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
                 for (int i = 0; i < NS; ++i) W[ods + i] = d[i];
             }
-            // Phi_k row li = Abar(li, :) + Bbar(li, :) K_k
-            auto load_f = [&](int k, real (&kr)[NU][NS], real& f) __attribute__((always_inline)) {
-                f = W[L.fv + k * NS + li];
+            // forward sweep ds_{k+1} = Phi_k ds_k + f_k, every lane the whole vector (as the
+            // backward sweep): Phi_k d = [A d_x + B (K_k d); d_th]
+            real Am[NX][NX], Bm[NX][NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+#pragma unroll
+                for (int c = 0; c < NX; ++c) Am[i][c] = Abar(i, c);
+#pragma unroll
+                for (int x = 0; x < NU; ++x) Bm[i][x] = Bbar(i, x);
+            }
+            struct FS { real f[NS], kk[NU][NS]; };
+            auto load_f = [&](int k, FS& o) __attribute__((always_inline)) {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) o.f[i] = W[L.fv + k * NS + i];
 #pragma unroll
                 for (int x = 0; x < NU; ++x)
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) kr[x][c] = W[L.K + k * NU * NS + x * NS + c];
+                    for (int c = 0; c < NS; ++c) o.kk[x][c] = W[L.K + k * NU * NS + x * NS + c];
             };
-            real k0[NU][NS], f0, k1[NU][NS], f1;
-            load_f(0, k0, f0);
-            if (N >= 2) load_f(1, k1, f1);
-            auto step_f = [&](int k, const real (&kr)[NU][NS], real f) __attribute__((always_inline)) {
-                real acc = f;
+            FS f0, f1;
+            load_f(0, f0);
+            if (N >= 2) load_f(1, f1);
+            auto step_f = [&](int k, const FS& o) __attribute__((always_inline)) {
+                real kd[NU];                                  // K_k d
 #pragma unroll
-                for (int c = 0; c < NS; ++c) {
-                    real ph = Arow[c];
+                for (int x = 0; x < NU; ++x) {
+                    real t = o.kk[x][0] * d[0];
 #pragma unroll
-                    for (int x = 0; x < NU; ++x) ph += Bli[x] * kr[x][c];
-                    acc += ph * d[c];
+                    for (int c = 1; c < NS; ++c) t = fmar(o.kk[x][c], d[c], t);
+                    kd[x] = t;
                 }
-                if (lane < NS) W[ods + (k + 1) * NS + lane] = acc;
+                real o2[NS];
 #pragma unroll
-                for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
+                for (int i = 0; i < NS; ++i) {
+                    real v = o.f[i];
+                    if (i < NX) {
+#pragma unroll
+                        for (int c = 0; c < NX; ++c) v = fmar(Am[i][c], d[c], v);
+                    } else {
+                        v += d[i];
+                    }
+                    o2[i] = v;
+                }
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    real v = o2[i];
+                    if (i < NX) {
+#pragma unroll
+                        for (int x = 0; x < NU; ++x) v = fmar(Bm[i][x], kd[x], v);
+                    }
+                    d[i] = v;
+                }
+                real mine = d[0];
+#pragma unroll
+                for (int i = 1; i < NS; ++i) mine = (lane == i) ? d[i] : mine;
+                if (lane < NS) W[ods + (k + 1) * NS + lane] = mine;
             };
             for (int k = 0; k < N; k += 2) {
-                step_f(k, k0, f0);
-                if (k + 2 < N) load_f(k + 2, k0, f0);
+                step_f(k, f0);
+                if (k + 2 < N) load_f(k + 2, f0);
                 if (k + 1 >= N) break;
-                step_f(k + 1, k1, f1);
-                if (k + 3 < N) load_f(k + 3, k1, f1);
+                step_f(k + 1, f1);
+                if (k + 3 < N) load_f(k + 3, f1);
             }
         }
         wave_sync();
@@ -1039,6 +1114,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // length: it is formed while the row wave runs the ratio test (before B5) and parked in the
     // cw_k slot (dead until the next factorisation); the update after B6 only scales it
     auto dual_dir = [&](int ids) __attribute__((always_inline)) {
+        const int lane = opq(lane_w);
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1059,6 +1135,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
     };
     auto update_stage_dir = [&](real al, int ids, int idu) __attribute__((always_inline)) {
+        const int lane = opq(lane_w);
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1076,6 +1153,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
     };
     auto update_stage = [&](real al, int ids, int idu) __attribute__((always_inline)) {
+        const int lane = opq(lane_w);
 #pragma unroll
         for (int j = 0; j < SPL; ++j) {
             const int k = lane + WAVE * j;
@@ -1457,6 +1535,43 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     unsigned bpk[(BPL + 1) / 2];
 #pragma unroll
     for (int b = 0; b < (BPL + 1) / 2; ++b) bpk[b] = 0;
+    // LDS offset of each box variable's entry of the per-stage diagonal D (L.Dx), 16 bits per
+    // variable pv: the row passes read it instead of re-deriving k, sl from the lane (the derived
+    // indices were hoisted and carried through the loop, the row wave's scratch spills)
+    unsigned dxk[(BPL / 2 + 1) / 2];
+#pragma unroll
+    for (int i = 0; i < (BPL / 2 + 1) / 2; ++i) dxk[i] = 0;
+#pragma unroll
+    for (int pv = 0; pv < BPL / 2; ++pv) {
+        const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
+        const unsigned off = (unsigned)(L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX)));
+        dxk[pv >> 1] |= (off & 0xffffu) << (16 * (pv & 1));
+    }
+    auto dx_off = [&](int pv) __attribute__((always_inline)) -> int {
+        return (int)((dxk[pv >> 1] >> (16 * (pv & 1))) & 0xffffu);
+    };
+    // lanes NV .. NV + NT - 1 of the transposed F'DF sum hold upper-triangle entry lane - NV =
+    // (i2, j2): its two LDS offsets in L.FD, packed (one register instead of two carried indices)
+    unsigned fdk = 0;
+    {
+        constexpr int NTF = NV * (NV + 1) / 2;
+        const int idx = lane - NV;
+        if (idx >= 0 && idx < NTF) {
+            int i2 = 0, st = 0;
+#pragma unroll
+            for (int r = 1; r < NV; ++r) {
+                const int sr = r * NV - r * (r - 1) / 2;
+                if (idx >= sr) { i2 = r; st = sr; }
+            }
+            const int j2 = i2 + (idx - st);
+            fdk = (unsigned)(L.FD + i2 * NV + j2) | ((unsigned)(L.FD + j2 * NV + i2) << 16);
+        }
+    }
+    auto fd_off = [&](int h) __attribute__((always_inline)) -> int {
+        unsigned k = fdk;
+        asm volatile("" : "+v"(k));     // formed at the use (hoisted, the offsets were spilled)
+        return (int)((k >> (16 * h)) & 0xffffu);
+    };
     unsigned bmsk = 0, binr = 0;         // present rows; rows in range (r < nbr)
     real bsl = 0.0, mcount = 0.0;
 #pragma unroll
@@ -1492,7 +1607,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     auto bcode = [&](int b) __attribute__((always_inline)) -> int { return (int)((bpk[b >> 1] >> (16 * (b & 1))) & 0xffffu); };
     auto binrange = [&](int b) __attribute__((always_inline)) -> bool { return (binr >> b) & 1u; };
     // polytope rows l, l+64, ...
-    const bool hpsh = LNG && a.sh_hp >= 0;           // polytope rhs in the shared tables
+    const bool hpsh = a.sh_hp >= 0;                  // polytope rhs in the shared tables
     real* hpi = hpsh ? const_cast<real*>(Sh) + a.sh_hp : W + L.hp;
     if (!hpsh) {
         const double* hg = a.hp + (int64_t)inst * a.shp;
@@ -1523,7 +1638,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     // row state: slack t, multiplier lam, 1/t; polytope rows also their residual ri (box-row
     // residuals are re-formed from the LDS stage vector and bounds when needed)
     real tx[BPL], lx[BPL];
-    real tp[RPL], lp[RPL], rp[RPL];
+    real tp[RPL], lp[RPL];
+    // polytope row residuals in LDS (L.rp): fewer registers carried through the loop (the row
+    // wave's scratch spills of round 3)
+#define RP(q) W[L.rp + lane + WAVE * (q)]
     // 1: the corrector carries Mehrotra's second-order term dt_a dlam_a; 0: this iteration's
     // predictor step was short on a feasible iterate, the corrector is a pure centring step
     real socf = 1.0;
@@ -1534,7 +1652,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 #pragma unroll
     for (int b = 0; b < BPL; ++b) { tx[b] = 1.0; lx[b] = 1.0; }
 #pragma unroll
-    for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; rp[q] = 0.0; }
+    for (int q = 0; q < RPL; ++q) { tp[q] = 1.0; lp[q] = 1.0; RP(q) = 0.0; }
 
     // ---- multiplier-side tables (depend on t, lam only): box multipliers, Fp'lam, 1/t,
     //      D = lam/t per stage, F'DF, sum t.lam ----
@@ -1562,10 +1680,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             if constexpr (LNG) {
                 if (binrange(2 * pv)) W[L.blam + lane + WAVE * pv] = blv;   // [upper] - [lower]
             }
-            if (binrange(2 * pv)) {
-                const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
-                W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
-            }
+            if (binrange(2 * pv)) W[dx_off(pv)] = d;
         }
         real gpp[NV];
         real fd[NV * (NV + 1) / 2];
@@ -1609,16 +1724,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             W[L.gpp + lane] = tot;
         } else if (lane < NV + NT) {
             // upper-triangle index -> (i2, j2), rows of length NV, NV-1, ...
-            const int idx = lane - NV;
-            int i2 = 0, st = 0;
-#pragma unroll
-            for (int r = 1; r < NV; ++r) {
-                const int sr = r * NV - r * (r - 1) / 2;
-                if (idx >= sr) { i2 = r; st = sr; }
-            }
-            const int j2 = i2 + (idx - st);
-            W[L.FD + i2 * NV + j2] = tot;
-            W[L.FD + j2 * NV + i2] = tot;
+            W[fd_off(0)] = tot;
+            W[fd_off(1)] = tot;
         } else if (lane == NV + NT) {
             X[X_CS] = tot;
         }
@@ -1653,7 +1760,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             const int r = lane + WAVE * q;
             if (r < mp) {
                 const real ri = fdot(r, vp) + tp[q] - hpi[r];
-                rp[q] = ri;
+                RP(q) = ri;
                 fe = fmax(fe, fabs(ri));
             }
         }
@@ -1708,7 +1815,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             const int r = lane + WAVE * q;
             if (r < mp) {
                 const real pr = corr ? prp_get(q, r) : 0.0;
-                const real e = (lp[q] * rp[q] - rcv(tp[q], lp[q], pr, corr, smu)) * frcp(tp[q]);
+                const real e = (lp[q] * RP(q) - rcv(tp[q], lp[q], pr, corr, smu)) * frcp(tp[q]);
 #pragma unroll
                 for (int c = 0; c < NV; ++c) gpe[c] += Fs[c * mpad + r] * e;
             }
@@ -1750,7 +1857,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             const real pr = corr ? prp_get(q, r) : 0.0;
             const real rc = rcv(tp[q], lp[q], pr, corr, smu);
             const real fd = fdot(r, dvp);
-            const real dt = -rp[q] - fd;
+            const real dt = -RP(q) - fd;
             const real dl = (-rc - lp[q] * dt) * frcp(tp[q]);
             if (mode == 0) {
                 acc = fmax(acc, -dt * frcp(tp[q]));
@@ -1759,8 +1866,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 // the polytope residual Fp v + t - hp of the stepped iterate, by the linear
                 // update r + al (Fp dv + dt): the next iteration needs no residual pass (and
                 // no barrier) before its factorisation
-                rp[q] += al * (fd + dt);
-                acc = fmax(acc, fabs(rp[q]));
+                RP(q) += al * (fd + dt);
+                acc = fmax(acc, fabs(RP(q)));
                 tp[q] += al * dt;
                 lp[q] += al * dl;
             }
@@ -1817,14 +1924,14 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             const real t = tp[q], l = lp[q];
             const real it = frcp(t);
             const real rc = t * l;
-            const real dt = -rp[q] - fd;
+            const real dt = -RP(q) - fd;
             const real dl = (-rc - l * dt) * it;
             rm = fmax(rm, -dt * it);
             rm = fmax(rm, -dl * frcp(l));
             const real pr = dt * dl;
             s2 += pr;
             W[L.prp + r] = pr;
-            const real e0 = (l * rp[q] - (rc + pr)) * it;
+            const real e0 = (l * RP(q) - (rc + pr)) * it;
 #pragma unroll
             for (int c = 0; c < NV; ++c) { gpe0[c] += f[c] * e0; gpi[c] += f[c] * it; }
         }
@@ -1878,10 +1985,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
             if constexpr (LNG) {
                 if (binrange(2 * pv)) W[L.blam + lane + WAVE * pv] = blv;   // [upper] - [lower]
             }
-            if (binrange(2 * pv)) {
-                const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
-                W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
-            }
+            if (binrange(2 * pv)) W[dx_off(pv)] = d;
         }
         real gpp[NV];
         real fdt[NV * (NV + 1) / 2];
@@ -1904,10 +2008,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 #pragma unroll
                 for (int c = 0; c < NV; ++c) fd += f[c] * dvp[c];
                 const real rc = rcv(tp[q], lp[q], prp_get(q, r), true, smu);
-                const real dt = -rp[q] - fd;
+                const real dt = -RP(q) - fd;
                 const real dl = (-rc - lp[q] * dt) * frcp(tp[q]);
-                rp[q] += al * (fd + dt);
-                fe = fmax(fe, fabs(rp[q]));
+                RP(q) += al * (fd + dt);
+                fe = fmax(fe, fabs(RP(q)));
                 tp[q] += al * dt;
                 lp[q] += al * dl;
 #pragma unroll
@@ -1937,16 +2041,8 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         if (lane < NV) {
             W[L.gpp + lane] = tot;
         } else if (lane < NV + NT) {
-            const int idx = lane - NV;
-            int i2 = 0, st = 0;
-#pragma unroll
-            for (int r = 1; r < NV; ++r) {
-                const int sr = r * NV - r * (r - 1) / 2;
-                if (idx >= sr) { i2 = r; st = sr; }
-            }
-            const int j2 = i2 + (idx - st);
-            W[L.FD + i2 * NV + j2] = tot;
-            W[L.FD + j2 * NV + i2] = tot;
+            W[fd_off(0)] = tot;
+            W[fd_off(1)] = tot;
         } else if (lane == NV + NT) {
             X[X_CS] = tot;
         }
@@ -2056,7 +2152,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                 if (bpres(b)) fe = fmax(fe, fabs(shp));
 #pragma unroll
             for (int q = 0; q < RPL; ++q)
-                if (prow(q)) { rp[q] += shp; fe = fmax(fe, fabs(rp[q])); }
+                if (prow(q)) { RP(q) += shp; fe = fmax(fe, fabs(RP(q))); }
             fe = wmax(fe);
             if (lane == 0) X[X_FEASB] = fe;
         }
@@ -2149,7 +2245,11 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         for (int b = 0; b < BPL; ++b) {
             ROW_FENCE(b);
             if (!binrange(b)) continue;
-            const int vi = lane + WAVE * (b >> 1), h = b & 1;
+            int vi = lane + WAVE * (b >> 1);
+            // opaque here: the output addresses are formed after the loop, not hoisted to the
+            // kernel start and carried through it (they were the row wave's scratch spills)
+            asm volatile("" : "+v"(vi));
+            const int h = b & 1;
             const int k = vi / NB, sl = vi - k * NB;
             const real lv = bpres(b) ? lb[b] : 0.0;      // layout per stage: [lower; upper]
             if (sl < NX) {
@@ -2264,10 +2364,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
                             }
                         }
                     }
-                    if (binrange(2 * pv)) {
-                        const int vi = lane + WAVE * pv, k = vi / NB, sl = vi - k * NB;
-                        W[L.Dx + k * NV + (sl < NX ? sl : NS + (sl - NX))] = d;
-                    }
+                    if (binrange(2 * pv)) W[dx_off(pv)] = d;
                 }
                 real vp[NV];
                 load_v(vp, L.xs, L.xu);
@@ -2527,6 +2624,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     STAMP_STORE(16);
 }
+#undef RP
 
 // ==========================================================================================
 // kernel: QPB instances per workgroup, waves [0, QPB) stage waves, [QPB, 2 QPB) row waves
@@ -2569,7 +2667,7 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
         for (int i = threadIdx.x; i < (N + 1) * a.hstride; i += blockDim.x) Hs[i] = a.H[i];
     if (!fpi)
         for (int i = threadIdx.x; i < NV * a.mpad; i += blockDim.x) Fs[i] = a.Fp[i];
-    if (LNG && a.sh_hp >= 0)
+    if (a.sh_hp >= 0)
         for (int r = threadIdx.x; r < a.mp; r += blockDim.x) lds[a.sh_hp + r] = a.hp[r];
     if (LNG && a.sh_bnd >= 0) {
         constexpr int NB = NX + NU;
@@ -2595,7 +2693,7 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
     if (!POL && SPL == 2 && a.redo_flag &&
         !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
         return;                        // mixed mode, cold retry launch: nothing to redo here
-    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, LNG && a.sh_hp >= 0,
+    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, a.sh_hp >= 0,
                                 LNG && a.sh_bnd >= 0, a.H_inst != nullptr);
     real* W = lds + a.shared_doubles + slot * L.total;
     if (fpi && rowwave) {
@@ -2696,9 +2794,11 @@ hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int 
 
 #if BQP_FAM_MG
 hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
-#ifdef BQP_ISA_ONLY_MG10
+#if defined(BQP_ISA_ONLY_MG10)
     // codegen inspection build (make isa): the MG N<64, 616-row instance only
     if (spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st, pol);
+    return hipErrorInvalidValue;
+#elif defined(BQP_ISA_ONLY_DI)
     return hipErrorInvalidValue;
 #else
     return launch_spl<4, 1, 1>(a, spl, rpl, blocks, lds, st, pol);
@@ -2707,7 +2807,13 @@ hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int 
 #endif
 #if BQP_FAM_DI && !defined(BQP_ISA_ONLY_MG10)
 hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
+#ifdef BQP_ISA_ONLY_DI
+    // codegen inspection build (make isa-di): the DI N<64, <= 64-row instance (config C3) only
+    if (spl == 1 && rpl == 1) return launch_t<2, 2, 2, 1, 1, 4>(a, blocks, lds, st, pol);
+    return hipErrorInvalidValue;
+#else
     return launch_spl<2, 2, 2>(a, spl, rpl, blocks, lds, st, pol);
+#endif
 }
 #endif
 
@@ -2758,7 +2864,7 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
     const size_t lds = sizeof(real) * ((size_t)a.shared_doubles +
                                        (size_t)a.wpb * BQP_CAT(ocp_wave_lds_doubles, BQP_SFX)(a.N, nx, nu, np, a.mpad,
                                                                                       a.Fp_inst != nullptr, BQP_LNG_OK && spl == 2,
-                                                                                      BQP_LNG_OK && spl == 2 && a.sh_hp >= 0,
+                                                                                      a.sh_hp >= 0,
                                                                                       BQP_LNG_OK && spl == 2 && a.sh_bnd >= 0,
                                                                                       a.H_inst != nullptr));
     if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st, pol);

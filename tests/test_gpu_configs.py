@@ -5,13 +5,18 @@ C ABI, against the oracle:
       exact z* of ALL 1000 states (tests/golden/lmpc_N20_all.npz, oracle/make_c2_fixture.py)
       and fmincon's stored moves, with the two states where fmincon stopped short (97, 124)
       adjudicated by the fixture (fmincon's move costs more than the exact optimum);
-  C3  trackingMPC DI N=30, batch 4096: the C restatement of the same algorithm, all instances;
+  C3  trackingMPC DI N=30, batch 4096: the C restatement of the same algorithm, all instances,
+      and the exact optimum (first move, theta) of every instance (tests/golden/c3_exact.npz,
+      oracle/make_full_pins.py);
   C4  65 536 perturbed (A, B) models (nominalModel.m:28 perturbed, solved at ocpLMPC.m:24): every
       exit flag equals the exact LDP/NNLS classification (1 feasible, -2 primal infeasible;
       tests/golden/c4_exact.npz, oracle/make_c4_fixture.py), z* of 4101 stored models incl. the
       round-2 reproducers 20712, 11001, 6264, 2008, 7019, and the C restatement on all models;
-  C5  MG DMS N=100, batch 8192, fp64 and mixed: z* first moves of the 64 fixture states,
-      properties at full size (every instance converges, copies of one state agree, KKT).
+  C5  MG DMS N=100, batch 8192, fp64 and mixed: exact first move and theta of all 499 stored
+      states the batch cycles (tests/golden/c5_exact.npz), properties at full size (every
+      instance converges, copies of one state agree, KKT);
+  C4 at N = 80 / 100: the generator's flags equal the exact classification
+      (tests/golden/c4_exact_N{80,100}.npz), z* of the polished and sampled models.
 (C1, the single-instance N=10 LBMPC, is tests/test_gpu_lbmpc.py::test_f3_lbmpc_c1_vs_restatement;
 the reference stores no N=10 fmincon run to pin it to.)"""
 import os
@@ -75,6 +80,11 @@ def test_c3_full_batch_vs_restatement(handle):
     assert np.abs(r.u[:, :-1] - c['u'][:, :-1]).max() < TOL
     assert np.abs(r.x[:, :-1] - c['x'][:, :-1]).max() < TOL
     assert np.abs(r.u - c['u']).max() < 1e-7 and np.abs(r.x - c['x']).max() < 1e-7
+    # independent optimum of every instance (u_{N-1} is not unique: it carries no cost)
+    ex = golden('c3_exact.npz')
+    gi = wl['gidx']
+    assert np.abs(r.u[:, 0, :] - ex['u0'][gi]).max() < TOL
+    assert np.abs(r.theta - ex['theta'][gi]).max() < TOL
 
 
 def test_c4_full_generator(handle):
@@ -113,7 +123,37 @@ def test_c5_full_batch(handle, precision):
     sel = np.array([b for b in range(len(gi)) if int(gi[b]) in pos])
     ust = np.array([g5['u_star'][pos[int(gi[b])]] for b in sel])
     assert np.abs(r.u[sel, 0, 0] + u_eq - ust).max() < TOL
+    # exact first move and theta of every stored state the batch cycles
+    ex = golden('c5_exact.npz')
+    assert np.abs(r.u[:, 0, 0] - ex['u'][gi, 0]).max() < TOL
+    assert np.abs(r.theta - ex['theta'][gi]).max() < TOL
     # copies of one stored state (the batch cycles 499 states) give the same answer
     n = len(g5['x'])
     assert np.abs(r.u[:n] - r.u[n:2 * n]).max() < 1e-12
     assert r.firstorderopt.max() < 1e-6 and r.constrviolation.max() < 1e-9
+
+
+@pytest.mark.parametrize('N', [80, 100])
+def test_c4_generator_long_horizon(handle, N):
+    """the C4 generator (65 536 perturbed models) at N = 80 / 100: every model ends 1 or -2, equal
+    to the exact classification; polished and sampled models at z* (first move and theta 1e-8)"""
+    import bqp
+    from oracle.make_c4_fixture import c4_models
+    from oracle import qp_forms
+    from oracle.mg_model import mg_problem
+    ex = golden('c4_exact_N%d.npz' % N)
+    mg = mg_problem()
+    ts = golden('term_set.npz')
+    lm = bqp.LMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                  mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                  ts['F_w_N'], ts['h_w_N'], N=N)
+    A, B, X = c4_models()
+    r = lm.solve(X, A=A, B=B, handle=handle)
+    hist = {int(k): int((r.exitflag == k).sum()) for k in np.unique(r.exitflag)}
+    print('C4 N=%d: %s, polished %d' % (N, hist, int(r.polished.sum())))
+    assert set(hist) <= {1, -2}, hist
+    assert np.array_equal(r.exitflag == 1, ex['feasible'])
+    zi = ex['z_idx']
+    z = np.concatenate([r.u.reshape(len(X), -1), r.theta], axis=1)[zi]
+    err = np.abs(z - ex['z_star'])
+    assert err[:, 0].max() < TOL and err[:, -1].max() < TOL, (err[:, 0].max(), err[:, -1].max())

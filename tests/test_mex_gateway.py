@@ -197,3 +197,126 @@ def test_ocp_gateway_per_instance_and_options(omex, mg, term_set):
     X, U, th, fval, flag = omex.call(5, _pstruct(omex, prob, hp=hpB), omex.mat(X0.T), opt)
     assert (flag == 1).all()
     assert np.abs(U - ref[1]).max() < 1e-8
+
+
+# ------------------------------------------------------------------ LBMPC gateways
+@pytest.fixture(scope='module')
+def lmex():
+    return Mex('lbmpc')
+
+
+@pytest.fixture(scope='module')
+def loopmex():
+    return Mex('lbmpc_loop')
+
+
+def _lbmpc_obj(mg, N, cls='LBMPC'):
+    import bqp
+    g = golden('lbmpc_instance.npz')
+    if cls == 'LBMPC':
+        return bqp.LBMPC(mg['A'], mg['B'], mg['K'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                         mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                         g['F_w_N'], g['h_w_N'], g['F_x_d'], g['h_x_d'], N=N)
+    return getattr(bqp, cls)(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                             mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                             g['F_w_N'], g['h_w_N'], g['F_x_d'], g['h_x_d'], mg['x_wp'],
+                             mg['u_wp'], N=N)
+
+
+def _lbmpc_struct(m, lb, extra=None):
+    """the model in lbmpc_gpu's MATLAB layout (the lbmpc_solve_gpu.m P struct)"""
+    d = dict(N=lb.N, n_run=lb.n_run, term_learned=int(lb.term_learned), hessian=1, A=lb.A,
+             B=lb.B, K=lb.K, Lq=lb.Lq, Lr=lb.Lr, Lp=lb.Lp, Lt=lb.Lt, LAMBDA=lb.LAMBDA, PSI=lb.PSI,
+             xs=lb.xs, Ain=lb.Ain, bandwidth=lb.bandwidth, **{'lambda': lb.lam})
+    d.update(extra or {})
+    return m.struct(d)
+
+
+def test_lbmpc_gateway_argument_errors(lmex, mg):
+    lb = _lbmpc_obj(mg, 10)
+    x0 = np.zeros((4, 2))
+    win = np.zeros((7, 20))
+    binm = np.repeat(lb.b0[:, None], 2, axis=1)
+    with pytest.raises(MexError) as e:                       # P must be a struct
+        lmex.call(1, lmex.mat(np.eye(2)), lmex.mat(x0), lmex.mat(win), lmex.mat(binm))
+    assert e.value.ident == 'bqp:args'
+    with pytest.raises(MexError) as e:                       # window with 6 rows
+        lmex.call(1, _lbmpc_struct(lmex, lb), lmex.mat(x0), lmex.mat(np.zeros((6, 20))), lmex.mat(binm))
+    assert e.value.ident == 'bqp:dims'
+    with pytest.raises(MexError) as e:                       # bin not m x batch
+        lmex.call(1, _lbmpc_struct(lmex, lb), lmex.mat(x0), lmex.mat(win), lmex.mat(binm[:, :1]))
+    assert e.value.ident == 'bqp:dims'
+    with pytest.raises(MexError) as e:                       # Ain with the wrong column count
+        lmex.call(1, _lbmpc_struct(lmex, lb, dict(Ain=lb.Ain[:, 1:])), lmex.mat(x0), lmex.mat(win),
+                  lmex.mat(binm))
+    assert e.value.ident == 'bqp:dims'
+    with pytest.raises(MexError) as e:                       # a weight factor of the wrong size
+        lmex.call(1, _lbmpc_struct(lmex, lb, dict(Lq=np.eye(3))), lmex.mat(x0), lmex.mat(win),
+                  lmex.mat(binm))
+    assert e.value.ident == 'bqp:dims'
+
+
+def test_lbmpc_loop_gateway_argument_errors(loopmex, mg):
+    mpc = _lbmpc_obj(mg, 10, 'DMSLBMPC')
+    P = dict(bin0=mpc.b0, Bx=mpc.Bx)
+    L = dict(steps=2, delta=0.01, x_eq=mpc.x_eq, u_eq=mpc.u_eq, q=20, mask=1, warm=1)
+    x0 = np.repeat(mpc.x_eq[:, None], 2, axis=1)
+    with pytest.raises(MexError) as e:                       # L must be a struct
+        loopmex.call(1, _lbmpc_struct(loopmex, mpc, P), loopmex.mat(np.eye(2)), loopmex.mat(x0))
+    assert e.value.ident == 'bqp:args'
+    with pytest.raises(MexError) as e:                       # L.q missing
+        Lb = dict(L); del Lb['q']
+        loopmex.call(1, _lbmpc_struct(loopmex, mpc, P), loopmex.struct(Lb), loopmex.mat(x0))
+    assert e.value.ident == 'bqp:args'
+    with pytest.raises(MexError) as e:                       # Bx of the wrong shape
+        loopmex.call(1, _lbmpc_struct(loopmex, mpc, dict(bin0=mpc.b0, Bx=mpc.Bx[:, :3])),
+                     loopmex.struct(L), loopmex.mat(x0))
+    assert e.value.ident == 'bqp:dims'
+    with pytest.raises(MexError) as e:                       # x_init with 3 rows
+        loopmex.call(1, _lbmpc_struct(loopmex, mpc, P), loopmex.struct(L), loopmex.mat(x0[:3]))
+    assert e.value.ident == 'bqp:dims'
+
+
+@pytest.mark.gpu
+def test_lbmpc_gateway_f3_late_solves(lmex, mg):
+    """ocpLBMPC.m:31 through lbmpc_gpu: the 32 late solves of the stored fmincon closed loop
+    LBMPC_N40_sys_full.mat (per-instance 7 x 99 windows in one call) - the same numbers as the
+    Python shim bqp.LBMPC on the same library, first moves within 1e-8 of the restated SQP"""
+    f = golden('lbmpc_N40.npz')
+    lb = _lbmpc_obj(mg, 40)
+    dx = f['late_dx']
+    W = np.asarray(f['late_windows'])               # (batch, 7, q)
+    B, _, q = W.shape
+    binm = (lb.b0[None, :] + dx @ lb.Bx.T).T        # m x batch
+    z, flag, lam, cost, its = lmex.call(5, _lbmpc_struct(lmex, lb, dict(q=q)), lmex.mat(dx.T),
+                                        lmex.mat(np.moveaxis(W, 0, -1)), lmex.mat(binm),
+                                        lmex.mat(None), lmex.struct(dict(max_iter=100, tol=1e-8)))
+    r = lb.solve(dx, W, max_iter=100)
+    assert (flag == 1).all() and (r.exitflag == 1).all()
+    assert np.array_equal(z.T, r.z) and np.array_equal(lam.T, r.lam)
+    assert np.array_equal(its[0], r.iterations)
+    assert np.abs(z[0] - f['late_z_oracle'][:, 0]).max() < 1e-8
+
+
+@pytest.mark.gpu
+def test_lbmpc_loop_gateway_dms(loopmex, mg):
+    """DMS_LBMPC_casadi.m:163-218 through lbmpc_loop_gpu (dms_lbmpc_loop_gpu.m): 6 closed-loop
+    steps for two initial states - the same trajectories, learned predictions, windows and SQP
+    solutions as bqp.closed_loop_sqp on the same library"""
+    import bqp
+    mpc = _lbmpc_obj(mg, 100, 'DMSLBMPC')
+    X_INIT = np.array([[0.15, 1.2875, 1.1547, 0.0], [0.17, 1.30, 1.1547, 0.0]])
+    T, q = 6, 100
+    P = _lbmpc_struct(loopmex, mpc, dict(bin0=mpc.b0, Bx=mpc.Bx))
+    L = loopmex.struct(dict(steps=T, delta=0.01, x_eq=mpc.x_eq, u_eq=mpc.u_eq, q=q, mask=1, warm=1))
+    X, U, E, XL, I, Wn, Z = loopmex.call(7, P, L, loopmex.mat(X_INIT.T),
+                                         loopmex.struct(dict(max_iter=200, tol=1e-8)))
+    r = bqp.closed_loop_sqp(mpc, X_INIT, T, learning=dict(q=q, mask=1), log_z=True)
+    b = len(X_INIT)
+    assert (E == 1).all() and (r.exitflag == 1).all()
+    assert np.array_equal(X.T.reshape(b, T + 1, 4), r.X)
+    assert np.array_equal(U.T.reshape(b, T, 1), r.U)
+    assert np.array_equal(XL.T.reshape(b, T + 1, 4), r.XL)
+    assert np.array_equal(Wn.T.reshape(b, q, 8), r.window)
+    assert np.array_equal(Z.T.reshape(b, T, -1), r.Z)
+    assert np.array_equal(I.T, r.iterations)

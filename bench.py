@@ -177,6 +177,33 @@ def cpu_reference(prob, sample, threads, timed):
                        '-march=native, OpenMP)' % (nall, present, nsh, threads, n1)), kref
 
 
+def cll_cpu_baseline(g, X0, threads):
+    """CPU leg of the CLL line: oracle/cpu_lbmpc.c, the C restatement of the same closed loop
+    (exact-Hessian SQP, dense IPM + polish, RK4 plant, window update; fp64, -O3 -march=native,
+    OpenMP over instances) - 3 steps from the first instances' states, on every host core of the
+    box, on the per-GPU core share and on one core."""
+    from oracle import cpu_lbmpc                  # CPU leg only
+    from oracle.mg_model import mg_problem
+    mg = mg_problem()
+    cpu_lbmpc.lib()
+
+    def rate(nthr, ninst):
+        xi = X0[np.arange(ninst) % len(X0)]
+        t0 = time.perf_counter()
+        cpu_lbmpc.loop(mg, dict(g), 100, 100, 3, xi, threads=nthr)
+        return 3 * ninst / (time.perf_counter() - t0), ninst
+
+    single, n1 = rate(1, 4)
+    present = len(os.sched_getaffinity(0))
+    allc, nall = rate(present, 4 * present)
+    share, nsh = (allc, nall) if threads == present else rate(threads, 4 * threads)
+    return dict(value=round(allc, 2), unit='instance-steps/s', cores=present, kind='port',
+                single_core=round(single, 2), share_value=round(share, 2), share_cores=threads,
+                sample='3 closed-loop steps of %d instances on all %d host cores, %d on the %d-core '
+                       'per-GPU share and %d single-core; oracle/cpu_lbmpc.c (same algorithm, '
+                       'fp64, -O3 -march=native, OpenMP)' % (nall, present, nsh, threads, n1))
+
+
 def free_port():
     import socket
     s = socket.socket()
@@ -569,8 +596,9 @@ def bench_aux(args):
     CL  closed-loop DSS tracking LMPC (N=100, RK4 plant), one step = one batched closed-loop
         step (solve + plant) over --batch initial states; timed over --steps steps of one loop;
     CLL the learned-model NLP loop of DMS_LBMPC_casadi.m (bqp_closed_loop_sqp), same step unit.
-    The CPU leg is the numpy restatement (oracle/lbmpc.py, interpreted) for C1 and the C
-    restatement + numpy RK4 for CL, on a bounded sample."""
+    The CPU leg is the numpy restatement (oracle/lbmpc.py, interpreted) for C1, the C
+    restatement + numpy RK4 for CL and the C restatement of the whole loop (oracle/cpu_lbmpc.c)
+    for CLL, on a bounded sample."""
     import time as _t
     import torch
     import bqp
@@ -739,11 +767,8 @@ def bench_aux(args):
         st = np.load(os.path.join(GOLD, 'dms_lbmpc_loops.npz'))['DMS_tLBMPC_q100']
         e0 = np.abs(r.X[0] - st[:args.steps + 1])
         roof = cll_subproblem_roofline(dl, X0, h)
-        from oracle import lbmpc as olb               # CPU leg only
-        from oracle.mg_model import mg_problem
-        c0 = _t.perf_counter()
-        olb.dms_lbmpc_loop(mg_problem(), dict(g), 100, 100, 3, x_init=X0[1])
-        cpu = 3 / (_t.perf_counter() - c0)
+        present = len(os.sched_getaffinity(0))
+        cpu = cll_cpu_baseline(g, X0, int(os.environ.get('OMP_NUM_THREADS', '0')) or present)
         line = dict(metric='learned-model NLP closed-loop steps/s (DMS_LBMPC_casadi.m, N=100, q=100)',
                     value=round(B * args.steps / el, 1), unit='instance-steps/s', n_gpus=1,
                     steps=args.steps, warmup=1, ms_per_step=round(1e3 * el / args.steps, 4),
@@ -752,8 +777,7 @@ def bench_aux(args):
                     config={'workload': 'CLL: DMS LBMPC closed loop, batch %d, %d steps' % (B, args.steps),
                             'batch_per_gpu': B, 'horizon': 100, 'parallelism': 'dp1'},
                     roofline=roof, kernel_ms=round(kms, 4),
-                    cpu_baseline=dict(value=round(cpu, 3), unit='instance-steps/s', cores=1, kind='port',
-                                      sample='3 steps of one instance, oracle/lbmpc.py dms_lbmpc_loop (numpy)'),
+                    cpu_baseline=cpu,
                     check=dict(converged_frac=float((r.exitflag == 1).mean()),
                                sqp_iterations_mean=float(r.iterations.mean()),
                                sqp_iterations_max=int(r.iterations.max()),

@@ -95,3 +95,21 @@ def test_stored_learned_loops(mg, name, N, q, mask):
     assert (r.exitflag == 1).all(), r.exitflag
     e = np.abs(r.X[0] - st[:T + 1])
     assert e[:, :2].max() < 1e-7 and e.max() < 5e-5, e.max(axis=1)
+
+
+def test_dms_lbmpc_loop_vs_c_restatement(mg):
+    """the GPU loop against the C restatement of the same algorithm (oracle/cpu_lbmpc.c, bench.py's
+    CLL CPU baseline) on 32 perturbed initial states of the CLL bench workload, 6 steps"""
+    import bqp
+    from oracle import cpu_lbmpc
+    rng = np.random.default_rng(11)
+    X0 = X_INIT + rng.uniform(-1, 1, (32, 4)) * np.array([0.005, 0.005, 0.0, 0.0])
+    T = 6
+    r = bqp.closed_loop_sqp(_mpc(mg), X0, T, learning=dict(q=100, mask=1))
+    Xc, Uc, itc, flc = cpu_lbmpc.loop(mg, dict(golden('lbmpc_instance.npz')), 100, 100, T, X0, threads=4)
+    assert (r.exitflag == 1).all() and (flc == 1).all()
+    e = np.abs(r.X - Xc)
+    print('GPU loop vs C restatement: slow %.2e, all %.2e; SQP iterations GPU %.2f C %.2f'
+          % (e[..., :2].max(), e.max(), r.iterations.mean(), itc.mean()))
+    assert e[..., :2].max() < 1e-7
+    assert e.max() < 1e-4

@@ -267,11 +267,16 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
  * measured states are fed back).  x_init (batch*nx), X (batch*(steps+1)*nx) and
  * U (batch*steps*nu) are absolute; exitflag (batch*steps, may be NULL) per solve.
  * Plant BQP_PLANT_MG_RK4: Moore-Greitzer `system` (:215-221) under one RK4 step of length
- * delta (`dynamic`, :297-304); nx = 4, nu = 1.
+ * delta (`dynamic`, :297-304); nx = 4, nu = 1.  BQP_PLANT_MG_ODE23: the same model integrated
+ * over delta by MATLAB's ode23 at its default options (RelTol 1e-3, AbsTol 1e-6, MaxStep
+ * delta/10) - models/trueModel.m:14/48 behind functions/transitionTrue.m, the plant of the
+ * fmincon loops (functions/ocpLMPC.m:11-40, ocpLBMPC.m); with bqp.LMPC's problem this runs
+ * examples/LMPC_RunExample.m's loop.
  * ---------------------------------------------------------------------------------------- */
 #define BQP_PLANT_MG_RK4 1
+#define BQP_PLANT_MG_ODE23 2
 typedef struct {
-    int plant;           /* BQP_PLANT_MG_RK4 */
+    int plant;           /* BQP_PLANT_MG_RK4 or BQP_PLANT_MG_ODE23 */
     int steps;           /* closed-loop steps (mpciterations) */
     double delta;        /* plant step (s) */
     const double* x_eq;  /* nx working point (device memory in the _device variant) */

@@ -14,6 +14,8 @@ from . import _lib
 from .ocp import OcpResult, _default_handle, pack
 
 BQP_PLANT_MG_RK4 = 1
+BQP_PLANT_MG_ODE23 = 2
+_PLANTS = {'rk4': BQP_PLANT_MG_RK4, 'ode23': BQP_PLANT_MG_ODE23}
 
 
 class ClosedLoop(C.Structure):
@@ -26,10 +28,15 @@ class Learning(C.Structure):
                 ('lambda_', C.c_double), ('XL', _lib._PD), ('window', _lib._PD)]
 
 
-def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, **opts):
-    """mpc: a TrackingLMPC / TrackingLBMPC (deviation coordinates around mpc.x_eq, mpc.u_eq);
+def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, plant='rk4',
+                x_eq=None, u_eq=None, **opts):
+    """mpc: a TrackingLMPC / TrackingLBMPC (deviation coordinates around mpc.x_eq, mpc.u_eq), or
+    an LMPC with the working point passed as x_eq / u_eq (functions/ocpLMPC.m: x_wp, u_wp);
     x_init (batch, n) absolute initial states.  Returns X (batch, steps+1, n), U (batch, steps,
     m) absolute, and the per-step exit flags (batch, steps).
+    plant: 'rk4' - one RK4 step per period (`dynamic` of the CasADi scripts); 'ode23' - MATLAB's
+    ode23 at its default options (models/trueModel.m behind transitionTrue.m, the plant of the
+    fmincon loops ocpLMPC.m / ocpLBMPC.m).
 
     learning=dict(q=100, mask=1[, bandwidth, lambda_]) also keeps the learned model's data window
     per instance (bqp_closed_loop_lbmpc: LBMPC_casadi.m:193-198 / DMS_LBMPC_casadi.m:198-207)
@@ -41,10 +48,10 @@ def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, **op
     x_init = np.ascontiguousarray(np.atleast_2d(x_init), dtype=np.float64)
     b = x_init.shape[0]
     prob = mpc.prob
-    dims, data, batch, keep = pack(prob, x_init - mpc.x_eq)
-    xeq = np.ascontiguousarray(mpc.x_eq, dtype=np.float64)
-    ueq = np.ascontiguousarray(mpc.u_eq, dtype=np.float64)
-    cl = ClosedLoop(BQP_PLANT_MG_RK4, int(steps), float(delta), _lib.ptr(xeq), _lib.ptr(ueq))
+    xeq = np.ascontiguousarray(mpc.x_eq if x_eq is None else np.ravel(x_eq), dtype=np.float64)
+    ueq = np.ascontiguousarray(mpc.u_eq if u_eq is None else np.ravel(u_eq), dtype=np.float64)
+    dims, data, batch, keep = pack(prob, x_init - xeq)
+    cl = ClosedLoop(_PLANTS[plant], int(steps), float(delta), _lib.ptr(xeq), _lib.ptr(ueq))
     X = np.zeros((b, steps + 1, prob.nx)); U = np.zeros((b, steps, prob.nu))
     flags = np.zeros((b, steps), np.int32)
     o = _lib.options(**opts)
@@ -67,7 +74,8 @@ def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, **op
 
 
 def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, handle=None,
-                    max_iter=200, tol=1e-8, log_z=False):
+                    max_iter=200, tol=1e-8, log_z=False, plant='rk4', x_eq=None,
+                    u_eq=None):
     """Learned-model NLP closed loop on the GPU (bqp_closed_loop_sqp): per step the batched
     Gauss-Newton SQP of mpc (a DMSLBMPC - DMS_LBMPC_casadi.m:163-218 -, HybridLBMPC -
     hybrid_LBMPC_casadi.m:163-204 - or LBMPC) at the measured states, one RK4 plant step with the
@@ -76,6 +84,9 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
     window (only the first, zero point valid at the start), mask 0 counts every point (the 7-row
     window of hybrid_LBMPC_casadi.m).  warm: the scripts' shifted guess (previous inputs moved one
     stage, zero last move, theta kept); otherwise z = 0 each step.
+    plant: 'rk4' (the CasADi scripts' `dynamic`) or 'ode23' (models/trueModel.m, the fmincon loop
+    functions/ocpLBMPC.m; its update_data.m window of q points equals this ring with q - 1: the
+    initial zero point leaves when the q-th sample arrives).
     Returns X (batch, steps+1, n), U (batch, steps, m) absolute, exitflag and iterations (batch,
     steps), XL (batch, steps+1, n) the learned one-step predictions, window (batch, q, 8) the
     final windows in ring order, and with log_z every step's solution Z (batch, steps, nz)."""
@@ -86,8 +97,11 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
     b = x_init.shape[0]
     q = int(learning.get('q', 100))
     mask = int(learning.get('mask', 1))
-    x_eq = np.ascontiguousarray(getattr(mpc, 'x_eq', np.zeros(mpc.n)), dtype=np.float64)
-    u_eq = np.ascontiguousarray(getattr(mpc, 'u_eq', np.zeros(mpc.m)), dtype=np.float64)
+    # working point: the caller's (LBMPC, ocpLBMPC.m's x_wp / u_wp), else the shim's own
+    x_eq = np.ascontiguousarray(getattr(mpc, 'x_eq', np.zeros(mpc.n)) if x_eq is None else np.ravel(x_eq),
+                                dtype=np.float64)
+    u_eq = np.ascontiguousarray(getattr(mpc, 'u_eq', np.zeros(mpc.m)) if u_eq is None else np.ravel(u_eq),
+                                dtype=np.float64)
     mrows = mpc.Ain.shape[0]
     keep = [np.ascontiguousarray(a, dtype=np.float64) for a in
             (mpc.A.T, mpc.B.T, mpc.K.T, mpc.Lq, mpc.Lr, mpc.Lp, mpc.Lt, mpc.LAMBDA.T, mpc.PSI.T,
@@ -103,7 +117,7 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
     flags = np.zeros((b, steps), np.int32); its = np.zeros((b, steps), np.int32)
     Z = np.zeros((b, steps, mpc.nz)) if log_z else None
     sl = _lib.SqpLoop(_lib.ptr(bin0), _lib.ptr(Bx), int(bool(warm)), _lib.ptr(Z), _lib.iptr(its))
-    cl = ClosedLoop(BQP_PLANT_MG_RK4, int(steps), float(delta), _lib.ptr(x_eq), _lib.ptr(u_eq))
+    cl = ClosedLoop(_PLANTS[plant], int(steps), float(delta), _lib.ptr(x_eq), _lib.ptr(u_eq))
     lw = Learning(q, mask, float(learning.get('bandwidth', 0.0)), float(learning.get('lambda_', 0.0)),
                   _lib.ptr(XL), _lib.ptr(win))
     o = _lib.options(max_iter=max_iter, tol_stat=tol)

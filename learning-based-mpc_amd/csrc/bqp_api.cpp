@@ -793,7 +793,7 @@ static int closed_loop_impl(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
     if (!h || !cl || !x_init || !X || !U) return BQP_E_ARG;
     int rc = ocp_check(d, batch, D);
     if (rc) return rc;
-    if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
+    if ((cl->plant != BQP_PLANT_MG_RK4 && cl->plant != BQP_PLANT_MG_ODE23) || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
         return BQP_E_ARG;
     if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;   // the MG plant
     if (lw && (lw->q < 1 || lw->q > (1 << 20) || !lw->XL)) return BQP_E_ARG;
@@ -827,7 +827,7 @@ static int closed_loop_impl(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
                                           nullptr, stream);
         if (rc) return rc;
         launches += h->launches + (lw ? 2 : 1);
-        HIP_TRY(bqp::launch_mg_plant(batch, N, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
+        HIP_TRY(bqp::launch_mg_plant(cl->plant, batch, N, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
                                      s, X, U, exitflag, st));
         if (lw)
             HIP_TRY(bqp::launch_lbmpc_window(batch, cl->steps, t, lw->q, bw, lam, D->A, D->sA, D->B,
@@ -867,7 +867,7 @@ static int closed_loop_host(bqp_handle h, const bqp_ocp_dims* d, int batch, cons
     int rc = ocp_check(d, batch, D);
     if (rc) return rc;
     // validate the loop description before sizing the staging buffers from it
-    if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
+    if ((cl->plant != BQP_PLANT_MG_RK4 && cl->plant != BQP_PLANT_MG_ODE23) || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
         return BQP_E_ARG;
     if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;
     DevScope ds(h->device);
@@ -954,7 +954,7 @@ static int sqp_loop_check(const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_da
                           const bqp_learning* lw, const double* x_init, const double* X,
                           const double* U) {
     if (!d || !D || !sl || !cl || !lw || !x_init || !X || !U || batch <= 0) return BQP_E_ARG;
-    if (cl->plant != BQP_PLANT_MG_RK4 || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
+    if ((cl->plant != BQP_PLANT_MG_RK4 && cl->plant != BQP_PLANT_MG_ODE23) || cl->steps <= 0 || !(cl->delta > 0) || !cl->x_eq || !cl->u_eq)
         return BQP_E_ARG;
     if (d->nx != 4 || d->nu != 1) return BQP_E_UNSUPPORTED;   // the MG plant
     if (lw->q != d->q || !lw->XL || (lw->mask != 0 && lw->mask != 1)) return BQP_E_ARG;
@@ -1019,7 +1019,7 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
         launches += h->launches;
         HIP_TRY(bqp::launch_sqp_loop_u0(batch, nx, n, D->K, s, z, uo, it, cl->steps, t,
                                         sl->Z, sl->iterations, st));
-        HIP_TRY(bqp::launch_mg_plant(batch, 1, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
+        HIP_TRY(bqp::launch_mg_plant(cl->plant, batch, 1, cl->steps, t, cl->delta, uo, fl, cl->x_eq, cl->u_eq,
                                      s, X, U, exitflag, st));
         HIP_TRY(bqp::launch_lbmpc_window(batch, cl->steps, t, q, bw, lam, D->A, 0, D->B, 0,
                                          cl->x_eq, cl->u_eq, X, U, win, lw->XL, st));

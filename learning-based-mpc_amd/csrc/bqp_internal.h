@@ -133,12 +133,13 @@ hipError_t launch_lbmpc_normal(const LbmpcArgs& a, hipStream_t st);
 hipError_t launch_lbmpc_update(const LbmpcArgs& a, hipStream_t st);
 hipError_t launch_lbmpc_hess(const LbmpcArgs& a, hipStream_t st);
 
-// closed-loop simulation (bqp_plant.hip): Moore-Greitzer RK4 plant between batched solves
+// closed-loop simulation (bqp_plant.hip): Moore-Greitzer plant (RK4 step or MATLAB ode23,
+// BQP_PLANT_*) between batched solves
 hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* xinit,
                                    const double* xeq, double* s, double* X, hipStream_t st);
-hipError_t launch_mg_plant(int batch, int N, int steps, int t, double delta, const double* uo,
-                           const int* fl, const double* xeq, const double* ueq, double* s,
-                           double* X, double* U, int* flags, hipStream_t st);
+hipError_t launch_mg_plant(int plant, int batch, int N, int steps, int t, double delta,
+                           const double* uo, const int* fl, const double* xeq, const double* ueq,
+                           double* s, double* X, double* U, int* flags, hipStream_t st);
 // learned-model NLP closed loop glue (bqp_closed_loop_sqp): per instance bin = bin0 + Bx s and
 // the warm start (z shifted one stage, zero last move, theta kept) before the SQP; u_0 = K s + z_0
 // for the plant, and the step's z / iteration count into the caller's logs after it

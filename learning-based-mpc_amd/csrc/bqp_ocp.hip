@@ -903,75 +903,50 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
         wave_sync();
         STAMP(10);
-        // backward sweep p_k = Phi_k' p_{k+1} + qh_k with Phi_k = Abar + Bbar K_k: EVERY lane
-        // computes the whole vector from uniform (broadcast) LDS reads - no cross-lane traffic on
-        // the sequential chain (round 3: lane i formed entry i and readlane broadcast the vector,
-        // ~250 cycles per stage).  Abar = [A 0; 0 I], Bbar = [B; 0] (the per-instance model in
-        // LDS), so Phi_k' p = [A' p_x; p_th] + K_k' (B' p_x): NX^2 + NX NU + NS NU FMAs in
-        // NS + NU independent chains.  Lanes < NS store their entry.
+        // backward sweep: lane i < NS computes entry i of p_k = Phi_k' p_{k+1} + qh_k; the new
+        // vector is broadcast with readlane (scalar registers); two register sets used
+        // alternately (stages k, k-1), each refilled two stages ahead.  (Round 4 tried every
+        // lane forming the whole vector from broadcast LDS reads, no readlane on the chain: the
+        // sweeps are issue-bound at one instance per SIMD, and the 3x longer instruction
+        // stream cost 9.4k -> 14.6k cycles per iteration)
         {
-            real Am[NX][NX], Bm[NX][NU];
+            real Acol[NS], Bl[NS][NU];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) {
+            for (int c = 0; c < NS; ++c) {
+                Acol[c] = Abar(c, li);
 #pragma unroll
-                for (int c = 0; c < NX; ++c) Am[i][c] = Abar(i, c);
-#pragma unroll
-                for (int x = 0; x < NU; ++x) Bm[i][x] = Bbar(i, x);
+                for (int x = 0; x < NU; ++x) Bl[c][x] = Bbar(c, x);
             }
             real p[NS];
 #pragma unroll
             for (int i = 0; i < NS; ++i) p[i] = W[L.pv + N * NS + i];
-            struct BS { real q[NS], kk[NU][NS]; };
-            auto load_b = [&](int k, BS& o) __attribute__((always_inline)) {
+            auto load_b = [&](int k, real (&kc)[NU], real& q) __attribute__((always_inline)) {
+                q = W[L.qt_xpi + k * NS + li];
 #pragma unroll
-                for (int i = 0; i < NS; ++i) o.q[i] = W[L.qt_xpi + k * NS + i];
-#pragma unroll
-                for (int x = 0; x < NU; ++x)
-#pragma unroll
-                    for (int i = 0; i < NS; ++i) o.kk[x][i] = W[L.K + k * NU * NS + x * NS + i];
+                for (int x = 0; x < NU; ++x) kc[x] = W[L.K + k * NU * NS + x * NS + li];
             };
-            BS b0, b1;
-            load_b(N - 1, b0);
-            if (N >= 2) load_b(N - 2, b1);
-            auto step_b = [&](int k, const BS& o) __attribute__((always_inline)) {
-                real sb[NU];                                  // B' p_x
+            real k0[NU], q0, k1[NU], q1;
+            load_b(N - 1, k0, q0);
+            if (N >= 2) load_b(N - 2, k1, q1);
+            auto step_b = [&](int k, const real (&kc)[NU], real q) __attribute__((always_inline)) {
+                real acc = q;
 #pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    real t = Bm[0][x] * p[0];
+                for (int c = 0; c < NS; ++c) {
+                    real ph = Acol[c];
 #pragma unroll
-                    for (int c = 1; c < NX; ++c) t = fmar(Bm[c][x], p[c], t);
-                    sb[x] = t;
+                    for (int x = 0; x < NU; ++x) ph += Bl[c][x] * kc[x];
+                    acc += ph * p[c];
                 }
-                real o2[NS];
+                if (lane < NS) W[L.pv + k * NS + lane] = acc;
 #pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    real v = o.q[j];
-                    if (j < NX) {
-#pragma unroll
-                        for (int c = 0; c < NX; ++c) v = fmar(Am[c][j], p[c], v);
-                    } else {
-                        v += p[j];
-                    }
-                    o2[j] = v;
-                }
-#pragma unroll
-                for (int j = 0; j < NS; ++j) {
-                    real v = o2[j];
-#pragma unroll
-                    for (int x = 0; x < NU; ++x) v = fmar(o.kk[x][j], sb[x], v);
-                    p[j] = v;
-                }
-                real mine = p[0];
-#pragma unroll
-                for (int j = 1; j < NS; ++j) mine = (lane == j) ? p[j] : mine;
-                if (lane < NS) W[L.pv + k * NS + lane] = mine;
+                for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
             };
             for (int k = N - 1; k >= 0; k -= 2) {
-                step_b(k, b0);
-                if (k >= 2) load_b(k - 2, b0);
+                step_b(k, k0, q0);
+                if (k >= 2) load_b(k - 2, k0, q0);
                 if (k == 0) break;
-                step_b(k - 1, b1);
-                if (k >= 3) load_b(k - 3, b1);
+                step_b(k - 1, k1, q1);
+                if (k >= 3) load_b(k - 3, k1, q1);
             }
         }
         wave_sync();
@@ -1005,7 +980,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         }
         wave_sync();
         STAMP(12);
-        // theta_0 step + forward sweep ds_{k+1} = Phi_k ds_k + f_k
+        // theta_0 step + forward sweep: lane i < NS computes entry i of ds_{k+1} = Phi_k ds_k + f_k
         {
             real d[NS];
 #pragma unroll
@@ -1020,69 +995,40 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #pragma unroll
                 for (int i = 0; i < NS; ++i) W[ods + i] = d[i];
             }
-            // forward sweep ds_{k+1} = Phi_k ds_k + f_k, every lane the whole vector (as the
-            // backward sweep): Phi_k d = [A d_x + B (K_k d); d_th]
-            real Am[NX][NX], Bm[NX][NU];
+            real Arow[NS], Bli[NU];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) {
+            for (int c = 0; c < NS; ++c) Arow[c] = Abar(li, c);
 #pragma unroll
-                for (int c = 0; c < NX; ++c) Am[i][c] = Abar(i, c);
-#pragma unroll
-                for (int x = 0; x < NU; ++x) Bm[i][x] = Bbar(i, x);
-            }
-            struct FS { real f[NS], kk[NU][NS]; };
-            auto load_f = [&](int k, FS& o) __attribute__((always_inline)) {
-#pragma unroll
-                for (int i = 0; i < NS; ++i) o.f[i] = W[L.fv + k * NS + i];
+            for (int x = 0; x < NU; ++x) Bli[x] = Bbar(li, x);
+            auto load_f = [&](int k, real (&kr)[NU][NS], real& f) __attribute__((always_inline)) {
+                f = W[L.fv + k * NS + li];
 #pragma unroll
                 for (int x = 0; x < NU; ++x)
 #pragma unroll
-                    for (int c = 0; c < NS; ++c) o.kk[x][c] = W[L.K + k * NU * NS + x * NS + c];
+                    for (int c = 0; c < NS; ++c) kr[x][c] = W[L.K + k * NU * NS + x * NS + c];
             };
-            FS f0, f1;
-            load_f(0, f0);
-            if (N >= 2) load_f(1, f1);
-            auto step_f = [&](int k, const FS& o) __attribute__((always_inline)) {
-                real kd[NU];                                  // K_k d
+            real k0[NU][NS], f0, k1[NU][NS], f1;
+            load_f(0, k0, f0);
+            if (N >= 2) load_f(1, k1, f1);
+            auto step_f = [&](int k, const real (&kr)[NU][NS], real f) __attribute__((always_inline)) {
+                real acc = f;
 #pragma unroll
-                for (int x = 0; x < NU; ++x) {
-                    real t = o.kk[x][0] * d[0];
+                for (int c = 0; c < NS; ++c) {
+                    real ph = Arow[c];
 #pragma unroll
-                    for (int c = 1; c < NS; ++c) t = fmar(o.kk[x][c], d[c], t);
-                    kd[x] = t;
+                    for (int x = 0; x < NU; ++x) ph += Bli[x] * kr[x][c];
+                    acc += ph * d[c];
                 }
-                real o2[NS];
+                if (lane < NS) W[ods + (k + 1) * NS + lane] = acc;
 #pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    real v = o.f[i];
-                    if (i < NX) {
-#pragma unroll
-                        for (int c = 0; c < NX; ++c) v = fmar(Am[i][c], d[c], v);
-                    } else {
-                        v += d[i];
-                    }
-                    o2[i] = v;
-                }
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    real v = o2[i];
-                    if (i < NX) {
-#pragma unroll
-                        for (int x = 0; x < NU; ++x) v = fmar(Bm[i][x], kd[x], v);
-                    }
-                    d[i] = v;
-                }
-                real mine = d[0];
-#pragma unroll
-                for (int i = 1; i < NS; ++i) mine = (lane == i) ? d[i] : mine;
-                if (lane < NS) W[ods + (k + 1) * NS + lane] = mine;
+                for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
             };
             for (int k = 0; k < N; k += 2) {
-                step_f(k, f0);
-                if (k + 2 < N) load_f(k + 2, f0);
+                step_f(k, k0, f0);
+                if (k + 2 < N) load_f(k + 2, k0, f0);
                 if (k + 1 >= N) break;
-                step_f(k + 1, f1);
-                if (k + 3 < N) load_f(k + 3, f1);
+                step_f(k + 1, k1, f1);
+                if (k + 3 < N) load_f(k + 3, k1, f1);
             }
         }
         wave_sync();

@@ -2,12 +2,17 @@
 // batched solves (bqp_closed_loop_ocp_device).
 //
 // Moore-Greitzer compressor (examples/DMS_tracking_LMPC_casadi.m:215-221, `system`; the same
-// model as models/trueModel.m:32-41) integrated by one classical RK4 step of length delta
-// (`dynamic`, :297-304).  One thread per instance: the plant is 4 states, the solve dominates.
+// model as models/trueModel.m:32-41) integrated over one sampling period delta by
+//   BQP_PLANT_MG_RK4    one classical RK4 step (`dynamic`, :297-304) - the CasADi scripts;
+//   BQP_PLANT_MG_ODE23  MATLAB's ode23 with its default options (trueModel.m:14/48,
+//                       simulate_cont) - the fmincon loops ocpLMPC.m / ocpLBMPC.m through
+//                       transitionTrue.m.
+// One thread per instance: the plant is 4 states, the solve dominates.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
 
+#include "../../include/bqp.h"
 #include "bqp_internal.h"
 
 namespace bqp {
@@ -35,6 +40,89 @@ __device__ __forceinline__ void mg_rk4(double delta, double (&x)[4], double u) {
     for (int i = 0; i < 4; ++i) x[i] = x[i] + delta / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
 }
 
+// MATLAB ode23 over [0, T] from y with the input held: the Bogacki-Shampine 3(2) pair with
+// first-same-as-last, local extrapolation and the step-size control of the MATLAB ODE suite
+// (Shampine & Reichelt 1997) at the defaults RelTol 1e-3, AbsTol 1e-6 (threshold AbsTol/RelTol),
+// MaxStep 0.1 T; initial step min(MaxStep, T) capped by 0.8 RelTol^(1/3) / |f0 / max(|y|, thr)|;
+// a step within 10 % of the end is stretched to it.  Error estimate
+// err = h |f E ./ max(|y|, |ynew|, thr)|_inf with E = [-5/72 1/12 1/9 -1/8]; a failed step
+// shrinks h by max(0.5, 0.8 (RelTol/err)^(1/3)) the first time, by 0.5 after; a step without
+// failure grows h by 1 / (1.25 (err/RelTol)^(1/3)), at most 5x.  The restatement
+// (oracle/mg_model.py mg_ode23) reproduces every stored transition x_k -> x_{k+1} of the
+// reference's fmincon runs (LMPC_N20/40/50, LBMPC_N40/50_sys_full.mat) to 1.4e-15.
+__device__ void mg_ode23(double T, double (&y)[4], double u) {
+    constexpr double rtol = 1e-3, thr = 1e-6 / 1e-3;
+    constexpr double E0 = -5.0 / 72.0, E1 = 1.0 / 12.0, E2 = 1.0 / 9.0, E3 = -1.0 / 8.0;
+    const double pw = 1.0 / 3.0, hmax = 0.1 * T;
+    double F0[4], F1[4], F2[4], F3[4], ys[4], yn[4];
+    mg_system(y, u, F0);
+    double absh = fmin(hmax, T), rh = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rh = fmax(rh, fabs(F0[i] / fmax(fabs(y[i]), thr)));
+    rh /= 0.8 * pow(rtol, pw);
+    if (absh * rh > 1.0) absh = 1.0 / rh;
+    double t = 0.0;
+    bool done = false;
+    // at most 4096 step attempts (the MG plant takes 10-14 per 0.01 s sampling period)
+    for (int guard = 0; !done && guard < 4096; ++guard) {
+        const double hmin = 16.0 * (nextafter(t, INFINITY) - t);
+        absh = fmin(hmax, fmax(hmin, absh));
+        double h = absh;
+        if (1.1 * absh >= fabs(T - t)) {
+            h = T - t;
+            absh = fabs(h);
+            done = true;
+        }
+        bool nofailed = true;
+        double err = 0.0;
+        for (;; ++guard) {
+            const double h1 = h * 0.5, h2 = h * 0.75;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ys[i] = y[i] + F0[i] * h1;
+            mg_system(ys, u, F1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ys[i] = y[i] + F1[i] * h2;
+            mg_system(ys, u, F2);
+            const double tnew = done ? T : t + h;
+            h = tnew - t;
+            const double b0 = h * (2.0 / 9.0), b1 = h * (1.0 / 3.0), b2 = h * (4.0 / 9.0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) yn[i] = y[i] + (F0[i] * b0 + F1[i] * b1 + F2[i] * b2);
+            mg_system(yn, u, F3);
+            double e = 0.0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double fe = F0[i] * E0 + F1[i] * E1 + F2[i] * E2 + F3[i] * E3;
+                e = fmax(e, fabs(fe / fmax(fmax(fabs(y[i]), fabs(yn[i])), thr)));
+            }
+            err = absh * e;
+            if (!(err > rtol)) {
+                t = tnew;
+                break;
+            }
+            if (absh <= hmin || guard >= 4096) {   // MATLAB warns and returns here
+                done = true;
+                t = tnew;
+                break;
+            }
+            absh = nofailed ? fmax(hmin, absh * fmax(0.5, 0.8 * pow(rtol / err, pw)))
+                            : fmax(hmin, 0.5 * absh);
+            nofailed = false;
+            h = absh;
+            done = false;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            y[i] = yn[i];
+            F0[i] = F3[i];
+        }
+        if (!done && nofailed) {
+            const double temp = 1.25 * pow(err / rtol, pw);
+            absh = temp > 0.2 ? absh / temp : 5.0 * absh;
+        }
+    }
+}
+
 // s (deviation state fed to the solver) = x_init - x_eq; X[:, 0] = x_init
 __global__ void closed_loop_init_kernel(int batch, int nx, int steps, const double* xinit,
                                         const double* xeq, double* s, double* X) {
@@ -47,8 +135,8 @@ __global__ void closed_loop_init_kernel(int batch, int nx, int steps, const doub
     }
 }
 
-// apply u_0 of the step-t solve to the plant: u = u_eq + du_0, x+ = RK4(x, u)
-__global__ void mg_plant_kernel(int batch, int N, int steps, int t, double delta,
+// apply u_0 of the step-t solve to the plant: u = u_eq + du_0, x+ = RK4(x, u) or ode23
+__global__ void mg_plant_kernel(int plant, int batch, int N, int steps, int t, double delta,
                                 const double* uo, const int* fl, const double* xeq,
                                 const double* ueq, double* s, double* X, double* U, int* flags) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -57,7 +145,8 @@ __global__ void mg_plant_kernel(int batch, int N, int steps, int t, double delta
 #pragma unroll
     for (int i = 0; i < 4; ++i) x[i] = s[(int64_t)b * 4 + i] + xeq[i];
     const double u = uo[(int64_t)b * N] + ueq[0];
-    mg_rk4(delta, x, u);
+    if (plant == BQP_PLANT_MG_ODE23) mg_ode23(delta, x, u);
+    else mg_rk4(delta, x, u);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         s[(int64_t)b * 4 + i] = x[i] - xeq[i];
@@ -229,10 +318,10 @@ hipError_t launch_closed_loop_init(int batch, int nx, int steps, const double* x
     return hipGetLastError();
 }
 
-hipError_t launch_mg_plant(int batch, int N, int steps, int t, double delta, const double* uo,
-                           const int* fl, const double* xeq, const double* ueq, double* s,
-                           double* X, double* U, int* flags, hipStream_t st) {
-    hipLaunchKernelGGL(mg_plant_kernel, dim3((batch + 255) / 256), dim3(256), 0, st, batch, N,
+hipError_t launch_mg_plant(int plant, int batch, int N, int steps, int t, double delta,
+                           const double* uo, const int* fl, const double* xeq, const double* ueq,
+                           double* s, double* X, double* U, int* flags, hipStream_t st) {
+    hipLaunchKernelGGL(mg_plant_kernel, dim3((batch + 255) / 256), dim3(256), 0, st, plant, batch, N,
                        steps, t, delta, uo, fl, xeq, ueq, s, X, U, flags);
     return hipGetLastError();
 }

@@ -137,3 +137,60 @@ def mg_rk4(delta, x, u):
     k3 = mg_rhs(x + delta / 2 * k2, u)
     k4 = mg_rhs(x + delta * k3, u)
     return x + delta / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+
+
+def mg_ode23(delta, x, u, rtol=1e-3, atol=1e-6):
+    """True-plant step of the fmincon loops: models/trueModel.m:14/48 (simulate_cont) integrates
+    the MG model over [0, delta] with MATLAB's ode23 at its default options.  Restated from the
+    published algorithm (Bogacki-Shampine 3(2) pair, FSAL, local extrapolation; the MATLAB ODE
+    suite's initial step and step-size control, Shampine & Reichelt 1997): MaxStep 0.1 delta,
+    threshold AbsTol/RelTol, error h |f E ./ max(|y|, |ynew|, thr)|_inf, E = [-5/72 1/12 1/9
+    -1/8], the last step stretched when within 10 % of the end.  Pinned: it reproduces every
+    stored transition of LMPC_N{20,40,50}_sys_full.mat and LBMPC_N{40,50}_sys_full.mat to
+    1.4e-15 (tests/test_oracle.py).  Returns x(delta)."""
+    f = lambda y: mg_rhs(y, u)                                    # noqa: E731
+    t, y = 0.0, np.array(x, float)
+    T = float(delta)
+    hmax, thr, pw = 0.1 * T, atol / rtol, 1.0 / 3.0
+    Bt = np.array([[1 / 2, 0, 2 / 9], [0, 3 / 4, 1 / 3], [0, 0, 4 / 9], [0, 0, 0]])
+    E = np.array([-5 / 72, 1 / 12, 1 / 9, -1 / 8])
+    F = np.zeros((4, 4))
+    F[:, 0] = f(y)
+    absh = min(hmax, T)
+    rh = np.max(np.abs(F[:, 0] / np.maximum(np.abs(y), thr))) / (0.8 * rtol ** pw)
+    if absh * rh > 1:
+        absh = 1 / rh
+    done = False
+    while not done:
+        hmin = 16 * np.spacing(t)
+        absh = min(hmax, max(hmin, absh))
+        h = absh
+        if 1.1 * absh >= abs(T - t):
+            h = T - t
+            absh = abs(h)
+            done = True
+        nofailed = True
+        while True:
+            hB = h * Bt
+            F[:, 1] = f(y + F @ hB[:, 0])
+            F[:, 2] = f(y + F @ hB[:, 1])
+            tnew = T if done else t + h
+            h = tnew - t
+            ynew = y + F @ (h * Bt[:, 2])
+            F[:, 3] = f(ynew)
+            err = absh * np.max(np.abs((F @ E) / np.maximum(np.maximum(np.abs(y), np.abs(ynew)), thr)))
+            if not err > rtol:
+                break
+            if absh <= hmin:
+                break                                             # MATLAB warns and returns
+            absh = max(hmin, absh * max(0.5, 0.8 * (rtol / err) ** pw)) if nofailed \
+                else max(hmin, 0.5 * absh)
+            nofailed = False
+            h = absh
+            done = False
+        if not done and nofailed:
+            temp = 1.25 * (err / rtol) ** pw
+            absh = absh / temp if temp > 0.2 else 5.0 * absh
+        t, y = tnew, ynew
+        F[:, 0] = F[:, 3]
+    return y

@@ -60,3 +60,35 @@ def test_f3_late_solves_batched(mg, handle, N):
     r = lb.solve(f['late_dx'], f['late_windows'], handle=handle, max_iter=100)
     _check(r, f['late_dx'], f['late_du_matlab'], f['late_z_oracle'], f['late_err_vs_matlab'],
            mg['K'])
+
+
+def test_f3_fmincon_loop_end_to_end(mg):
+    """examples/LBMPC_RunExample.m's loop regenerated on the GPU (bqp_closed_loop_sqp): per step
+    the F3 SQP at the measured state (ocpLBMPC.m:27-31), u = K dx + c_0 + u_wp to the true plant
+    (transitionTrue.m -> models/trueModel.m: MATLAB ode23, BQP_PLANT_MG_ODE23), then the window
+    update of ocpLBMPC.m:12-19 / update_data.m with q = 100 - which keeps q - 1 = 99 points once
+    full (the initial zero point leaves when the 100th sample arrives), i.e. the loop's ring with
+    q = 99 and the validity row.  1000 steps from the stored x_init against the stored run
+    LBMPC_N40_sys_full.mat (column k + 1: the state of step k and fmincon's move)."""
+    import bqp
+    from oracle.mg_model import mg_ode23
+    H = golden('fmincon_runs.npz')['LBMPC_N40']
+    xwp = np.asarray(mg['x_wp'], float); uwp = np.ravel(mg['u_wp'])[:1].astype(float)
+    lb = _lbmpc(mg, 40)
+    Xs = H[:4, 1:].T + xwp                          # states of steps 1..1000
+    Us = H[4, 1:] + uwp
+    T = len(Us)
+    r = bqp.closed_loop_sqp(lb, Xs[:1], T, learning=dict(q=99, mask=1), plant='ode23',
+                            x_eq=xwp, u_eq=uwp)
+    assert (r.exitflag == 1).all()
+    ep = max(np.abs(mg_ode23(0.01, r.X[0, k], r.U[0, k, 0]) - r.X[0, k + 1]).max()
+             for k in range(0, T, 9))
+    e = np.abs(r.X[0, :T] - Xs)
+    eu = np.abs(r.U[0, :, 0] - Us)
+    print('LBMPC N=40 fmincon loop on the GPU: plant kernel vs restatement %.2e; vs '
+          'LBMPC_N40_sys_full.mat: slow states %.2e, all states %.2e (k >= 200: %.2e), moves '
+          'median %.2e max %.2e; SQP iterations mean %.2f max %d'
+          % (ep, e[:, :2].max(), e.max(), e[200:].max(), np.median(eu), eu.max(),
+             r.iterations.mean(), r.iterations.max()))
+    assert ep < 1e-13
+    assert e[:, :2].max() < 5e-3

@@ -111,3 +111,18 @@ def test_lbmpc_instance_fixture():
     assert g['y_OL'].shape == (505,)
     assert g['data'].shape == (7, 100)
     assert g['F_w_N'].shape == (16, 5)
+
+
+@pytest.mark.parametrize('name', ['LMPC_N20', 'LMPC_N40', 'LMPC_N50', 'LBMPC_N40', 'LBMPC_N50'])
+def test_ode23_plant_reproduces_stored_transitions(mg, name):
+    """the ode23 restatement (oracle/mg_model.py mg_ode23, models/trueModel.m:14/48) against every
+    transition of the reference's stored fmincon runs: x_{k+1} = ode23(x_k, u_k) to round-off"""
+    from oracle.mg_model import mg_ode23
+    H = golden('fmincon_runs.npz')[name]
+    xwp = np.asarray(mg['x_wp'], float); uwp = float(np.ravel(mg['u_wp'])[0])
+    if name.startswith('LMPC'):       # column k+1: state after step k, move of step k
+        pairs = [(H[:4, k], H[4, k + 1], H[:4, k + 1]) for k in range(H.shape[1] - 1)]
+    else:                             # column k+1: state of step k and its move
+        pairs = [(H[:4, k], H[4, k], H[:4, k + 1]) for k in range(1, H.shape[1] - 1)]
+    err = max(np.abs(mg_ode23(0.01, x + xwp, u + uwp) - (xn + xwp)).max() for x, u, xn in pairs)
+    assert err < 5e-15, err

@@ -18,7 +18,8 @@ import numpy as np
 import bqp
 from bqp import _lib
 
-_lib.LIB_PATH = os.path.join(ROOT, 'learning-based-mpc_amd', 'build', 'stamps', 'libbqp_stamps.so')
+_lib.LIB_PATH = os.environ.get('BQP_STAMPS_LIB') or os.path.join(ROOT, 'learning-based-mpc_amd', 'build', 'stamps',
+                                                                 'libbqp_stamps.so')
 lib = _lib.load()
 lib.bqp_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _lib._PD]
 import bench

@@ -768,7 +768,7 @@ def bench_aux(args):
         e0 = np.abs(r.X[0] - st[:args.steps + 1])
         roof = cll_subproblem_roofline(dl, X0, h)
         present = len(os.sched_getaffinity(0))
-        cpu = cll_cpu_baseline(g, X0, int(os.environ.get('OMP_NUM_THREADS', '0')) or present)
+        cpu = None if args.no_cpu else cll_cpu_baseline(g, X0, int(os.environ.get('OMP_NUM_THREADS', '0')) or present)
         line = dict(metric='learned-model NLP closed-loop steps/s (DMS_LBMPC_casadi.m, N=100, q=100)',
                     value=round(B * args.steps / el, 1), unit='instance-steps/s', n_gpus=1,
                     steps=args.steps, warmup=1, ms_per_step=round(1e3 * el / args.steps, 4),

@@ -206,7 +206,7 @@ struct QpLds {
     // shared tables when the batch shares them (hpsh, bndsh).  The polytope rhs is in the
     // shared tables whenever the batch shares it (hpsh, every horizon).
     // hinst: per-instance stage-cost table (bqp_ocp_data.sW != 0) in the slot (short horizons)
-    __host__ __device__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false,
+    __host__ __device__ __forceinline__ static QpLds make(int N, int NX, int NU, int NP, int mpad, bool fpi = false,
                                           bool lng = false, bool hpsh = false, bool bndsh = false,
                                           bool hinst = false) {
         const int NS = NX + NP, NV = NS + NU, NB = NX + NU;
@@ -245,7 +245,9 @@ struct QpLds {
         o.gpe = c;    c += NV;                       // Fp' e
         o.prp = c;    c += mpad;                     // predictor dt*dlam of the polytope rows
         o.hp = c;     c += hpsh ? 0 : mpad;          // polytope right-hand side (hpsh: shared)
-        o.rp = c;     c += mpad;                     // polytope row residuals (row wave)
+        // polytope row residuals of the row wave (short horizons; the long-horizon kernels keep
+        // them in registers: 5 KB more per instance would leave one instance per workgroup)
+        o.rp = c;     c += lng ? 0 : mpad;
         o.xch = c;    c += X_NXCH;
         o.Fi = c;     c += fpi ? NV * mpad : 0;      // per-instance polytope (column-major)
         o.Hi = c;     c += (hinst && !lng) ? (N + 1) * (NV * NV + 1) : 0;   // per-instance H table
@@ -301,7 +303,7 @@ __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
                 a.stamps[(int64_t)inst * 32 + (base) + i_] = (double)st_acc[i_]; \
         }                                                                  \
     } while (0)
-#elif defined(BQP_ISA_ONLY_MG10) || defined(BQP_ISA_ONLY_DI)
+#elif defined(BQP_ISA_ONLY_MG10) || defined(BQP_ISA_ONLY_DI) || defined(BQP_ISA_ONLY_MG_LNG)
 #define STAMP(id) asm volatile(";BQP_PHASE " #id)
 #define STAMP_DECL do { } while (0)
 #define STAMP_STORE(base) do { } while (0)
@@ -834,6 +836,9 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // ======================= Newton solve ==================================================
     // right-hand side q = r_v + C'((lam o ri - rc)/t): the row wave supplies the box terms
     // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
+#ifndef BQP_SWEEP_DPP
+#define BQP_SWEEP_DPP 0   // 1: the sweep vector passed by DPP row broadcast instead of readlane
+#endif
     const int li = lane < NS ? lane : NS - 1;
     auto solve = [&](int ods, int odu) __attribute__((always_inline)) {
         const int lane = opq(lane_w);
@@ -938,8 +943,12 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                     acc += ph * p[c];
                 }
                 if (lane < NS) W[L.pv + k * NS + lane] = acc;
+#if BQP_SWEEP_DPP
+                rbc_all<0, NS>(acc, p);
+#else
 #pragma unroll
                 for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
+#endif
             };
             for (int k = N - 1; k >= 0; k -= 2) {
                 step_b(k, k0, q0);
@@ -1020,8 +1029,12 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                     acc += ph * d[c];
                 }
                 if (lane < NS) W[ods + (k + 1) * NS + lane] = acc;
+#if BQP_SWEEP_DPP
+                rbc_all<0, NS>(acc, d);
+#else
 #pragma unroll
                 for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
+#endif
             };
             for (int k = 0; k < N; k += 2) {
                 step_f(k, k0, f0);
@@ -1585,9 +1598,16 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
     // residuals are re-formed from the LDS stage vector and bounds when needed)
     real tx[BPL], lx[BPL];
     real tp[RPL], lp[RPL];
-    // polytope row residuals in LDS (L.rp): fewer registers carried through the loop (the row
-    // wave's scratch spills of round 3)
-#define RP(q) W[L.rp + lane + WAVE * (q)]
+    // polytope row residuals: in LDS (L.rp) for the short horizons - fewer registers carried
+    // through the loop (the row wave's scratch spills of round 3); in registers for the long
+    // horizons, whose LDS holds two instances per workgroup only without them (and whose
+    // 512-register budget has room)
+    real rpr[LNG ? RPL : 1];
+    auto rp_ref = [&](int q) __attribute__((always_inline)) -> real& {
+        if constexpr (LNG) return rpr[q];
+        else return W[L.rp + lane + WAVE * q];
+    };
+#define RP(q) rp_ref(q)
     // 1: the corrector carries Mehrotra's second-order term dt_a dlam_a; 0: this iteration's
     // predictor step was short on a feasible iterate, the corrector is a pure centring step
     real socf = 1.0;
@@ -2744,6 +2764,10 @@ hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int 
     // codegen inspection build (make isa): the MG N<64, 616-row instance only
     if (spl == 1 && rpl == 10 && a.N + 1 <= 25) return launch_t<4, 1, 1, 1, 10, 4>(a, blocks, lds, st, pol);
     return hipErrorInvalidValue;
+#elif defined(BQP_ISA_ONLY_MG_LNG)
+    // the MG N = 100 / 616-row long-horizon instance (config C5) only (make isa-lng)
+    if (spl == 2 && rpl == 10) return launch_t<4, 1, 1, 2, 10, 16>(a, blocks, lds, st, pol);
+    return hipErrorInvalidValue;
 #elif defined(BQP_ISA_ONLY_DI)
     return hipErrorInvalidValue;
 #else
@@ -2751,7 +2775,7 @@ hipError_t BQP_CAT(launch_ocp_mg, BQP_SFX)(const OcpKernelArgs& a, int spl, int 
 #endif
 }
 #endif
-#if BQP_FAM_DI && !defined(BQP_ISA_ONLY_MG10)
+#if BQP_FAM_DI && !defined(BQP_ISA_ONLY_MG10) && !defined(BQP_ISA_ONLY_MG_LNG)
 hipError_t BQP_CAT(launch_ocp_di, BQP_SFX)(const OcpKernelArgs& a, int spl, int rpl, int blocks, size_t lds, hipStream_t st, bool pol) {
 #ifdef BQP_ISA_ONLY_DI
     // codegen inspection build (make isa-di): the DI N<64, <= 64-row instance (config C3) only
@@ -2814,7 +2838,7 @@ hipError_t BQP_CAT(launch_ocp, BQP_SFX)(const OcpKernelArgs& a, int nx, int nu, 
                                                                                       BQP_LNG_OK && spl == 2 && a.sh_bnd >= 0,
                                                                                       a.H_inst != nullptr));
     if (nx == 4 && nu == 1 && np == 1) return BQP_CAT(launch_ocp_mg, BQP_SFX)(a, spl, rpl, blocks, lds, st, pol);
-#ifndef BQP_ISA_ONLY_MG10
+#if !defined(BQP_ISA_ONLY_MG10) && !defined(BQP_ISA_ONLY_MG_LNG)
     if (nx == 2 && nu == 2 && np == 2) return BQP_CAT(launch_ocp_di, BQP_SFX)(a, spl, rpl, blocks, lds, st, pol);
 #endif
     return hipErrorInvalidValue;

@@ -125,6 +125,24 @@ __device__ __forceinline__ float rl(float v, int src) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
 }
 
+// lane C's value in every lane of its 16-lane row (gfx950 DPP row_newbcast: one v_mov_b64_dpp
+// / v_mov_b32_dpp, the value stays in vector registers); rbc_all fills p[c] = lane c's v for
+// c < NC (NC <= 16), the sweep broadcast without a scalar round trip
+template <int C>
+__device__ __forceinline__ double rbc(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + C, 0xf, 0xf, false);
+}
+template <int C>
+__device__ __forceinline__ float rbc(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                 0x150 + C, 0xf, 0xf, false));
+}
+template <int C, int NC, typename T>
+__device__ __forceinline__ void rbc_all(T v, T (&p)[NC]) {
+    p[C] = rbc<C>(v);
+    if constexpr (C + 1 < NC) rbc_all<C + 1, NC>(v, p);
+}
+
 template <int CTRL, typename T, int KI, int KO>
 __device__ __forceinline__ void tsum_step(const T (&in)[KI], T (&out)[KO], bool hi) {
 #pragma unroll

@@ -836,9 +836,6 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     // ======================= Newton solve ==================================================
     // right-hand side q = r_v + C'((lam o ri - rc)/t): the row wave supplies the box terms
     // [upper, lower] per stage (ebox) and Fp'e (gpe); direction written to (ods, odu)
-#ifndef BQP_SWEEP_DPP
-#define BQP_SWEEP_DPP 0   // 1: the sweep vector passed by DPP row broadcast instead of readlane
-#endif
     const int li = lane < NS ? lane : NS - 1;
     auto solve = [&](int ods, int odu) __attribute__((always_inline)) {
         const int lane = opq(lane_w);
@@ -909,8 +906,11 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
         wave_sync();
         STAMP(10);
         // backward sweep: lane i < NS computes entry i of p_k = Phi_k' p_{k+1} + qh_k; the new
-        // vector is broadcast with readlane (scalar registers); two register sets used
-        // alternately (stages k, k-1), each refilled two stages ahead.  (Round 4 tried every
+        // vector reaches every lane of the row by DPP row broadcasts (v_mov_b64_dpp
+        // row_newbcast:c, one per entry: the value stays in vector registers - the round-3
+        // readlane broadcast went through scalar registers: 9.6k -> 8.0k cycles per iteration
+        // for the backward sweep, 10.9k -> 9.4k for the forward one, C2 -3.8 %); two register
+        // sets used alternately (stages k, k-1), each refilled two stages ahead.  (Round 4 tried every
         // lane forming the whole vector from broadcast LDS reads, no readlane on the chain: the
         // sweeps are issue-bound at one instance per SIMD, and the 3x longer instruction
         // stream cost 9.4k -> 14.6k cycles per iteration)
@@ -943,12 +943,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                     acc += ph * p[c];
                 }
                 if (lane < NS) W[L.pv + k * NS + lane] = acc;
-#if BQP_SWEEP_DPP
-                rbc_all<0, NS>(acc, p);
-#else
-#pragma unroll
-                for (int c = 0; c < NS; ++c) p[c] = rl(acc, c);
-#endif
+                rbc_all<0, NS>(acc, p);   // lanes c < NS of the row hold entry c
             };
             for (int k = N - 1; k >= 0; k -= 2) {
                 step_b(k, k0, q0);
@@ -1029,12 +1024,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
                     acc += ph * d[c];
                 }
                 if (lane < NS) W[ods + (k + 1) * NS + lane] = acc;
-#if BQP_SWEEP_DPP
-                rbc_all<0, NS>(acc, d);
-#else
-#pragma unroll
-                for (int c = 0; c < NS; ++c) d[c] = rl(acc, c);
-#endif
+                rbc_all<0, NS>(acc, d);   // lanes c < NS of the row hold entry c
             };
             for (int k = 0; k < N; k += 2) {
                 step_f(k, k0, f0);

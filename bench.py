@@ -577,11 +577,18 @@ def cll_subproblem_roofline(dl, X0, h):
     kms, nl = h.kernel_ms()
     its = out['iterations'].astype(float)
     F_it = nz * (nz + 1) * mr + nz ** 3 / 3.0 + 12.0 * nz * mr + 8.0 * nz * nz
+    # HBM bytes per launch and MFMA busy fraction of the same kernel in the loop (rocprofv3 PMC
+    # passes of bench.py --config CLL, tools/gpu_r04_prof.sh -> profiles/pmc_CLL.json)
+    traffic = tsrc = mfma = None
+    pj = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_CLL.json')
+    if os.path.exists(pj):
+        pm = json.load(open(pj))
+        traffic, tsrc, mfma = pm['hbm_bytes_per_launch'], pm['source'], round(pm['mfma_busy_frac_est'], 4)
     flops = float(its.sum() * F_it)
     ach = flops / (kms * 1e-3) / 1e12
     return dict(bound='fp64_mfma', achieved=round(ach, 4), peak=FP64_PEAK_TFLOPS, unit='TFLOP/s',
-                frac=round(ach / FP64_PEAK_TFLOPS, 5), traffic=None, kernel_ms=round(kms, 4),
-                flops_per_launch=flops, launches=nl,
+                frac=round(ach / FP64_PEAK_TFLOPS, 5), traffic=traffic, kernel_ms=round(kms, 4),
+                flops_per_launch=flops, launches=nl, traffic_source=tsrc, mfma_busy_frac=mfma,
                 note='dense_ipm_kernel on the loop sub-problem shape (n = %d, m = %d, batch %d, '
                      'mean %.1f IPM iterations, exit flags %s): K = H + A\'DA on the fp64 matrix '
                      'cores; kernel_ms covers the solve and the polish launch' %

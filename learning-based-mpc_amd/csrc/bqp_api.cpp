@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "../../include/bqp.h"
 #include "bqp_internal.h"
@@ -710,6 +711,20 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
         if (a.hess) HIP_TRY(bqp::launch_lbmpc_hess(a, st));
         q.polish = o.polish < 0 ? 0 : (it >= LB_POLISH_STALL ? 2 : 1);
         HIP_TRY(bqp::launch_dense(q, st));
+        if (getenv("BQP_LB_TRACE")) {     // diagnostic: sub-problem exit flags per SQP iteration
+            std::vector<int> fl(batch), dn(batch);
+            HIP_TRY(hipMemcpyAsync(fl.data(), a.qpflag, sizeof(int) * batch, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipMemcpyAsync(dn.data(), a.done, sizeof(int) * batch, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            int c1 = 0, c0 = 0, c8 = 0, co = 0, act = 0;
+            for (int b = 0; b < batch; ++b) {
+                if (dn[b]) continue;
+                ++act;
+                if (fl[b] == 1) ++c1; else if (fl[b] == 0) ++c0; else if (fl[b] == -8) ++c8; else ++co;
+            }
+            fprintf(stderr, "bqp sqp it %d: active %d, sub-problem flags 1:%d 0:%d -8:%d other:%d\n", it, act,
+                    c1, c0, c8, co);
+        }
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
         HIP_TRY(bqp::launch_lbmpc_update(a, st));
         launches += a.hess ? 6 : 5;

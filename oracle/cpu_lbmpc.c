@@ -24,6 +24,7 @@
  * use).  Only the DMS form (K = 0, nu = np = 1, nx = 4, running cost delta-weighted for k < N,
  * terminal cost on the learned x_N) - the CLL workload. */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -590,6 +591,7 @@ static int sqp(const cll_prob *P, cll_work *W, const double *dx0, int *iters) {
         }
         for (int i = 0; i < m; ++i) W->bsh[i] = W->bin[i] - rdot(W, i, W->z);
         const int qflag = dense_ipm(W, it >= POL_STALL ? 2 : 1, 100);
+        if (getenv("CLL_TRACE")) fprintf(stderr, "sqp it %d qflag %d\n", it, qflag);
         memcpy(W->d, W->zq, sizeof(double) * n);
         memcpy(W->lam, W->l, sizeof(double) * m);
         /* lbmpc_update_kernel */

@@ -75,7 +75,7 @@ def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, plan
 
 def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, handle=None,
                     max_iter=200, tol=1e-8, log_z=False, plant='rk4', x_eq=None,
-                    u_eq=None):
+                    u_eq=None, polish=1):
     """Learned-model NLP closed loop on the GPU (bqp_closed_loop_sqp): per step the batched
     Gauss-Newton SQP of mpc (a DMSLBMPC - DMS_LBMPC_casadi.m:163-218 -, HybridLBMPC -
     hybrid_LBMPC_casadi.m:163-204 - or LBMPC) at the measured states, one RK4 plant step with the
@@ -86,7 +86,8 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
     stage, zero last move, theta kept); otherwise z = 0 each step.
     plant: 'rk4' (the CasADi scripts' `dynamic`) or 'ode23' (models/trueModel.m, the fmincon loop
     functions/ocpLBMPC.m; its update_data.m window of q points equals this ring with q - 1: the
-    initial zero point leaves when the q-th sample arrives).
+    initial zero point leaves when the q-th sample arrives).  polish: the QP sub-problems'
+    active-set polish (bqp_options.polish encoding; -1 off).
     Returns X (batch, steps+1, n), U (batch, steps, m) absolute, exitflag and iterations (batch,
     steps), XL (batch, steps+1, n) the learned one-step predictions, window (batch, q, 8) the
     final windows in ring order, and with log_z every step's solution Z (batch, steps, nz)."""
@@ -120,7 +121,7 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
     cl = ClosedLoop(_PLANTS[plant], int(steps), float(delta), _lib.ptr(x_eq), _lib.ptr(u_eq))
     lw = Learning(q, mask, float(learning.get('bandwidth', 0.0)), float(learning.get('lambda_', 0.0)),
                   _lib.ptr(XL), _lib.ptr(win))
-    o = _lib.options(max_iter=max_iter, tol_stat=tol)
+    o = _lib.options(max_iter=max_iter, tol_stat=tol, polish=polish)
     rc = lib.bqp_closed_loop_sqp(h.value, C.byref(dims), b, C.byref(dd), C.byref(sl), C.byref(o),
                                  C.byref(cl), C.byref(lw), _lib.ptr(x_init), _lib.ptr(X),
                                  _lib.ptr(U), _lib.iptr(flags))

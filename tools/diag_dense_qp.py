@@ -41,14 +41,15 @@ ex = exact_qp.solve(H, f, Ain, b)
 print('n %d m %d, exact status %s, active %d' % (len(f), len(b), ex['status'], len(ex['active'])))
 h = bqp.Handle(0)
 for batch in (1, 256):
+  for pol in (1, -1):                      # the polish launch on (C default) / off
     Hb = np.broadcast_to(H, (batch,) + H.shape)
     fb = np.broadcast_to(f, (batch,) + f.shape)
     for rep in range(2):
         t0 = time.perf_counter()
-        xq, fv, flag, out, lam = bqp.quadprog(Hb, fb, Ain, b, handle=h)
+        xq, fv, flag, out, lam = bqp.quadprog(Hb, fb, Ain, b, handle=h, options=dict(polish=pol))
         el = time.perf_counter() - t0
     its = out['iterations']
     kms, nl = h.kernel_ms()
-    print('batch %d: %.1f ms host, %.2f ms kernels (%d launches), flags %s, iterations %s, |x - x*| %.2e' % (
-        batch, 1e3 * el, kms, nl, np.unique(flag).tolist(), np.unique(np.asarray(its)).tolist(),
-        np.abs(np.atleast_2d(xq) - ex['z']).max()))
+    print('batch %d polish %d: %.1f ms host, %.2f ms kernels (%d launches), flags %s, iterations %s, '
+          '|x - x*| %.2e' % (batch, pol, 1e3 * el, kms, nl, np.unique(flag).tolist(),
+                             np.unique(np.asarray(its)).tolist(), np.abs(np.atleast_2d(xq) - ex['z']).max()))

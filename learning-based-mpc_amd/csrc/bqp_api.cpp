@@ -728,7 +728,11 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
         HIP_TRY(bqp::launch_lbmpc_update(a, st));
         launches += a.hess ? 6 : 5;
-        if ((it & 3) == 3 || it + 1 == o.max_iter) {
+        // the batch is done when every instance is: polled after each iteration for large
+        // sub-problems (an SQP iteration is ~20 ms of kernels at the learned loop's N = 100 shape,
+        // and polling every 4th ran up to three iterations past the last instance's convergence),
+        // every 4th for small ones (the host round trip against ~0.3 ms iterations at N = 10)
+        if ((it + 1) % (n >= 64 ? 1 : 4) == 0 || it + 1 == o.max_iter) {
             int nd_h = 0;
             HIP_TRY(hipMemcpyAsync(&nd_h, a.ndone, sizeof(int), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));

@@ -39,7 +39,8 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_POL_ROUNDS 4       // active-set corrections of the polish
 
 struct DWork {
-    int64_t K, Y, S, z, y, q, w, dz, dy, rd, re, tA, lA, riA, rcA, dtA, dlA, tB, lB, riB, rcB, dtB, dlB, total;
+    int64_t K, Y, S, z, y, q, w, dz, dy, rd, re, tA, lA, riA, rcA, dtA, dlA, tB, lB, riB, rcB, dtB, dlB, hr, th,
+        total;
     __host__ __device__ static DWork make(int n, int m, int me) {
         DWork o;
         int64_t c = 0;
@@ -55,6 +56,8 @@ struct DWork {
         // bound rows: 2n (upper: 0..n-1, lower: n..2n-1)
         o.tB = c; c += 2 * n; o.lB = c; c += 2 * n; o.riB = c; c += 2 * n; o.rcB = c; c += 2 * n;
         o.dtB = c; c += 2 * n; o.dlB = c; c += 2 * n;
+        // nonzero column bound of each row of A and of each TILE-row tile (dense_ipm_kernel)
+        o.hr = c; c += m; o.th = c; c += (m + 31) / 32;
         o.total = (c + 7) & ~7;
         return o;
     }
@@ -634,8 +637,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     auto lo_present = [&](int j) -> bool { return lb && isfinite(lb[j]); };
     // rows r0 .. r0 + rows - 1 of A into tileA (row-major, stride ts): 8 clamped loads in flight
     // per thread before the LDS stores (the load -> store loop waited on every load)
-    auto load_tile = [&](int r0, int rows) {
-        const int tot = rows * n;
+    auto load_tile = [&](int r0, int rows, int ncol) {   // columns 0 .. ncol - 1
+        const int tot = rows * ncol;
         const bool full = rows == TILE;
         for (int b0 = 0; b0 < tot; b0 += 8 * DT) {
             double v[8];
@@ -653,17 +656,27 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             }
         }
     };
-    // (A v)_r for one row r of column-major A: four independent chains
+    // (A v)_r for one row r of column-major A over its nonzero columns j < hr[r]: four independent
+    // chains (the skipped products are exact zeros)
+    double* hr = W + L.hr;
+    double* th = W + L.th;
     auto arow = [&](int r, const double* v) -> double {
+        const int jm = (int)hr[r];
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
         int j = 0;
-        for (; j + 4 <= n; j += 4) {
+        for (; j + 4 <= jm; j += 4) {
             s0 = fma(A[(int64_t)j * m + r], v[j], s0);
             s1 = fma(A[(int64_t)(j + 1) * m + r], v[j + 1], s1);
             s2 = fma(A[(int64_t)(j + 2) * m + r], v[j + 2], s2);
             s3 = fma(A[(int64_t)(j + 3) * m + r], v[j + 3], s3);
         }
-        for (; j < n; ++j) s0 = fma(A[(int64_t)j * m + r], v[j], s0);
+        for (; j < jm; ++j) {
+            const double t = A[(int64_t)j * m + r] * 1.0;
+            if ((j & 3) == 0) s0 = fma(t, v[j], s0);
+            else if ((j & 3) == 1) s1 = fma(t, v[j], s1);
+            else if ((j & 3) == 2) s2 = fma(t, v[j], s2);
+            else s3 = fma(t, v[j], s3);
+        }
         return (s0 + s1) + (s2 + s3);
     };
     // A'(w) for a row weight w(r) (every thread calls it): A streamed through LDS row tiles
@@ -688,6 +701,10 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 for (int c = 0; c < 16; ++c) ac[c] = 0.0;
                 const double* Ag = A + (int64_t)(16 * g) * m;
                 for (int r = lane; r < m; r += 64) {
+                    // rows r - lane .. r - lane + 63 (two tiles) all zero in this column group
+                    const int t0 = (r - lane) / TILE;
+                    const double thm = fmax(th[t0], (t0 + 1) * TILE < m ? th[t0 + 1] : 0.0);
+                    if (thm <= 16.0 * g) continue;
                     const double vr = wl[r];
 #pragma unroll
                     for (int c = 0; c < 16; ++c)
@@ -705,7 +722,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         for (int r0 = 0; r0 < m; r0 += TILE) {
             const int rows = min(TILE, m - r0);
             __syncthreads();
-            load_tile(r0, rows);
+            load_tile(r0, rows, n);
             if (tid < rows) tileA[tid * ts + tw] = wfun(r0 + tid);
             __syncthreads();
             if (tid < n)
@@ -714,6 +731,23 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         __syncthreads();
         return acc;
     };
+    // nonzero column bound of every row of A (1 + its last nonzero column) and of every TILE-row
+    // tile (the max over its rows), once per launch: the products skip the columns and tiles past
+    // it - exact zeros.  The condensed rows of an MPC problem reach only the inputs up to their
+    // stage (the learned-model loop's sub-problem: each row k of the state / input boxes sees
+    // u_0 .. u_{k-1}), so A'DA runs on about a third of its tiles there.
+    for (int r = tid; r < m; r += DT) {
+        int j = n - 1;
+        while (j >= 0 && A[(int64_t)j * m + r] == 0.0) --j;
+        hr[r] = (double)(j + 1);
+    }
+    __syncthreads();
+    for (int t = tid; t * TILE < m; t += DT) {
+        double mx = 0.0;
+        for (int rr = t * TILE; rr < min(m, (t + 1) * TILE); ++rr) mx = fmax(mx, hr[rr]);
+        th[t] = mx;
+    }
+    __syncthreads();
     // row count
     double cnt = 0.0;
     for (int j = tid; j < n; j += DT) cnt += (up_present(j) ? 1.0 : 0.0) + (lo_present(j) ? 1.0 : 0.0);
@@ -809,7 +843,10 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             for (int r0 = 0; r0 < m; r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
-                load_tile(r0, rows);
+                // only the columns the tile's rows reach, to the 16-column block (the MFMA operands
+                // read columns below 16 (I + 1) <= that of tiles I < thi / 16; the rest are zeros)
+                const double thi = th[r0 / TILE];
+                load_tile(r0, rows, min(n, 16 * (((int)thi + 15) / 16)));
                 if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
                 for (int s4 = 0; s4 < rows; s4 += 4) {
@@ -818,7 +855,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     const double dr = rr < rows ? Tr[tw] : 0.0;
 #pragma unroll
                     for (int u = 0; u < TPW; ++u) {
-                        if (wv + 4 * u < ntl) {          // wave-uniform
+                        // wave-uniform: the tile exists and the rows reach its column block I (J <= I)
+                        if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
                             const double ai = Tr[min(16 * tI[u] + c16, n - 1)];
                             const double aj = Tr[min(16 * tJ[u] + c16, n - 1)];
                             acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, dr * aj, acc[u], 0, 0, 0);
@@ -867,7 +905,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             for (int r0 = 0; r0 < m; r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
-                load_tile(r0, rows);
+                load_tile(r0, rows, n);
                 if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
 #pragma unroll

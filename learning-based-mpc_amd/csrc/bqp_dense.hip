@@ -306,43 +306,60 @@ __device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
 // upper triangle block_cholesky leaves, backward) - no workgroup barrier inside (the per-entry
 // block reductions of chol_solve_vec cost two barriers per entry).  Every thread calls it.
 __device__ void chol_solve_w(const double* L, int n, double* xs) {
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < 64 && n > 0) {
         const int l = threadIdx.x;
-        double xr[4];
+        double xr[4], dr[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) xr[q] = (l + 64 * q < n) ? xs[l + 64 * q] : 0.0;
+        for (int q = 0; q < 4; ++q) {
+            const int k = min(l + 64 * q, n - 1);
+            xr[q] = (l + 64 * q < n) ? xs[l + 64 * q] : 0.0;
+            dr[q] = 1.0 / L[(int64_t)k * n + k];   // the pivots' reciprocals, off the chain
+        }
+        // the column (row) of the next step is loaded one step ahead; entry i of the solution
+        // is lane i's value times the reciprocal pivot (one multiply on the sequential chain
+        // instead of a division)
+        double cv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cv[q] = L[min(l + 64 * q, n - 1)];
         for (int i = 0; i < n; ++i) {             // L y = b
             const int qi = i >> 6, li = i & 63;
-            double xi = 0.0;
+            double xi = 0.0, di = 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) if (q == qi) xi = rl(xr[q], li);
-            const double* col = L + (int64_t)i * n;
-            double cv[4];
+            for (int q = 0; q < 4; ++q) if (q == qi) { xi = rl(xr[q], li); di = rl(dr[q], li); }
+            double cn[4];
+            const double* coln = L + (int64_t)min(i + 1, n - 1) * n;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = col[min(l + 64 * q, n - 1)];   // unconditional loads
-            xi /= col[i];
+            for (int q = 0; q < 4; ++q) cn[q] = coln[min(l + 64 * q, n - 1)];   // unconditional loads
+            xi *= di;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = l + 64 * q;
                 if (k > i && k < n) xr[q] -= cv[q] * xi;
                 if (k == i) xr[q] = xi;
+                cv[q] = cn[q];
             }
+        }
+        {
+            const double* row = L + (int64_t)(n - 1) * n;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cv[q] = row[min(l + 64 * q, n - 1)];
         }
         for (int i = n - 1; i >= 0; --i) {        // L' x = y
             const int qi = i >> 6, li = i & 63;
-            double xi = 0.0;
+            double xi = 0.0, di = 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) if (q == qi) xi = rl(xr[q], li);
-            const double* row = L + (int64_t)i * n;   // upper: L(i, k) at [i n + k], k < i
-            double rv[4];
+            for (int q = 0; q < 4; ++q) if (q == qi) { xi = rl(xr[q], li); di = rl(dr[q], li); }
+            double cn[4];
+            const double* rown = L + (int64_t)max(i - 1, 0) * n;   // upper: L(i, k) at [i n + k], k < i
 #pragma unroll
-            for (int q = 0; q < 4; ++q) rv[q] = row[min(l + 64 * q, n - 1)];
-            xi /= row[i];
+            for (int q = 0; q < 4; ++q) cn[q] = rown[min(l + 64 * q, n - 1)];
+            xi *= di;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = l + 64 * q;
-                if (k < i) xr[q] -= rv[q] * xi;
+                if (k < i) xr[q] -= cv[q] * xi;
                 if (k == i) xr[q] = xi;
+                cv[q] = cn[q];
             }
         }
 #pragma unroll

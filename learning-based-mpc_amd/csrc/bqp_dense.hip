@@ -27,6 +27,7 @@ namespace bqp {
 
 #define DT 256
 #define TILE 32
+#define DQ_THL 256   // A row-tile bounds kept in LDS (m <= 8192 rows)
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_PIV_FLOOR 1e-14    // static pivot floor of K, relative to its largest diagonal entry
 #define DQ_CONVEX_EPS 1e-10   // shift of the convexity test (relative)
@@ -300,66 +301,78 @@ __device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
     }
 }
 
+// one 16-entry block of the substitutions: the block's entries sit in one 16-lane row of a slot
+// (lane jl of the row holds entry e0 + jl); entry j = e0 + JJ is final when step JJ starts, reaches
+// the row by a DPP row broadcast (v_mov_b64_dpp row_newbcast), is scaled by its reciprocal pivot
+// and updates the row's later (forward) or earlier (backward) entries of the block
+template <int JJ, bool FWD>
+__device__ __forceinline__ void tri_blk(double& xv, double dv, const double (&lc)[16], int jl, bool inrow,
+                                        int nval) {
+    constexpr int J = FWD ? JJ : 15 - JJ;
+    const double xj = rbc<J>(xv) * rbc<J>(dv);
+    const bool ok = inrow && J < nval;       // entries past n (partial last block) never broadcast
+    if (ok && (FWD ? jl > J : jl < J)) xv -= lc[J] * xj;
+    if (ok && jl == J) xv = xj;
+    if constexpr (JJ + 1 < 16) tri_blk<JJ + 1, FWD>(xv, dv, lc, jl, inrow, nval);
+}
+
 // solve L L' x = b in place (xs in LDS, n <= 256) by the first wave alone: lane l keeps entries
-// l, l + 64, .. in registers; column-oriented substitutions broadcast each solved entry with
-// readlane and update the remaining ones from a contiguous column of L (forward) or of L' (the
-// upper triangle block_cholesky leaves, backward) - no workgroup barrier inside (the per-entry
-// block reductions of chol_solve_vec cost two barriers per entry).  Every thread calls it.
+// l, l + 64, .. in registers.  Blocked substitutions (round 4): 16-entry diagonal blocks solved
+// inside one 16-lane row (DPP row broadcasts, no scalar round trip per entry), each solved block
+// published through LDS and applied to the remaining entries as a 16-column update (the
+// column-at-a-time form spent ~530 cycles per entry on its readlane / load / update chain).  L's
+// column j (forward) and row i (backward, the upper triangle block_cholesky leaves) are both at
+// [j n + e].  No workgroup barrier inside; every thread calls it.
 __device__ void chol_solve_w(const double* L, int n, double* xs) {
     if (threadIdx.x < 64 && n > 0) {
-        const int l = threadIdx.x;
+        const int l = threadIdx.x, jl = l & 15, rw = l >> 4;
         double xr[4], dr[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int k = min(l + 64 * q, n - 1);
             xr[q] = (l + 64 * q < n) ? xs[l + 64 * q] : 0.0;
-            dr[q] = 1.0 / L[(int64_t)k * n + k];   // the pivots' reciprocals, off the chain
+            dr[q] = 1.0 / L[(int64_t)k * n + k];   // the pivots' reciprocals
         }
-        // the column (row) of the next step is loaded one step ahead; entry i of the solution
-        // is lane i's value times the reciprocal pivot (one multiply on the sequential chain
-        // instead of a division)
-        double cv[4];
+        const int nb = (n + 15) >> 4;
+        for (int pass = 0; pass < 2; ++pass) {
+            const bool fwd = pass == 0;
+            for (int bi = 0; bi < nb; ++bi) {
+                const int b = fwd ? bi : nb - 1 - bi;
+                const int qb = b >> 2, e0 = 16 * b;
+                const bool inrow = rw == (b & 3);
+                double xv = 0.0, dv = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cv[q] = L[min(l + 64 * q, n - 1)];
-        for (int i = 0; i < n; ++i) {             // L y = b
-            const int qi = i >> 6, li = i & 63;
-            double xi = 0.0, di = 0.0;
+                for (int q = 0; q < 4; ++q) if (q == qb) { xv = xr[q]; dv = dr[q]; }
+                // the block's coefficients of this lane's entry e0 + jl: [(e0 + jj) n + e0 + jl]
+                double lc[16];
+                const int ec = min(e0 + jl, n - 1);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) if (q == qi) { xi = rl(xr[q], li); di = rl(dr[q], li); }
-            double cn[4];
-            const double* coln = L + (int64_t)min(i + 1, n - 1) * n;
+                for (int jj = 0; jj < 16; ++jj) lc[jj] = L[(int64_t)min(e0 + jj, n - 1) * n + ec];
+                // the last block may be partial: steps past n are skipped (backward: they come
+                // first and would reach valid entries)
+                if (fwd) tri_blk<0, true>(xv, dv, lc, jl, inrow, n - e0);
+                else     tri_blk<0, false>(xv, dv, lc, jl, inrow, n - e0);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cn[q] = coln[min(l + 64 * q, n - 1)];   // unconditional loads
-            xi *= di;
+                for (int q = 0; q < 4; ++q) if (q == qb) xr[q] = xv;
+                // publish the block, then the 16-column update of the entries after (forward) /
+                // before (backward) it
+                if (inrow) xs[e0 + jl] = xv;
+                wave_sync();
+                double xb[16];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int k = l + 64 * q;
-                if (k > i && k < n) xr[q] -= cv[q] * xi;
-                if (k == i) xr[q] = xi;
-                cv[q] = cn[q];
-            }
-        }
-        {
-            const double* row = L + (int64_t)(n - 1) * n;
+                for (int jj = 0; jj < 16; ++jj) xb[jj] = (e0 + jj < n) ? xs[e0 + jj] : 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) cv[q] = row[min(l + 64 * q, n - 1)];
-        }
-        for (int i = n - 1; i >= 0; --i) {        // L' x = y
-            const int qi = i >> 6, li = i & 63;
-            double xi = 0.0, di = 0.0;
+                for (int q = 0; q < 4; ++q) {
+                    const int e = l + 64 * q;
+                    const bool upd = e < n && (fwd ? e >= e0 + 16 : e < e0);
+                    if (!upd) continue;
+                    double acc = 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) if (q == qi) { xi = rl(xr[q], li); di = rl(dr[q], li); }
-            double cn[4];
-            const double* rown = L + (int64_t)max(i - 1, 0) * n;   // upper: L(i, k) at [i n + k], k < i
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cn[q] = rown[min(l + 64 * q, n - 1)];
-            xi *= di;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int k = l + 64 * q;
-                if (k < i) xr[q] -= cv[q] * xi;
-                if (k == i) xr[q] = xi;
-                cv[q] = cn[q];
+                    for (int jj = 0; jj < 16; ++jj)
+                        acc = fma(L[(int64_t)min(e0 + jj, n - 1) * n + e], xb[jj], acc);
+                    xr[q] -= acc;
+                }
+                wave_sync();
             }
         }
 #pragma unroll
@@ -628,6 +641,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     if (inst >= a.batch) return;
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
     __shared__ double sc[16];
+    __shared__ double thl[DQ_THL];   // tile bounds of A (below)
     extern __shared__ double dlds[];
     const int ts = dense_ts(n), tw = ts - 1;
     double* tileA = dlds;
@@ -677,6 +691,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     // chains (the skipped products are exact zeros)
     double* hr = W + L.hr;
     double* th = W + L.th;
+    // the tile bounds from LDS (the first DQ_THL tiles; later ones are taken as full)
+    auto tbound = [&](int t) -> double { return t < DQ_THL ? thl[t] : (double)n; };
     auto arow = [&](int r, const double* v) -> double {
         const int jm = (int)hr[r];
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -720,7 +736,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 for (int r = lane; r < m; r += 64) {
                     // rows r - lane .. r - lane + 63 (two tiles) all zero in this column group
                     const int t0 = (r - lane) / TILE;
-                    const double thm = fmax(th[t0], (t0 + 1) * TILE < m ? th[t0 + 1] : 0.0);
+                    const double thm = fmax(tbound(t0), (t0 + 1) * TILE < m ? tbound(t0 + 1) : 0.0);
                     if (thm <= 16.0 * g) continue;
                     const double vr = wl[r];
 #pragma unroll
@@ -763,6 +779,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         double mx = 0.0;
         for (int rr = t * TILE; rr < min(m, (t + 1) * TILE); ++rr) mx = fmax(mx, hr[rr]);
         th[t] = mx;
+        if (t < DQ_THL) thl[t] = mx;
     }
     __syncthreads();
     // row count
@@ -862,7 +879,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 __syncthreads();
                 // only the columns the tile's rows reach, to the 16-column block (the MFMA operands
                 // read columns below 16 (I + 1) <= that of tiles I < thi / 16; the rest are zeros)
-                const double thi = th[r0 / TILE];
+                const double thi = tbound(r0 / TILE);
                 load_tile(r0, rows, min(n, 16 * (((int)thi + 15) / 16)));
                 if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();

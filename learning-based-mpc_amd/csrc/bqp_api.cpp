@@ -705,13 +705,34 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     q.stats = (double*)h->dwork.p + (size_t)wst * B;
     HIP_TRY(hipEventRecord(h->ev0, st));
     int launches = 0;
+    // diagnostic (BQP_LB_TRACE=2): per-launch event times of the first SQP iterations
+    const char* lbt = getenv("BQP_LB_TRACE");
+    const bool lbt2 = lbt && atoi(lbt) >= 2;
+    hipEvent_t tev[6] = {};
+    if (lbt2)
+        for (auto& e : tev) HIP_TRY(hipEventCreate(&e));
     for (int it = 0; it < o.max_iter; ++it) {
+        if (lbt2) HIP_TRY(hipEventRecord(tev[0], st));
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 1, st));
+        if (lbt2) HIP_TRY(hipEventRecord(tev[1], st));
         HIP_TRY(bqp::launch_lbmpc_normal(a, st));
         if (a.hess) HIP_TRY(bqp::launch_lbmpc_hess(a, st));
+        if (lbt2) HIP_TRY(hipEventRecord(tev[2], st));
         q.polish = o.polish < 0 ? 0 : (it >= LB_POLISH_STALL ? 2 : 1);
         HIP_TRY(bqp::launch_dense(q, st));
-        if (getenv("BQP_LB_TRACE")) {     // diagnostic: sub-problem exit flags per SQP iteration
+        if (lbt2) {
+            HIP_TRY(hipEventRecord(tev[3], st));
+            HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
+            HIP_TRY(hipEventRecord(tev[4], st));
+            HIP_TRY(bqp::launch_lbmpc_update(a, st));
+            HIP_TRY(hipEventRecord(tev[5], st));
+            HIP_TRY(hipEventSynchronize(tev[5]));
+            float ms[5];
+            for (int k = 0; k < 5; ++k) HIP_TRY(hipEventElapsedTime(&ms[k], tev[k], tev[k + 1]));
+            fprintf(stderr, "bqp sqp it %d ms: rollout+sens %.3f normal+hess %.3f dense(+polish) %.3f trials %.3f update %.3f\n",
+                    it, ms[0], ms[1], ms[2], ms[3], ms[4]);
+        }
+        if (lbt && !lbt2) {     // diagnostic: sub-problem exit flags per SQP iteration
             std::vector<int> fl(batch), dn(batch);
             HIP_TRY(hipMemcpyAsync(fl.data(), a.qpflag, sizeof(int) * batch, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipMemcpyAsync(dn.data(), a.done, sizeof(int) * batch, hipMemcpyDeviceToHost, st));
@@ -725,8 +746,10 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
             fprintf(stderr, "bqp sqp it %d: active %d, sub-problem flags 1:%d 0:%d -8:%d other:%d\n", it, act,
                     c1, c0, c8, co);
         }
-        HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
-        HIP_TRY(bqp::launch_lbmpc_update(a, st));
+        if (!lbt2) {
+            HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
+            HIP_TRY(bqp::launch_lbmpc_update(a, st));
+        }
         launches += a.hess ? 6 : 5;
         // the batch is done when every instance is: polled after each iteration for large
         // sub-problems (an SQP iteration is ~20 ms of kernels at the learned loop's N = 100 shape,
@@ -739,6 +762,8 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
             if (nd_h >= batch) break;
         }
     }
+    if (lbt2)
+        for (auto& e : tev) hipEventDestroy(e);
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->timed = true;
     h->launches = launches;

@@ -75,7 +75,9 @@ typedef struct {
                           0 (default) or 1: after an iteration-limit or numerical-failure exit
                           (e.g. multipliers ~1e3-1e5 drive D = lam/t out of fp64 range);
                           2: also when a row is left weakly active (slack and multiplier both
-                          above 1e-10); -1: off (interior-point iterate only) */
+                          above 1e-10); 3 (SQP routines bqp_lbmpc_* / bqp_closed_loop_sqp;
+                          the closed loop's default): the sub-problems are polished only once
+                          the SQP has stalled at a step; -1: off (interior-point iterate only) */
 } bqp_options;
 
 typedef struct {

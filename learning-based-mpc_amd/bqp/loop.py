@@ -75,7 +75,7 @@ def closed_loop(mpc, x_init, steps, delta=0.01, handle=None, learning=None, plan
 
 def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, handle=None,
                     max_iter=200, tol=1e-8, log_z=False, plant='rk4', x_eq=None,
-                    u_eq=None, polish=1):
+                    u_eq=None, polish=0):
     """Learned-model NLP closed loop on the GPU (bqp_closed_loop_sqp): per step the batched
     Gauss-Newton SQP of mpc (a DMSLBMPC - DMS_LBMPC_casadi.m:163-218 -, HybridLBMPC -
     hybrid_LBMPC_casadi.m:163-204 - or LBMPC) at the measured states, one RK4 plant step with the
@@ -87,7 +87,8 @@ def closed_loop_sqp(mpc, x_init, steps, learning=None, warm=True, delta=0.01, ha
     plant: 'rk4' (the CasADi scripts' `dynamic`) or 'ode23' (models/trueModel.m, the fmincon loop
     functions/ocpLBMPC.m; its update_data.m window of q points equals this ring with q - 1: the
     initial zero point leaves when the q-th sample arrives).  polish: the QP sub-problems'
-    active-set polish (bqp_options.polish encoding; -1 off).
+    active-set polish (bqp_options.polish encoding; 0 = the loop's default 3, polish only once the
+    SQP stalls at a step; 1 also after -8 sub-problem exits; -1 off).
     Returns X (batch, steps+1, n), U (batch, steps, m) absolute, exitflag and iterations (batch,
     steps), XL (batch, steps+1, n) the learned one-step predictions, window (batch, q, 8) the
     final windows in ring order, and with log_z every step's solution Z (batch, steps, nz)."""

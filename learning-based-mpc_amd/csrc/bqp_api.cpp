@@ -695,12 +695,15 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     q.sH = (int64_t)n * n; q.sf = n; q.sA = 0; q.sb = m;
     q.x = a.d; q.lam_ineqlin = a.lam; q.exitflag = a.qpflag;
     q.work = (double*)h->dwork.p; q.work_stride = wst;
-    // sub-problem polish: after 0 / -8 exits always; the active-set polish of every converged
-    // sub-problem (mode 2) only once the SQP has run LB_POLISH_STALL iterations - the
-    // Gauss-Newton iteration converges linearly on the learned costs of DMS_LBMPC_casadi.m and
-    // interior-point steps accurate to ~1e-8 left it wandering at that level
-    // (tools/diag_dms_gpu.py); with the exact Hessian the SQP ends in 1-4 iterations, where the
-    // polish launch after every sub-problem was 12 % of the loop
+    // sub-problem polish after 0 / -8 exits (modes 0-2; mode 3: not before the stall), and on every
+    // sub-problem (mode 2) once the SQP has run LB_POLISH_STALL iterations at a step: the Gauss-Newton iteration converges linearly on the learned costs of
+    // DMS_LBMPC_casadi.m and interior-point steps accurate to ~1e-8 left it wandering at that level
+    // (tools/diag_dms_gpu.py); with the exact Hessian the SQP ends in 1-4 iterations.  Before the
+    // stall, mode 3 (the closed loop's default) leaves -8 exits unpolished: in the learned loop ~10 %
+    // of the sub-problems end -8 once mu ~ 1e-15 (the factor leaves fp64 range one step past an
+    // accurate iterate, which the update kernel takes as is), and the polish launch for them was
+    // ~1/3 of each SQP iteration (5.5 of 16 ms, BQP_LB_TRACE=2).  A single solve keeps mode 1: its
+    // weakly determined tail inputs move ~1e-6 without the polish.
     constexpr int LB_POLISH_STALL = 6;
     q.stats = (double*)h->dwork.p + (size_t)wst * B;
     HIP_TRY(hipEventRecord(h->ev0, st));
@@ -718,7 +721,7 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
         HIP_TRY(bqp::launch_lbmpc_normal(a, st));
         if (a.hess) HIP_TRY(bqp::launch_lbmpc_hess(a, st));
         if (lbt2) HIP_TRY(hipEventRecord(tev[2], st));
-        q.polish = o.polish < 0 ? 0 : (it >= LB_POLISH_STALL ? 2 : 1);
+        q.polish = o.polish < 0 ? 0 : (it >= LB_POLISH_STALL ? 2 : (o.polish == 3 ? 0 : 1));
         HIP_TRY(bqp::launch_dense(q, st));
         if (lbt2) {
             HIP_TRY(hipEventRecord(tev[3], st));
@@ -1035,6 +1038,10 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     int* fl = (int*)(win + B * (size_t)q * 8);
     int* it = fl + B;
     if (lw->window) win = lw->window;
+    bqp_options ol;                       // the loop's default polish: only once the SQP stalls
+    resolve(opt, &ol);
+    if (ol.polish == 0) ol.polish = 3;
+    opt = &ol;
     HIP_TRY(bqp::launch_closed_loop_init(batch, nx, cl->steps, x_init, cl->x_eq, s, X, st));
     HIP_TRY(bqp::launch_lbmpc_window_init(batch, cl->steps, q, lw->mask, x_init, win, lw->XL, st));
     HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));

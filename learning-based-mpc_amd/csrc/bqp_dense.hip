@@ -874,41 +874,15 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             dbl4 acc[TPW];
 #pragma unroll
             for (int u = 0; u < TPW; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
-            // the row tiles of A pass through registers: the next tile's entries are fetched while
-            // this tile's MFMAs run (TILE x 128 / DT = 16 doubles per thread at most), only the
-            // columns the tile's rows reach, to the 16-column block (the MFMA operands read columns
-            // below 16 (I + 1) <= that of the tiles I < thi / 16; the rest are zeros)
-            constexpr int PF = TILE * 128 / DT;
-            double pf[PF];
-            auto ncol_of = [&](int r0) -> int {
-                return min(n, 16 * (((int)tbound(r0 / TILE) + 15) / 16));
-            };
-            auto fetch = [&](int r0, int rows, int ncol) {
-                const int tot = rows * ncol;
-#pragma unroll
-                for (int u = 0; u < PF; ++u) {
-                    const int t2 = min(tid + u * DT, max(tot - 1, 0));
-                    const int rr = rows == TILE ? (t2 & (TILE - 1)) : t2 % rows;
-                    const int j = rows == TILE ? (t2 / TILE) : t2 / rows;
-                    pf[u] = tot > 0 ? A[(int64_t)j * m + r0 + rr] : 0.0;
-                }
-            };
-            fetch(0, min(TILE, m), ncol_of(0));
             for (int r0 = 0; r0 < m; r0 += TILE) {
                 const int rows = min(TILE, m - r0);
-                const double thi = tbound(r0 / TILE);
-                const int ncol = ncol_of(r0), tot = rows * ncol;
                 __syncthreads();
-#pragma unroll
-                for (int u = 0; u < PF; ++u) {
-                    const int t2 = tid + u * DT;
-                    const int rr = rows == TILE ? (t2 & (TILE - 1)) : t2 % rows;
-                    const int j = rows == TILE ? (t2 / TILE) : t2 / rows;
-                    if (t2 < tot) tileA[rr * ts + j] = pf[u];
-                }
+                // only the columns the tile's rows reach, to the 16-column block (the MFMA operands
+                // read columns below 16 (I + 1) <= that of tiles I < thi / 16; the rest are zeros)
+                const double thi = tbound(r0 / TILE);
+                load_tile(r0, rows, min(n, 16 * (((int)thi + 15) / 16)));
                 if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
                 __syncthreads();
-                if (r0 + TILE < m) fetch(r0 + TILE, min(TILE, m - r0 - TILE), ncol_of(r0 + TILE));
                 for (int s4 = 0; s4 < rows; s4 += 4) {
                     const int rr = s4 + k4;
                     const double* Tr = tileA + min(rr, rows - 1) * ts;

@@ -344,6 +344,13 @@ static double kdiag_max(const cll_work *W) {
     return mx;
 }
 
+/* CLL_TRACE=1: per sub-problem exit diagnostics on stderr (read once) */
+static int cll_trace(void) {
+    static int v = -1;
+    if (v < 0) v = getenv("CLL_TRACE") != NULL;
+    return v;
+}
+
 /* ---------------------------------------------------------------- active-set polish ------ */
 /* oracle/dense_ipm.py _polish (bqp_dense.hip dense_polish) without equality rows / bounds */
 static int polish(cll_work *W, double bscale, double tol_stat) {
@@ -513,7 +520,9 @@ static int dense_ipm(cll_work *W, int polish_mode, int max_iter) {
         mu *= minv;
         if (stat <= tol_stat * (1 + gs) && feas <= tol_feas * (1 + bscale) && mu <= tol_comp &&
             cmax <= CMAX_K * tol_comp) { flag = 1; break; }
-        if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
+        if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) {
+            if (cll_trace()) fprintf(stderr, "ipm -8 residual at it %d stat %g feas %g mu %g\n", it, stat, feas, mu);
+            flag = -8; break; }
         if (amax(W->zq, n) > zscale) { flag = -3; break; }
         if (mu > MU_BLOWUP * mu_min && feas > FEAS_GUARD * (1 + bscale)) { flag = -2; break; }
         mu_min = fmin(mu_min, mu);
@@ -532,10 +541,13 @@ static int dense_ipm(cll_work *W, int polish_mode, int max_iter) {
         const double a = fmin(1.0, tau * ipm_step(W));
         int fin = isfinite(a);
         for (int j = 0; j < n && fin; ++j) fin = isfinite(W->dz[j]);
-        if (!fin) { flag = -8; break; }
+        if (!fin) {
+            if (cll_trace()) fprintf(stderr, "ipm -8 step at it %d mu %g a %g\n", it, mu, a);
+            flag = -8; break; }
         for (int j = 0; j < n; ++j) W->zq[j] += a * W->dz[j];
         for (int r = 0; r < m; ++r) { W->t[r] += a * W->dtt[r]; W->l[r] += a * W->dl[r]; }
     }
+    if (cll_trace()) fprintf(stderr, "ipm flag %d\n", flag);
     if (polish_mode && (flag == 0 || flag == -8 || (polish_mode == 2 && flag == 1)) && m && isfinite(gs))
         if (polish(W, bscale, tol_stat)) flag = 1;
     return flag;
@@ -590,8 +602,8 @@ static int sqp(const cll_prob *P, cll_work *W, const double *dx0, int *iters) {
             if (!chol(W->K, n, 1e-10 * hd, 1)) memcpy(W->H, W->Hg, sizeof(double) * n * n);
         }
         for (int i = 0; i < m; ++i) W->bsh[i] = W->bin[i] - rdot(W, i, W->z);
-        const int qflag = dense_ipm(W, it >= POL_STALL ? 2 : 1, 100);
-        if (getenv("CLL_TRACE")) fprintf(stderr, "sqp it %d qflag %d\n", it, qflag);
+        const int qflag = dense_ipm(W, it >= POL_STALL ? 2 : 0, 100);
+        if (cll_trace()) fprintf(stderr, "sqp it %d qflag %d\n", it, qflag);
         memcpy(W->d, W->zq, sizeof(double) * n);
         memcpy(W->lam, W->l, sizeof(double) * m);
         /* lbmpc_update_kernel */
@@ -706,6 +718,7 @@ int cll_rows(const cll_prob *P) { return P->nd + P->nT + P->N * (P->nFx + P->nFu
 int cll_loop(const cll_prob *P, int mask, int nb, const double *x_init, int steps, double *X,
              double *U, int *iters, int *flags, int threads) {
     if (!P || P->N < 1 || P->q < 1 || nb < 0 || steps < 0) return -1;
+    (void)cll_trace();                    /* read before the worker threads start */
     const int N = P->N, n = N + 1, m = cll_rows(P), q = P->q;
     double *Ain = xcalloc((size_t)m * n, sizeof(double));
     int *lo = xcalloc(m, sizeof(int)), *hi = xcalloc(m, sizeof(int));

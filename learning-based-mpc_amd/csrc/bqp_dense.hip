@@ -687,28 +687,48 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             }
         }
     };
-    // (A v)_r for one row r of column-major A over its nonzero columns j < hr[r]: four independent
-    // chains (the skipped products are exact zeros)
+    // (A v)_r for one row r of column-major A over its nonzero columns j < hr[r] (the skipped
+    // products are exact zeros): v staged in LDS (vlds, by stage_v), 16 clamped loads of A in
+    // flight per batch and four independent chains (four loads per step with v read from global
+    // took one memory round trip per four columns)
     double* hr = W + L.hr;
     double* th = W + L.th;
     // the tile bounds from LDS (the first DQ_THL tiles; later ones are taken as full)
     auto tbound = [&](int t) -> double { return t < DQ_THL ? thl[t] : (double)n; };
-    auto arow = [&](int r, const double* v) -> double {
+    double* vlds = tileA + TILE * ts - n;   // the end of the tile buffer (free around the row products)
+    auto stage_v = [&](const double* v) {
+        __syncthreads();
+        for (int j = tid; j < n; j += DT) vlds[j] = v[j];
+        __syncthreads();
+    };
+    auto arow = [&](int r) -> double {
         const int jm = (int)hr[r];
+        const double* pr = A + r;
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-        int j = 0;
-        for (; j + 4 <= jm; j += 4) {
-            s0 = fma(A[(int64_t)j * m + r], v[j], s0);
-            s1 = fma(A[(int64_t)(j + 1) * m + r], v[j + 1], s1);
-            s2 = fma(A[(int64_t)(j + 2) * m + r], v[j + 2], s2);
-            s3 = fma(A[(int64_t)(j + 3) * m + r], v[j + 3], s3);
+        int j0 = 0;
+        for (; j0 + 16 <= jm; j0 += 16) {        // whole batches: no clamps or selects
+            double av[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) av[u] = pr[(int64_t)(j0 + u) * m];
+#pragma unroll
+            for (int u = 0; u < 16; u += 4) {
+                s0 = fma(av[u], vlds[j0 + u], s0);
+                s1 = fma(av[u + 1], vlds[j0 + u + 1], s1);
+                s2 = fma(av[u + 2], vlds[j0 + u + 2], s2);
+                s3 = fma(av[u + 3], vlds[j0 + u + 3], s3);
+            }
         }
-        for (; j < jm; ++j) {
-            const double t = A[(int64_t)j * m + r] * 1.0;
-            if ((j & 3) == 0) s0 = fma(t, v[j], s0);
-            else if ((j & 3) == 1) s1 = fma(t, v[j], s1);
-            else if ((j & 3) == 2) s2 = fma(t, v[j], s2);
-            else s3 = fma(t, v[j], s3);
+        if (j0 < jm) {                           // the tail (clamped, masked)
+            double av[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) av[u] = pr[(int64_t)min(j0 + u, jm - 1) * m];
+#pragma unroll
+            for (int u = 0; u < 16; u += 4) {
+                s0 = fma(j0 + u < jm ? av[u] : 0.0, vlds[min(j0 + u, n - 1)], s0);
+                s1 = fma(j0 + u + 1 < jm ? av[u + 1] : 0.0, vlds[min(j0 + u + 1, n - 1)], s1);
+                s2 = fma(j0 + u + 2 < jm ? av[u + 2] : 0.0, vlds[min(j0 + u + 2, n - 1)], s2);
+                s3 = fma(j0 + u + 3 < jm ? av[u + 3] : 0.0, vlds[min(j0 + u + 3, n - 1)], s3);
+            }
         }
         return (s0 + s1) + (s2 + s3);
     };
@@ -733,15 +753,25 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 #pragma unroll
                 for (int c = 0; c < 16; ++c) ac[c] = 0.0;
                 const double* Ag = A + (int64_t)(16 * g) * m;
-                for (int r = lane; r < m; r += 64) {
-                    // rows r - lane .. r - lane + 63 (two tiles) all zero in this column group
+                // two 64-row steps per pass: 32 loads in flight
+                for (int r = lane; r < m; r += 128) {
+                    // rows r - lane .. r - lane + 127 (four tiles) all zero in this column group
                     const int t0 = (r - lane) / TILE;
-                    const double thm = fmax(tbound(t0), (t0 + 1) * TILE < m ? tbound(t0 + 1) : 0.0);
-                    if (thm <= 16.0 * g) continue;
-                    const double vr = wl[r];
+                    double thm = tbound(t0);
 #pragma unroll
-                    for (int c = 0; c < 16; ++c)
-                        ac[c] = fma(Ag[(int64_t)min(c, n - 1 - 16 * g) * m + r], vr, ac[c]);
+                    for (int k = 1; k < 4; ++k) thm = fmax(thm, (t0 + k) * TILE < m ? tbound(t0 + k) : 0.0);
+                    if (thm <= 16.0 * g) continue;
+                    const int r2 = min(r + 64, m - 1);
+                    const double vr = wl[r], vr2 = r + 64 < m ? wl[r2] : 0.0;
+                    double a1[16], a2[16];
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) {
+                        const int64_t co = (int64_t)min(c, n - 1 - 16 * g) * m;
+                        a1[c] = Ag[co + r];
+                        a2[c] = Ag[co + r2];
+                    }
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) ac[c] = fma(a2[c], vr2, fma(a1[c], vr, ac[c]));
                 }
                 const double sv = wsum_t(ac, lane);
                 if (lane < 16 && 16 * g + lane < n) out[16 * g + lane] = sv;
@@ -792,12 +822,27 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     auto residuals = [&](double& stat, double& feq, double& fin, double& csum, double& gscale, double& zmax,
                          double& cmax) {
         double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0, cm = 0.0;
+        stage_v(z);
         for (int r = tid; r < m; r += DT) {
-            const double v = tA[r] - b[r] + arow(r, z);
+            const double v = tA[r] - b[r] + arow(r);
             riA[r] = v;
             fe = fmax(fe, fabs(v));
             cs += tA[r] * lA[r];
             cm = fmax(cm, tA[r] * lA[r]);
+        }
+        // f + H z (z from vlds; row j of H read across the lanes - coalesced, H symmetric as
+        // the factorisation assumes; 16 loads in flight) into rd, completed below
+        for (int j = tid; j < n; j += DT) {
+            double v = f[j];
+            for (int i0 = 0; i0 < n; i0 += 16) {
+                double hv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) hv[u] = H[(int64_t)min(i0 + u, n - 1) * n + j];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (i0 + u < n) v = fma(hv[u], vlds[i0 + u], v);
+            }
+            rd[j] = v;
         }
         DST(0);
         for (int r = tid; r < me; r += DT) {
@@ -809,8 +854,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         const double alam = atw([&](int r) { return lA[r]; });   // (A' lam)_tid
         DST(10);
         for (int j = tid; j < n; j += DT) {
-            double v = f[j];
-            for (int i = 0; i < n; ++i) v += H[(int64_t)j * n + i] * z[i];
+            double v = rd[j];
             gs = fmax(gs, fabs(v));
             for (int r = 0; r < me; ++r) v += E[(int64_t)j * me + r] * y[r];
             v += alam;
@@ -880,8 +924,11 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 // only the columns the tile's rows reach, to the 16-column block (the MFMA operands
                 // read columns below 16 (I + 1) <= that of tiles I < thi / 16; the rest are zeros)
                 const double thi = tbound(r0 / TILE);
+                // the row weights' loads ahead of the tile's (one round trip for both)
+                const int rd0 = r0 + min(tid, rows - 1);
+                const double la = lA[rd0], ta = tA[rd0];
                 load_tile(r0, rows, min(n, 16 * (((int)thi + 15) / 16)));
-                if (tid < rows) tileA[tid * ts + tw] = lA[r0 + tid] / tA[r0 + tid];
+                if (tid < rows) tileA[tid * ts + tw] = la / ta;
                 __syncthreads();
                 for (int s4 = 0; s4 < rows; s4 += 4) {
                     const int rr = s4 + k4;
@@ -1026,9 +1073,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             for (int r = 0; r < me; ++r) v -= Y[(int64_t)r * n + j] * dy[r];
             dz[j] = v;
         }
-        __syncthreads();
+        stage_v(dz);
         for (int r = tid; r < m; r += DT) {
-            const double v = arow(r, dz);
+            const double v = arow(r);
             dtA[r] = -riA[r] - v;
             dlA[r] = (-rcA[r] - lA[r] * dtA[r]) / tA[r];
         }

@@ -930,18 +930,30 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 load_tile(r0, rows, min(n, 16 * (((int)thi + 15) / 16)));
                 if (tid < rows) tileA[tid * ts + tw] = la / ta;
                 __syncthreads();
-                for (int s4 = 0; s4 < rows; s4 += 4) {
-                    const int rr = s4 + k4;
-                    const double* Tr = tileA + min(rr, rows - 1) * ts;
-                    const double dr = rr < rows ? Tr[tw] : 0.0;
+                // per output tile u the 8 k-steps of the row tile: 16 operand reads issued
+                // together, then 8 MFMAs on acc[u] (with the k-steps outermost every tile's pair
+                // of reads sat in its own branch block, one LDS round trip per MFMA)
+                double drv[TILE / 4];
 #pragma unroll
-                    for (int u = 0; u < TPW; ++u) {
-                        // wave-uniform: the tile exists and the rows reach its column block I (J <= I)
-                        if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
-                            const double ai = Tr[min(16 * tI[u] + c16, n - 1)];
-                            const double aj = Tr[min(16 * tJ[u] + c16, n - 1)];
-                            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai, dr * aj, acc[u], 0, 0, 0);
+                for (int s4 = 0; s4 < TILE / 4; ++s4) {
+                    const int rr = 4 * s4 + k4;
+                    drv[s4] = rr < rows ? tileA[min(rr, rows - 1) * ts + tw] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < TPW; ++u) {
+                    // wave-uniform: the tile exists and the rows reach its column block I (J <= I)
+                    if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
+                        const int ci = min(16 * tI[u] + c16, n - 1), cj = min(16 * tJ[u] + c16, n - 1);
+                        double ai[TILE / 4], aj[TILE / 4];
+#pragma unroll
+                        for (int s4 = 0; s4 < TILE / 4; ++s4) {
+                            const double* Tr = tileA + min(4 * s4 + k4, rows - 1) * ts;
+                            ai[s4] = Tr[ci];
+                            aj[s4] = Tr[cj];
                         }
+#pragma unroll
+                        for (int s4 = 0; s4 < TILE / 4; ++s4)
+                            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s4], drv[s4] * aj[s4], acc[u], 0, 0, 0);
                     }
                 }
             }

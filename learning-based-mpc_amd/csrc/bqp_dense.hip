@@ -625,12 +625,25 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
 // it fits, the n x n factor K = L (lower) / L' (upper) itself: the Cholesky and the four
 // triangular solves per iteration then run on LDS instead of L2 round trips
 #define DENSE_LDS_MAX (152 * 1024)
+#define DQ_GB 33     // A'DA row-tile buffers filled by global_load_lds: column stride (32 rows + 1)
 __host__ __device__ inline int dense_ts(int n) { return 32 * ((n + 31) / 32) + 1; }
+// one A'DA buffer: column-major 32-row tile, columns 0 .. n-1 of A and column n the row weights
+__host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 1); }
+// the two-buffer A'DA (global_load_lds of tile t + 1 in flight while the MFMAs run on tile t)
+// when both buffers and the factor fit in LDS; otherwise the single row-major tile
+__host__ __device__ inline bool dense_glds(int n) {
+    const int a = TILE * dense_ts(n), b = 2 * dense_gbuf(n);
+    return n <= 128 && (size_t)((a > b ? a : b) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
+}
+__host__ __device__ inline int dense_tiles(int n) {   // doubles of LDS before the factor
+    const int a = TILE * dense_ts(n), b = 2 * dense_gbuf(n);
+    return dense_glds(n) && b > a ? b : a;
+}
 __host__ __device__ inline bool dense_k_lds(int n) {
-    return (size_t)(TILE * dense_ts(n) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
+    return (size_t)(dense_tiles(n) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
 }
 __host__ __device__ inline size_t dense_lds_bytes(int n) {
-    return sizeof(double) * (size_t)(TILE * dense_ts(n) + (dense_k_lds(n) ? n * n : 0));
+    return sizeof(double) * (size_t)(dense_tiles(n) + (dense_k_lds(n) ? n * n : 0));
 }
 
 template <bool KL>   // KL: the factor lives in LDS (dense_k_lds(n)); a compile-time choice so that
@@ -661,7 +674,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double *rd = W + L.rd, *re = W + L.re;
     double *tA = W + L.tA, *lA = W + L.lA, *riA = W + L.riA, *rcA = W + L.rcA, *dtA = W + L.dtA, *dlA = W + L.dlA;
     double *tB = W + L.tB, *lB = W + L.lB, *riB = W + L.riB, *rcB = W + L.rcB, *dtB = W + L.dtB, *dlB = W + L.dlB;
-    double* K = KL ? dlds + TILE * ts : W + L.K;   // the factor (LDS when it fits)
+    double* K = KL ? dlds + dense_tiles(n) : W + L.K;   // the factor (LDS when it fits)
     double* Y = W + L.Y;
     double* S = W + L.S;
     auto up_present = [&](int j) -> bool { return ub && isfinite(ub[j]); };
@@ -918,7 +931,71 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             dbl4 acc[TPW];
 #pragma unroll
             for (int u = 0; u < TPW; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
-            for (int r0 = 0; r0 < m; r0 += TILE) {
+            const bool gl = KL && m > 0 && dense_glds(n);   // (m = 0: no rows, A may be null)
+            if (gl) {
+                // two column-major buffers: tile t + 1 is copied by global_load_lds (no VGPR
+                // staging) while the MFMAs consume tile t, one barrier per tile.  One 4-byte
+                // load per lane moves one column's 32 rows (256 B) - rows past m read row m - 1,
+                // whose weight slot is 0 - so each column lands at its own padded offset.
+                const int ntile = (m + TILE - 1) / TILE;
+                const int rowl = lane >> 1;
+                auto issue = [&](int t, double* buf) {
+                    const int ncol = min(n, 16 * (((int)tbound(t) + 15) / 16));
+                    const char* src = (const char*)(A + min(t * TILE + rowl, m - 1)) + 4 * (lane & 1);
+                    for (int j = wv; j < ncol; j += DT / 64)
+                        __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)j * m * sizeof(double)),
+                                                         (__attribute__((address_space(3))) void*)(buf + DQ_GB * j),
+                                                         4, 0, 0);
+                };
+                double* gb0 = dlds;
+                double* gb1 = dlds + dense_gbuf(n);
+                {
+                    const int rd0 = min(tid, min(TILE, m) - 1);
+                    const double la = lA[rd0], ta = tA[rd0];
+                    issue(0, gb0);
+                    if (tid < TILE) gb0[DQ_GB * n + tid] = tid < min(TILE, m) ? la / ta : 0.0;
+                }
+                __syncthreads();
+                for (int t = 0; t < ntile; ++t) {
+                    double* cur = (t & 1) ? gb1 : gb0;
+                    double* nxt = (t & 1) ? gb0 : gb1;
+                    const int r0 = t * TILE, rows = min(TILE, m - r0);
+                    const bool more = t + 1 < ntile;
+                    double la = 1.0, ta = 1.0;
+                    const int rows1 = more ? min(TILE, m - r0 - TILE) : 0;
+                    if (more) {
+                        const int rd1 = r0 + TILE + min(tid, rows1 - 1);
+                        la = lA[rd1]; ta = tA[rd1];
+                        issue(t + 1, nxt);
+                    }
+                    const double thi = tbound(t);
+                    double drv[TILE / 4];
+#pragma unroll
+                    for (int s4 = 0; s4 < TILE / 4; ++s4) {
+                        const int rr = 4 * s4 + k4;
+                        drv[s4] = rr < rows ? cur[DQ_GB * n + rr] : 0.0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < TPW; ++u) {
+                        if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
+                            const int ci = min(16 * tI[u] + c16, n - 1), cj = min(16 * tJ[u] + c16, n - 1);
+                            double ai[TILE / 4], aj[TILE / 4];
+#pragma unroll
+                            for (int s4 = 0; s4 < TILE / 4; ++s4) {
+                                const int rr = min(4 * s4 + k4, rows - 1);
+                                ai[s4] = cur[DQ_GB * ci + rr];
+                                aj[s4] = cur[DQ_GB * cj + rr];
+                            }
+#pragma unroll
+                            for (int s4 = 0; s4 < TILE / 4; ++s4)
+                                acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s4], drv[s4] * aj[s4], acc[u], 0, 0, 0);
+                        }
+                    }
+                    if (more && tid < TILE) nxt[DQ_GB * n + tid] = tid < rows1 ? la / ta : 0.0;
+                    __syncthreads();
+                }
+            }
+            for (int r0 = 0; r0 < (gl ? 0 : m); r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
                 // only the columns the tile's rows reach, to the 16-column block (the MFMA operands

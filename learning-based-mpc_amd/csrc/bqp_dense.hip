@@ -625,7 +625,8 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
 // it fits, the n x n factor K = L (lower) / L' (upper) itself: the Cholesky and the four
 // triangular solves per iteration then run on LDS instead of L2 round trips
 #define DENSE_LDS_MAX (152 * 1024)
-#define DQ_GB 33     // A'DA row-tile buffers filled by global_load_lds: column stride (32 rows + 1)
+#define DQ_GB 34     // A'DA row-tile buffers filled by global_load_lds: column stride (32 rows + 2:
+                     // 16-byte aligned columns, 16 lanes' b128 reads on distinct banks)
 __host__ __device__ inline int dense_ts(int n) { return 32 * ((n + 31) / 32) + 1; }
 // one A'DA buffer: column-major 32-row tile, columns 0 .. n-1 of A and column n the row weights
 __host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 1); }
@@ -642,8 +643,11 @@ __host__ __device__ inline int dense_tiles(int n) {   // doubles of LDS before t
 __host__ __device__ inline bool dense_k_lds(int n) {
     return (size_t)(dense_tiles(n) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
 }
+// + the reduction scratch (16) and the A tile bounds (DQ_THL) at the end: the kernel's only LDS
+// object is the dynamic array (a second __shared__ object made hipcc wait for the in-flight
+// global_load_lds before every LDS read)
 __host__ __device__ inline size_t dense_lds_bytes(int n) {
-    return sizeof(double) * (size_t)(dense_tiles(n) + (dense_k_lds(n) ? n * n : 0));
+    return sizeof(double) * (size_t)(dense_tiles(n) + (dense_k_lds(n) ? n * n : 0) + 16 + DQ_THL);
 }
 
 template <bool KL>   // KL: the factor lives in LDS (dense_k_lds(n)); a compile-time choice so that
@@ -653,9 +657,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
     if (inst >= a.batch) return;
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
-    __shared__ double sc[16];
-    __shared__ double thl[DQ_THL];   // tile bounds of A (below)
-    extern __shared__ double dlds[];
+    extern __shared__ __attribute__((aligned(16))) double dlds[];
+    double* sc = dlds + dense_tiles(n) + (KL ? n * n : 0);
+    double* thl = sc + 16;           // tile bounds of A (below)
     const int ts = dense_ts(n), tw = ts - 1;
     double* tileA = dlds;
     Red red{sc};
@@ -939,14 +943,24 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 // whose weight slot is 0 - so each column lands at its own padded offset.
                 const int ntile = (m + TILE - 1) / TILE;
                 const int rowl = lane >> 1;
+                // The copy is issued from inline asm (M0 = the column's LDS byte address): with
+                // the builtin, hipcc cannot tell the two buffers apart and waited for the copy of
+                // tile t + 1 before the first LDS read of tile t.  Its completion is waited for
+                // explicitly (vmcnt(0)) before the barrier that hands the buffer over.
                 auto issue = [&](int t, double* buf) {
                     const int ncol = min(n, 16 * (((int)tbound(t) + 15) / 16));
                     const char* src = (const char*)(A + min(t * TILE + rowl, m - 1)) + 4 * (lane & 1);
-                    for (int j = wv; j < ncol; j += DT / 64)
-                        __builtin_amdgcn_global_load_lds((const void*)(src + (int64_t)j * m * sizeof(double)),
-                                                         (__attribute__((address_space(3))) void*)(buf + DQ_GB * j),
-                                                         4, 0, 0);
+                    for (int j = wv; j < ncol; j += DT / 64) {
+                        const char* g = src + (int64_t)j * m * sizeof(double);
+                        const unsigned ldsa = __builtin_amdgcn_readfirstlane(
+                            (unsigned)(uintptr_t)(__attribute__((address_space(3))) double*)(buf + DQ_GB * j));
+                        unsigned keep;
+                        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                                     "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                                     : "=&s"(keep) : "v"(g), "s"(ldsa) : "memory");
+                    }
                 };
+                auto copy_wait = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
                 double* gb0 = dlds;
                 double* gb1 = dlds + dense_gbuf(n);
                 {
@@ -955,11 +969,12 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     issue(0, gb0);
                     if (tid < TILE) gb0[DQ_GB * n + tid] = tid < min(TILE, m) ? la / ta : 0.0;
                 }
+                copy_wait();
                 __syncthreads();
                 for (int t = 0; t < ntile; ++t) {
                     double* cur = (t & 1) ? gb1 : gb0;
                     double* nxt = (t & 1) ? gb0 : gb1;
-                    const int r0 = t * TILE, rows = min(TILE, m - r0);
+                    const int r0 = t * TILE;
                     const bool more = t + 1 < ntile;
                     double la = 1.0, ta = 1.0;
                     const int rows1 = more ? min(TILE, m - r0 - TILE) : 0;
@@ -969,22 +984,27 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                         issue(t + 1, nxt);
                     }
                     const double thi = tbound(t);
+                    // k-step s of lane group k4 takes row 8 k4 + s: each lane's 8 rows of a column
+                    // are contiguous, read as four ds_read_b128 (rows past the tile hold finite
+                    // copies of row m - 1 and weight 0)
                     double drv[TILE / 4];
+                    {
+                        const double2* dp = reinterpret_cast<const double2*>(cur + DQ_GB * n + 8 * k4);
 #pragma unroll
-                    for (int s4 = 0; s4 < TILE / 4; ++s4) {
-                        const int rr = 4 * s4 + k4;
-                        drv[s4] = rr < rows ? cur[DQ_GB * n + rr] : 0.0;
+                        for (int h = 0; h < TILE / 8; ++h) { const double2 v = dp[h]; drv[2 * h] = v.x; drv[2 * h + 1] = v.y; }
                     }
 #pragma unroll
                     for (int u = 0; u < TPW; ++u) {
                         if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
                             const int ci = min(16 * tI[u] + c16, n - 1), cj = min(16 * tJ[u] + c16, n - 1);
+                            const double2* pa = reinterpret_cast<const double2*>(cur + DQ_GB * ci + 8 * k4);
+                            const double2* pb = reinterpret_cast<const double2*>(cur + DQ_GB * cj + 8 * k4);
                             double ai[TILE / 4], aj[TILE / 4];
 #pragma unroll
-                            for (int s4 = 0; s4 < TILE / 4; ++s4) {
-                                const int rr = min(4 * s4 + k4, rows - 1);
-                                ai[s4] = cur[DQ_GB * ci + rr];
-                                aj[s4] = cur[DQ_GB * cj + rr];
+                            for (int h = 0; h < TILE / 8; ++h) {
+                                const double2 va = pa[h], vb = pb[h];
+                                ai[2 * h] = va.x; ai[2 * h + 1] = va.y;
+                                aj[2 * h] = vb.x; aj[2 * h + 1] = vb.y;
                             }
 #pragma unroll
                             for (int s4 = 0; s4 < TILE / 4; ++s4)
@@ -992,6 +1012,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                         }
                     }
                     if (more && tid < TILE) nxt[DQ_GB * n + tid] = tid < rows1 ? la / ta : 0.0;
+                    copy_wait();
                     __syncthreads();
                 }
             }

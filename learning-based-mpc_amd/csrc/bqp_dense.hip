@@ -280,6 +280,123 @@ __device__ __forceinline__ bool chol_1b(double* K, int n, double fl, double* jun
     return true;
 }
 
+// two pivots j, j + 1 per barrier (rank-2 trailing update): L(r, j) = K(r, j) / l_jj and
+// L(r, j+1) = (K(r, j+1) - L(r, j) a) / l_{j+1,j+1} (a = L(j+1, j)) formed in registers from
+// the unupdated columns, then K(r, c) -= L(r, j) L(c, j) + L(r, j+1) L(c, j+1) over the trailing
+// block from row / column j + 2 - one pass over the trailing triangle and one barrier for the
+// two pivots (chol_upd: one each).  Same operation order per entry as two chol_upd steps.
+template <int NB>
+__device__ __forceinline__ void chol_upd2(double* K, int n, int j, int rem2, double inv0, double a,
+                                          double inv1, double* junk) {
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const double* k0 = K + (int64_t)j * n + j + 2;         // column j, rows j + 2 ..
+    const double* k1 = K + (int64_t)(j + 1) * n + j + 2;   // column j + 1, rows j + 2 ..
+    double r0[NB], c0[NB], r1[NB], c1[NB];
+#pragma unroll
+    for (int p = 0; p < NB; ++p) {
+        const int ir = min(ty + 16 * p, rem2 - 1), ic = min(tx + 16 * p, rem2 - 1);
+        r0[p] = k0[ir]; c0[p] = k0[ic];
+        r1[p] = k1[ir]; c1[p] = k1[ic];
+    }
+#pragma unroll
+    for (int p = 0; p < NB; ++p) {
+        r0[p] *= inv0; c0[p] *= inv0;
+        r1[p] = (r1[p] - r0[p] * a) * inv1;
+        c1[p] = (c1[p] - c0[p] * a) * inv1;
+    }
+    if (ty == 0) {             // rows j and j + 1 of L' (upper triangle) from row j + 2 on
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int cc = tx + 16 * q;
+            if (cc < rem2) {
+                K[(int64_t)(j + 2 + cc) * n + j] = c0[q];
+                K[(int64_t)(j + 2 + cc) * n + j + 1] = c1[q];
+            }
+        }
+    }
+    double* jk = junk + (tid & 63);
+    constexpr int NH = (NB + 3) / 4;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+        double t[4][NB];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qq = 4 * h + q, cc = min(tx + 16 * qq, rem2 - 1);
+#pragma unroll
+            for (int p = 0; p < NB; ++p)
+                if (qq < NB && p >= qq)
+                    t[q][p] = K[(int64_t)(j + 2 + cc) * n + j + 2 + min(ty + 16 * p, rem2 - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qq = 4 * h + q, cc = tx + 16 * qq;
+#pragma unroll
+            for (int p = 0; p < NB; ++p) {
+                if (qq < NB && p >= qq) {
+                    const int rr = ty + 16 * p;
+                    double* dst = (cc < rem2 && rr < rem2 && rr >= cc) ? K + (int64_t)(j + 2 + cc) * n + j + 2 + rr : jk;
+                    *dst = (t[q][p] - r0[p] * c0[qq]) - r1[p] * c1[qq];
+                }
+            }
+        }
+    }
+}
+
+// chol_1b with two pivots per barrier (chol_upd2); a last odd pivot as in chol_1b
+__device__ __forceinline__ bool chol_2b(double* K, int n, double fl, double* junk) {   // inlined: K stays LDS
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    double lp0 = 0.0, lp1 = 0.0;
+    int jp = -1;                      // the previous step's first pivot (its diagonals are stored late)
+    int j = 0;
+    for (; j + 1 < n; j += 2) {
+        double d0 = K[(int64_t)j * n + j];
+        if (fl >= 0.0 && !(d0 > fl)) d0 = fl;
+        if (!(d0 > 0.0)) { __syncthreads(); return false; }   // uniform: every thread read d0
+        const double l00 = sqrt(d0), inv0 = 1.0 / l00;
+        const double a = K[(int64_t)j * n + j + 1] * inv0;     // L(j+1, j)
+        double d1 = K[(int64_t)(j + 1) * n + j + 1] - a * a;
+        if (fl >= 0.0 && !(d1 > fl)) d1 = fl;
+        if (!(d1 > 0.0)) { __syncthreads(); return false; }
+        const double l11 = sqrt(d1), inv1 = 1.0 / l11;
+        if (tid == 0) {
+            if (jp >= 0) {
+                K[(int64_t)jp * n + jp] = lp0;
+                K[(int64_t)(jp + 1) * n + jp + 1] = lp1;
+            }
+            K[(int64_t)(j + 1) * n + j] = a;                  // row j of L', entry j + 1
+        }
+        jp = j; lp0 = l00; lp1 = l11;
+        const int rem2 = n - j - 2;
+        switch ((rem2 + 15) >> 4) {     // block-uniform; each case branch-free inside
+            case 1: chol_upd2<1>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 2: chol_upd2<2>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 3: chol_upd2<3>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 4: chol_upd2<4>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 5: chol_upd2<5>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 6: chol_upd2<6>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 7: chol_upd2<7>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            case 8: chol_upd2<8>(K, n, j, rem2, inv0, a, inv1, junk); break;
+            default: break;
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && jp >= 0) {
+        K[(int64_t)jp * n + jp] = lp0;
+        K[(int64_t)(jp + 1) * n + jp + 1] = lp1;
+    }
+    if (j < n) {                      // the last pivot of an odd n (nothing trails it)
+        double d = K[(int64_t)j * n + j];
+        if (fl >= 0.0 && !(d > fl)) d = fl;
+        __syncthreads();              // every thread has read d before thread 0 overwrites it
+        if (!(d > 0.0)) return false;
+        if (tid == 0) K[(int64_t)j * n + j] = sqrt(d);
+    }
+    for (int c = ty; c < n; c += 16)                 // lower <- upper: L(r, c) = K[r n + c]
+        for (int r = c + 1 + tx; r < n; r += 16) K[(int64_t)c * n + r] = K[(int64_t)r * n + c];
+    __syncthreads();
+    return true;
+}
+
 // solve L L' x = b in place (x in LDS vector xs of length n), thread-parallel dot products
 template <int NTH = DT, class R = Red>
 __device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
@@ -1124,7 +1241,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         }
         const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
         DST(1);
-        if (!(n <= 128 ? chol_1b(K, n, kfl, tileA) : block_cholesky(K, n, sc, kfl))) return false;
+        if (!(n <= 128 ? chol_2b(K, n, kfl, tileA) : block_cholesky(K, n, sc, kfl))) return false;
         DST(2);
         // Y = K^{-1} Aeq' (one thread per equality row), S = Aeq Y
         for (int r = tid; r < me; r += DT) {
@@ -1260,7 +1377,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             K[e2] = H[e2] + (i == j ? sh : 0.0);
         }
         __syncthreads();
-        if (!(n <= 128 ? chol_1b(K, n, -1.0, tileA) : block_cholesky(K, n, sc, -1.0))) flag = -6;
+        if (!(n <= 128 ? chol_2b(K, n, -1.0, tileA) : block_cholesky(K, n, sc, -1.0))) flag = -6;
     }
     double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0, cmax = 0.0;
     residuals(stat, feq, fin, csum, gscale, zmax, cmax);

@@ -138,10 +138,63 @@ def ocp_dict(prob):
                 Fp=prob.Fp, hp=prob.hp, kp=prob.poly_stage)
 
 
+def host_cpu_quota():
+    """CPUs the cgroup lets this process use (cgroup v2 cpu.max / v1 cfs quota), or None when
+    unlimited: on the GPU box the affinity mask shows the whole machine (256 CPUs) while the
+    job's quota is its per-GPU share, so threads beyond the quota only contend."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            return float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def sweep_points(share):
+    """thread counts of the CPU-baseline sweep: 1, 16, 64, 128 and every core of the affinity
+    mask, plus the per-GPU share the box sets (OMP_NUM_THREADS)"""
+    present = len(os.sched_getaffinity(0))
+    pts = sorted({t for t in (1, 16, 64, 128, present, share) if 1 <= t <= present})
+    return pts, present
+
+
+def thread_sweep(rate, share, unit, what):
+    """CPU baseline over a thread sweep: rate(nthr, eff) -> (units/s, sample size) where eff is
+    the parallelism the work should be sized for (min(nthr, cgroup quota)).  value = the best
+    point, cores = its thread count; every point is reported."""
+    pts, present = sweep_points(share)
+    quota = host_cpu_quota()
+    sweep = {}
+    for t in pts:
+        eff = t if quota is None else max(1, min(t, int(round(quota))))
+        sweep[t] = rate(t, eff)
+    best = max(pts, key=lambda t: sweep[t][0])
+    note = ('every core of the affinity mask (%d) is available' % present if quota is None else
+            'the cgroup CPU quota of this job is %.1f CPUs of the %d in the affinity mask: thread '
+            'counts above it time-share the quota (contention), so the all-mask point is not '
+            'an all-core figure' % (quota, present))
+    return dict(value=round(sweep[best][0], 2), unit=unit, cores=best, kind='port',
+                sweep={str(t): round(v[0], 2) for t, v in sweep.items()},
+                single_core=round(sweep[1][0], 2),
+                share_value=round(sweep[share][0], 2) if share in sweep else None,
+                share_cores=share, cores_present=present, cpu_quota=quota,
+                cores_note='value = the best point of the thread sweep (threads = cores); ' + note,
+                sample=what % {'pts': '/'.join(str(t) for t in pts),
+                               'n': ', '.join('%d@%d' % (v[1], t) for t, v in sweep.items())})
+
+
 def cpu_reference(prob, sample, threads, timed):
     """CPU leg: the C restatement of the same IPM (oracle/cpu_ipm.c), fp64.  Returns the
     per-instance iteration counts of the sample (K_ref of the algorithmic flop count, SURVEY.md
-    8(d)) and, if timed, single-core and all-core throughput on a bounded sample."""
+    8(d)) and, if timed, the throughput over a thread sweep on a bounded sample."""
     from oracle import cpu_ref
     ocp = ocp_dict(prob)
     cpu_ref.lib()
@@ -156,52 +209,40 @@ def cpu_reference(prob, sample, threads, timed):
     t0 = time.perf_counter(); cpu_ref.solve(ocp, X[:n1], threads=1, **kw1); t1 = time.perf_counter()
     single = n1 / (t1 - t0)
 
-    def timed_run(nthr):
-        # about one second of work on nthr threads (at least 64 QPs per thread)
-        want = max(64 * nthr, int(single * nthr * 1.0))
+    def rate(nthr, eff):
+        # about one second of work on the parallelism the box grants (at least 64 QPs per thread)
+        want = max(64 * nthr, int(single * eff * 1.0))
         reps = max(1, int(np.ceil(want / len(X))))
         kwa = {k: np.concatenate([v] * reps) for k, v in kw.items()}
         Xa = np.concatenate([X] * reps)
         t0 = time.perf_counter(); cpu_ref.solve(ocp, Xa, threads=nthr, **kwa); t1 = time.perf_counter()
         return len(Xa) / (t1 - t0), len(Xa)
 
-    # every host core of the box (the affinity mask), and beside it the per-GPU
-    # share of the box's cores (OMP_NUM_THREADS) that the driver sets
-    present = len(os.sched_getaffinity(0))
-    allc, nall = timed_run(present)
-    share, nsh = (allc, nall) if threads == present else timed_run(threads)
-    return dict(value=round(allc, 1), unit='QP-steps/s', cores=present, kind='port',
-                single_core=round(single, 1), share_value=round(share, 1), share_cores=threads,
-                sample='%d QPs on all %d host cores, %d QPs on the %d-core per-GPU share and %d '
-                       'single-core, of the same workload; oracle/cpu_ipm.c (same IPM, fp64, -O3 '
-                       '-march=native, OpenMP)' % (nall, present, nsh, threads, n1)), kref
+    return thread_sweep(rate, threads, 'QP-steps/s',
+                        'thread sweep %(pts)s over the same workload (QPs@threads: %(n)s); '
+                        'oracle/cpu_ipm.c (same IPM, fp64, -O3 -march=native, OpenMP, per-thread '
+                        'workspaces)'), kref
 
 
 def cll_cpu_baseline(g, X0, threads):
     """CPU leg of the CLL line: oracle/cpu_lbmpc.c, the C restatement of the same closed loop
     (exact-Hessian SQP, dense IPM + polish, RK4 plant, window update; fp64, -O3 -march=native,
-    OpenMP over instances) - 3 steps from the first instances' states, on every host core of the
-    box, on the per-GPU core share and on one core."""
+    OpenMP over instances) - 3 steps from the first instances' states, over a thread sweep."""
     from oracle import cpu_lbmpc                  # CPU leg only
     from oracle.mg_model import mg_problem
     mg = mg_problem()
     cpu_lbmpc.lib()
 
-    def rate(nthr, ninst):
+    def rate(nthr, eff):
+        ninst = max(4 * eff, nthr)
         xi = X0[np.arange(ninst) % len(X0)]
         t0 = time.perf_counter()
         cpu_lbmpc.loop(mg, dict(g), 100, 100, 3, xi, threads=nthr)
         return 3 * ninst / (time.perf_counter() - t0), ninst
 
-    single, n1 = rate(1, 4)
-    present = len(os.sched_getaffinity(0))
-    allc, nall = rate(present, 4 * present)
-    share, nsh = (allc, nall) if threads == present else rate(threads, 4 * threads)
-    return dict(value=round(allc, 2), unit='instance-steps/s', cores=present, kind='port',
-                single_core=round(single, 2), share_value=round(share, 2), share_cores=threads,
-                sample='3 closed-loop steps of %d instances on all %d host cores, %d on the %d-core '
-                       'per-GPU share and %d single-core; oracle/cpu_lbmpc.c (same algorithm, '
-                       'fp64, -O3 -march=native, OpenMP)' % (nall, present, nsh, threads, n1))
+    return thread_sweep(rate, threads, 'instance-steps/s',
+                        'thread sweep %(pts)s, 3 closed-loop steps per instance (instances@threads: '
+                        '%(n)s); oracle/cpu_lbmpc.c (same algorithm, fp64, -O3 -march=native, OpenMP)')
 
 
 def free_port():
@@ -346,10 +387,12 @@ def main():
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
     args = ap.parse_args()
-    if args.config in ('C1', 'CL', 'CLL', 'C2H', 'C2D'):
+    if args.config in ('C1', 'C2H', 'C2D'):
         return bench_aux(args)
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         return launch_ranks(args)
+    if args.config in ('CL', 'CLL'):
+        return bench_loop(args)
 
     import torch
     import torch.distributed as dist
@@ -463,10 +506,6 @@ def main():
             threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or present
             # the CPU baseline is timed at N=1 only (the multi-GPU lines carry K_ref, not a timing)
             cpu, kref_u = cpu_reference(prob, wl['sample'], threads, not args.no_cpu and world == 1)
-            if cpu is not None:
-                cpu['cores_present'] = present
-                cpu['cores_note'] = ('value: every core in the affinity mask; share_value: '
-                                     'OMP_NUM_THREADS threads (the per-GPU CPU share the box sets)')
             # algorithmic flops per launch: sum over the batch of K_ref x F_iter;
             # instances the reference solver does not converge on (infeasible) count with their
             # own iteration count
@@ -595,17 +634,212 @@ def cll_subproblem_roofline(dl, X0, h):
                      (nz, mr, B, its.mean(), dict(zip(*[v.tolist() for v in np.unique(flag, return_counts=True)]))))
 
 
+def loop_workload(cfg, batch, rank, world):
+    """Closed-loop configs: the instances of the whole job are numbered
+    globally and rank r runs its contiguous shard [r B, (r + 1) B) (weak scaling: B per GPU), so
+    the trajectories a rank produces do not depend on the number of ranks.
+    CL  the DSS tracking LMPC loop (DMS_tracking_LMPC_casadi.m:153-189, N = 100, RK4 plant) from
+        the stored DSS_tLMPC.mat states cycled;
+    CLL the learned-model NLP loop (DMS_LBMPC_casadi.m:163-218, N = 100, q = 100) from x_init
+        (:99) and seeded perturbations of it (+-0.005 in x1, x2)."""
+    import bqp
+    d, ts = _mg_design()
+    B = batch or (256 if cfg == 'CLL' else 1024)
+    gi = np.arange(rank * B, (rank + 1) * B)
+    if cfg == 'CL':
+        gl = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
+        mpc = bqp.TrackingLMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                               d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], ts['F_w_N'],
+                               ts['h_w_N'], d['x_wp'], d['u_wp'], N=100)
+        X0 = gl['x'][gi % len(gl['x'])]
+        return dict(mpc=mpc, X0=X0, gidx=gi, B=B,
+                    text='CL: DSS tracking LMPC closed loop (N=100, RK4 plant), batch %d per GPU' % B,
+                    data='initial states = stored DSS_tLMPC.mat states cycled',
+                    metric='closed-loop MPC steps/s (DSS tracking LMPC N=100, RK4 plant)')
+    g = np.load(os.path.join(GOLD, 'lbmpc_instance.npz'))
+    mpc = bqp.DMSLBMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
+                       d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], g['F_w_N'], g['h_w_N'],
+                       g['F_x_d'], g['h_x_d'], d['x_wp'], d['u_wp'], N=100)
+    x_init = np.array([0.15, 1.2875, 1.1547, 0.0])
+    # perturbation of global instance i: row i of a seed-11 stream (independent of world size)
+    P = np.random.default_rng(11).uniform(-1, 1, ((rank + 1) * B, 4))[gi]
+    X0 = x_init + P * np.array([0.005, 0.005, 0.0, 0.0])
+    if rank == 0:
+        X0[0] = x_init                                     # DMS_LBMPC_casadi.m:99
+    return dict(mpc=mpc, X0=X0, gidx=gi, B=B, g=g,
+                text='CLL: DMS LBMPC closed loop (N=100, q=100), batch %d per GPU' % B,
+                data='x_init of DMS_LBMPC_casadi.m and seeded perturbations (+-0.005 in x1, x2)',
+                metric='learned-model NLP closed-loop steps/s (DMS_LBMPC_casadi.m, N=100, q=100)')
+
+
+class LoopRunner:
+    """One rank's closed loops on its GPU (bqp.closed_loop / bqp.closed_loop_sqp)."""
+
+    def __init__(self, cfg, wl, local):
+        import bqp
+        self.bqp, self.cfg, self.wl = bqp, cfg, wl
+        self.h = bqp.Handle(local)
+
+    def run(self, steps):
+        b = self.bqp
+        if self.cfg == 'CL':
+            r = b.closed_loop(self.wl['mpc'], self.wl['X0'], steps, handle=self.h)
+        else:
+            r = b.closed_loop_sqp(self.wl['mpc'], self.wl['X0'], steps,
+                                  learning=dict(q=100, mask=1), handle=self.h)
+        return r
+
+    def kernel_ms(self):
+        return self.h.kernel_ms()[0]
+
+
+class StubLoop:
+    """CPU dry run of the multi-rank closed-loop harness (--dry-run, gloo): a deterministic stand-in
+    for the loop (x+ = 0.9 x + 0.01 sin(sum x) + u, u = -0.1 sum x), so the per-rank shards, the
+    timing and the trajectory all-gather run without a GPU and can be compared with the unsharded
+    run."""
+
+    def __init__(self, cfg, wl):
+        self.cfg, self.wl = cfg, wl
+
+    @staticmethod
+    def simulate(X0, steps, learned):
+        b, n = X0.shape
+        X = np.zeros((b, steps + 1, n)); U = np.zeros((b, steps, 1))
+        X[:, 0] = X0
+        for k in range(steps):
+            u = -0.1 * X[:, k].sum(axis=1)
+            U[:, k, 0] = u
+            X[:, k + 1] = 0.9 * X[:, k] + 0.01 * np.sin(X[:, k].sum(axis=1))[:, None] + u[:, None]
+        fl = (np.floor(np.abs(U[:, :, 0]) * 1e3) % 2).astype(np.int32)
+        r = dict(X=X, U=U, exitflag=fl)
+        if learned:
+            r['XL'] = X + 1e-3
+        return r
+
+    def run(self, steps):
+        return self.simulate(self.wl['X0'], steps, self.cfg == 'CLL')
+
+    def kernel_ms(self):
+        return None
+
+
+def bench_loop(args):
+    """CL / CLL on N ranks (north_star: "an RCCL all-gather over xGMI only to
+    collect trajectories"): each rank runs the closed loops of its shard for --steps steps (one
+    call: solve + plant + window per step on its GPU, no communication), timed between barriers
+    with the max over ranks; then one all-gather per trajectory array - X (B, steps+1, 4), U
+    (B, steps, 1), the exit flags (B, steps) and for CLL the learned predictions XL - assembles the
+    whole job's trajectories on every rank (bqp.dist.gather_rows; RCCL on the GPU box, gloo in the
+    dry run).  value = instance-steps/s of all ranks."""
+    import torch
+    import torch.distributed as dist
+    from bqp import dist as bd
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('gloo' if args.dry_run else 'nccl')
+    if args.dry_run:
+        dev = torch.device('cpu')
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device('cuda', local)
+    wl = loop_workload(args.config, args.batch, rank, world)
+    B = wl['B']
+    runner = StubLoop(args.config, wl) if args.dry_run else LoopRunner(args.config, wl, local)
+    if args.warmup > 0:
+        runner.run(1)                                   # module load, workspaces
+    if not args.dry_run:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    r = runner.run(args.steps)
+    if not args.dry_run:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = bd.max_over_ranks(time.perf_counter() - t0, dev, world)
+    kms = runner.kernel_ms()
+    # trajectory collection: one all-gather per array after the timed region
+    total = B * world
+    names = ['X', 'U', 'exitflag'] + (['XL'] if args.config == 'CLL' else [])
+    tg0 = time.perf_counter()
+    gathered = {}
+    nbytes = 0
+    for k in names:
+        t = torch.from_numpy(np.ascontiguousarray(r[k])).to(dev)
+        gathered[k] = bd.gather_rows(t, total, world).cpu().numpy()
+        nbytes += gathered[k].nbytes
+    t_gather = bd.max_over_ranks(time.perf_counter() - tg0, dev, world)
+    fl = gathered['exitflag']
+    check = dict(converged_frac_all_ranks=float((fl == 1).mean()),
+                 gathered_instances=int(gathered['X'].shape[0]),
+                 gathered_bytes=int(nbytes), gather_s=round(t_gather, 4))
+    if 'iterations' in r and r.get('iterations') is not None:
+        check.update(sqp_iterations_mean=float(np.mean(r['iterations'])),
+                     sqp_iterations_max=int(np.max(r['iterations'])))
+    if args.dry_run and rank == 0:
+        full = loop_workload(args.config, B * world, 0, 1)
+        # the stub's per-instance result depends only on the instance's own x0, so the unsharded
+        # run of the same global instances must equal the gathered shards
+        X0_all = np.concatenate([loop_workload(args.config, B, q, world)['X0'] for q in range(world)])
+        ref = StubLoop.simulate(X0_all, args.steps, args.config == 'CLL')
+        check['gather_matches_unsharded'] = bool(all(np.array_equal(gathered[k], ref[k]) for k in names))
+        check['x0_independent_of_world'] = bool(np.array_equal(full['X0'], X0_all))
+    line = None
+    if rank == 0:
+        cpu, roof = None, None
+        if args.config == 'CLL' and not args.dry_run:
+            g = wl['g']
+            X0 = wl['X0']
+            st = np.load(os.path.join(GOLD, 'dms_lbmpc_loops.npz'))['DMS_tLBMPC_q100']
+            e0 = np.abs(gathered['X'][0] - st[:args.steps + 1])
+            check.update(x_init_vs_stored_q100_slow_max=float(e0[:, :2].max()),
+                         x_init_vs_stored_q100_all_max=float(e0.max()))
+            roof = cll_subproblem_roofline(wl['mpc'], X0, runner.h)
+            if not args.no_cpu and world == 1:
+                present = len(os.sched_getaffinity(0))
+                cpu = cll_cpu_baseline(g, X0, int(os.environ.get('OMP_NUM_THREADS', '0')) or present)
+        elif args.config == 'CL' and not args.dry_run and not args.no_cpu and world == 1:
+            from oracle import cpu_ref, qp_forms          # CPU leg only
+            from oracle.mg_model import mg_problem, mg_rk4
+            mgp = mg_problem()
+            _, ts = _mg_design()
+            ocp = qp_forms.dms_ocp(mgp, 100, ts['F_w_N'], ts['h_w_N'])
+            c0 = time.perf_counter()
+            x = wl['X0'][:16].copy()
+            for k in range(10):
+                c = cpu_ref.solve(ocp, x - mgp['x_wp'], threads=1)
+                u = c['u'][:, 0, 0] + mgp['u_wp']
+                x = np.array([mg_rk4(0.01, x[i], u[i]) for i in range(len(x))])
+            cpu = dict(value=round(16 * 10 / (time.perf_counter() - c0), 1), unit='instance-steps/s',
+                       cores=1, kind='port', sample='16 instances x 10 steps, oracle/cpu_ipm.c + numpy RK4')
+        line = dict(metric=wl['metric'], value=round(total * args.steps / elapsed, 1),
+                    unit='instance-steps/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
+                    ms_per_step=round(1e3 * elapsed / args.steps, 4), higher_is_better=True,
+                    scaling='weak', vs_baseline=None, dtype='f64',
+                    data=wl['data'] + (' [CPU dry run: stub loop, gloo]' if args.dry_run else ''),
+                    config={'workload': wl['text'] + ', %d steps' % args.steps, 'batch_per_gpu': B,
+                            'horizon': 100, 'parallelism': 'dp%d' % world},
+                    roofline=roof, kernel_ms=None if kms is None else round(kms, 4),
+                    cpu_baseline=cpu, check=check)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def bench_aux(args):
     """Single-GPU measurements of the SURVEY.md §8(f) paths (not the driver's bench line):
     C1  LBMPC (fmincon form F3, costLBMPC.m / constraintsLBMPC.m), N=10, NW window
         train_data(:, 1:100), Gauss-Newton SQP on the GPU (bqp_lbmpc_solve_batched); one step =
         one batched SQP solve (default batch 1 = the reference's single-instance config);
-    CL  closed-loop DSS tracking LMPC (N=100, RK4 plant), one step = one batched closed-loop
-        step (solve + plant) over --batch initial states; timed over --steps steps of one loop;
-    CLL the learned-model NLP loop of DMS_LBMPC_casadi.m (bqp_closed_loop_sqp), same step unit.
-    The CPU leg is the numpy restatement (oracle/lbmpc.py, interpreted) for C1, the C
-    restatement + numpy RK4 for CL and the C restatement of the whole loop (oracle/cpu_lbmpc.c)
-    for CLL, on a bounded sample."""
+    C2H / C2D  the C2 workload through the host-pointer entry point / in quadprog form.
+    The CPU leg of C1 is the numpy restatement (oracle/lbmpc.py, interpreted), on a bounded
+    sample.  The closed-loop configs CL / CLL run on N ranks: bench_loop."""
     import time as _t
     import torch
     import bqp
@@ -753,77 +987,6 @@ def bench_aux(args):
                                       kind='port', sample='%d solves of oracle/lbmpc.py (numpy)' % ns),
                     check=dict(converged_frac=float((r.exitflag == 1).mean()),
                                mean_sqp_iterations=float(r.iterations.mean())))
-    elif args.config == 'CLL':
-        # the learned-model NLP closed loop of DMS_LBMPC_casadi.m (cost on the learned states,
-        # 8 x 100 window): per step the GN-SQP with the exact Hessian, the RK4 plant and the
-        # window update, all on the GPU (bqp_closed_loop_sqp), over --batch initial states
-        g = np.load(os.path.join(GOLD, 'lbmpc_instance.npz'))
-        dl = bqp.DMSLBMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
-                          d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], g['F_w_N'], g['h_w_N'],
-                          g['F_x_d'], g['h_x_d'], d['x_wp'], d['u_wp'], N=100)
-        B = args.batch or 256
-        rng = np.random.default_rng(11)
-        x_init = np.array([0.15, 1.2875, 1.1547, 0.0])
-        X0 = x_init + rng.uniform(-1, 1, (B, 4)) * np.array([0.005, 0.005, 0.0, 0.0])
-        X0[0] = x_init                                     # DMS_LBMPC_casadi.m:99
-        bqp.closed_loop_sqp(dl, X0, 1, learning=dict(q=100, mask=1), handle=h)
-        t0 = _t.perf_counter()
-        r = bqp.closed_loop_sqp(dl, X0, args.steps, learning=dict(q=100, mask=1), handle=h)
-        el = _t.perf_counter() - t0
-        kms = h.kernel_ms()[0]
-        st = np.load(os.path.join(GOLD, 'dms_lbmpc_loops.npz'))['DMS_tLBMPC_q100']
-        e0 = np.abs(r.X[0] - st[:args.steps + 1])
-        roof = cll_subproblem_roofline(dl, X0, h)
-        present = len(os.sched_getaffinity(0))
-        cpu = None if args.no_cpu else cll_cpu_baseline(g, X0, int(os.environ.get('OMP_NUM_THREADS', '0')) or present)
-        line = dict(metric='learned-model NLP closed-loop steps/s (DMS_LBMPC_casadi.m, N=100, q=100)',
-                    value=round(B * args.steps / el, 1), unit='instance-steps/s', n_gpus=1,
-                    steps=args.steps, warmup=1, ms_per_step=round(1e3 * el / args.steps, 4),
-                    higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
-                    data='x_init of DMS_LBMPC_casadi.m and seeded perturbations (+-0.005 in x1, x2)',
-                    config={'workload': 'CLL: DMS LBMPC closed loop, batch %d, %d steps' % (B, args.steps),
-                            'batch_per_gpu': B, 'horizon': 100, 'parallelism': 'dp1'},
-                    roofline=roof, kernel_ms=round(kms, 4),
-                    cpu_baseline=cpu,
-                    check=dict(converged_frac=float((r.exitflag == 1).mean()),
-                               sqp_iterations_mean=float(r.iterations.mean()),
-                               sqp_iterations_max=int(r.iterations.max()),
-                               x_init_vs_stored_q100_slow_max=float(e0[:, :2].max()),
-                               x_init_vs_stored_q100_all_max=float(e0.max())))
-    else:
-        gl = np.load(os.path.join(GOLD, 'dms_DSS_tLMPC.npz'))
-        tl = bqp.TrackingLMPC(d['A'], d['B'], d['Q'], d['R'], d['P'], float(d['T']), d['LAMBDA'],
-                              d['PSI'], d['F_x'], d['h_x'], d['F_u'], d['h_u'], ts['F_w_N'],
-                              ts['h_w_N'], d['x_wp'], d['u_wp'], N=100)
-        B = args.batch or 1024
-        X0 = gl['x'][np.arange(B) % len(gl['x'])]
-        bqp.closed_loop(tl, X0, 2, handle=h)
-        t0 = _t.perf_counter()
-        r = bqp.closed_loop(tl, X0, args.steps, handle=h)
-        el = _t.perf_counter() - t0
-        kms = h.kernel_ms()[0]
-        from oracle import cpu_ref, qp_forms          # CPU leg only
-        from oracle.mg_model import mg_problem, mg_rk4
-        mgp = mg_problem()
-        ocp = qp_forms.dms_ocp(mgp, 100, ts['F_w_N'], ts['h_w_N'])
-        c0 = _t.perf_counter()
-        x = X0[:16].copy()
-        for k in range(10):
-            c = cpu_ref.solve(ocp, x - mgp['x_wp'], threads=1)
-            u = c['u'][:, 0, 0] + mgp['u_wp']
-            x = np.array([mg_rk4(0.01, x[i], u[i]) for i in range(len(x))])
-        cpu = 16 * 10 / (_t.perf_counter() - c0)
-        line = dict(metric='closed-loop MPC steps/s (DSS tracking LMPC N=100, RK4 plant)',
-                    value=round(B * args.steps / el, 1), unit='instance-steps/s', n_gpus=1,
-                    steps=args.steps, warmup=1, ms_per_step=round(1e3 * el / args.steps, 4),
-                    higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
-                    data='initial states = stored DSS_tLMPC.mat states cycled',
-                    config={'workload': 'CL: closed loop, batch %d, %d steps' % (B, args.steps),
-                            'batch_per_gpu': B, 'horizon': 100, 'parallelism': 'dp1'},
-                    roofline=None, kernel_ms=round(kms, 4),
-                    cpu_baseline=dict(value=round(cpu, 1), unit='instance-steps/s', cores=1,
-                                      kind='port', sample='16 instances x 10 steps, oracle/cpu_ipm.c + numpy RK4'),
-                    check=dict(converged_frac=float((r.exitflag == 1).mean())))
     print(json.dumps(line))
 
 

@@ -141,6 +141,8 @@ int bqp_create(bqp_handle* h, int device);
 int bqp_destroy(bqp_handle h);
 void bqp_default_options(bqp_options* opt);
 const char* bqp_version(void);
+/* SHA-1 of the sources the library was built from (csrc files in name order, then include/bqp.h) */
+const char* bqp_build_source_sha1(void);
 
 /* Host-pointer structured solve.  Outputs (host): x batch*(N+1)*nx, u batch*N*nu,
  * theta batch*np, fval batch, exitflag batch, out batch (out/fval/duals may be NULL). */
@@ -164,6 +166,9 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* dims, int bat
  *   min 0.5 x'Hx + f'x  s.t.  A x <= b, Aeq x = beq, lb <= x <= ub.
  * H n*n, f n, A m*n, b m, Aeq me*n, beq me, lb/ub n (NULL = unbounded), x0 ignored (IPM).
  * lambda outputs follow quadprog: H x + f + A'l_ineqlin + Aeq'l_eqlin - l_lower + l_upper = 0.
+ * H: as quadprog, the host entry solves with the symmetric part (H + H')/2 (a symmetric H is
+ * used bit for bit); the _device entry takes H as given and requires it symmetric (the kernels
+ * read both triangles).
  * ---------------------------------------------------------------------------------------- */
 typedef struct {
     int n;   /* variables */

@@ -69,7 +69,7 @@ class LbmpcData(C.Structure):
                 ('bandwidth', C.c_double), ('lambda_', C.c_double)]
 
 
-EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version',
+EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version', 'bqp_build_source_sha1',
            'bqp_solve_ocp_batched', 'bqp_solve_ocp_batched_device', 'bqp_quadprog_batched',
            'bqp_quadprog_batched_device', 'bqp_last_kernel_ms', 'bqp_nw_oracle',
            'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device',
@@ -93,6 +93,7 @@ def load():
                        '__graft_entry__.build()' % LIB_PATH)
     lib = C.CDLL(LIB_PATH)
     lib.bqp_version.restype = C.c_char_p
+    lib.bqp_build_source_sha1.restype = C.c_char_p
     lib.bqp_create.argtypes = [C.POINTER(C.c_void_p), C.c_int]
     lib.bqp_destroy.argtypes = [C.c_void_p]
     lib.bqp_default_options.argtypes = [C.POINTER(Options)]

@@ -118,7 +118,7 @@ class _LearnedOCP:
         self.Bx = np.vstack(rx)
         self.Ain_cm = np.ascontiguousarray(self.Ain.T)             # column-major m x nz
 
-    def _solve(self, x0, data, z0, handle, max_iter, tol):
+    def _solve(self, x0, data, z0, handle, max_iter, tol, polish=0):
         lib = _lib.load()
         h = handle or _default_handle()
         x0 = np.ascontiguousarray(np.atleast_2d(x0), dtype=np.float64)
@@ -138,7 +138,7 @@ class _LearnedOCP:
                               mrows, mask, int(self.hessian == 'exact'))
         dd = _lib.LbmpcData(*[_lib.ptr(a) for a in keep], _lib.ptr(w), sd, _lib.ptr(x0), self.n,
                             _lib.ptr(self.Ain_cm), _lib.ptr(bin_), mrows, self.bandwidth, self.lam)
-        o = _lib.options(max_iter=max_iter, tol_stat=tol)
+        o = _lib.options(max_iter=max_iter, tol_stat=tol, polish=polish)
         rc = lib.bqp_lbmpc_solve_batched(h.value, C.byref(dims), b, C.byref(dd), C.byref(o),
                                          _lib.ptr(z), _lib.ptr(lam), _lib.ptr(cost),
                                          _lib.iptr(flag), _lib.iptr(it))
@@ -155,11 +155,13 @@ class LBMPC(_LearnedOCP):
                          F_x_d, h_x_d, N, w_run=1.0, n_run=max(N - 2, 0), term_learned=True,
                          n_box=N - 1, xs=xs, bandwidth=bandwidth, lam=lam)
 
-    def solve(self, dx, data, opt_var0=None, handle=None, max_iter=50, tol=1e-8):
+    def solve(self, dx, data, opt_var0=None, handle=None, max_iter=50, tol=1e-8, polish=0):
         """dx (batch, n) states w.r.t. the working point, data the NW window (7 x q, or batch
         x 7 x q, or {X, Y}), opt_var0 the warm start (ocpLBMPC.m:31 passes the previous
-        opt_var).  Returns opt_var (batch, N*m + m) = [c; theta], c0, du0 = K dx + c0."""
-        r = self._solve(dx, data, opt_var0, handle, max_iter, tol)
+        opt_var).  polish: the QP sub-problems' active-set polish (bqp_options.polish: 0/1/2
+        after 0 / -8 sub-problem exits, every sub-problem once the SQP stalls; 3 only once it
+        stalls; -1 off).  Returns opt_var (batch, N*m + m) = [c; theta], c0, du0 = K dx + c0."""
+        r = self._solve(dx, data, opt_var0, handle, max_iter, tol, polish)
         dx = np.atleast_2d(dx)
         c0 = r.z[:, :self.m]
         r.update(opt_var=r.z, c0=c0, theta=r.z[:, self.N * self.m:],
@@ -180,7 +182,7 @@ class HybridLBMPC(_LearnedOCP):
         self.x_eq = np.asarray(x_eq, float).ravel()
         self.u_eq = np.atleast_1d(np.asarray(u_eq, float)).ravel()
 
-    def solve(self, xmeasure, data, y0=None, handle=None, max_iter=50, tol=1e-8):
+    def solve(self, xmeasure, data, y0=None, handle=None, max_iter=50, tol=1e-8, polish=0):
         """xmeasure (batch, n) absolute states, data the 7 x q window (or 8 x q with the validity
         row).  Returns y_OL (batch, (N+1)n + Nm + p) in the reference's layout (nominal state
         trajectory, inputs, theta) and u0."""
@@ -192,7 +194,7 @@ class HybridLBMPC(_LearnedOCP):
             y0 = np.atleast_2d(y0)
             z0 = np.concatenate([y0[:, (N + 1) * n:(N + 1) * n + N * m] - np.tile(self.u_eq, N),
                                  y0[:, -self.p:]], axis=1)
-        r = self._solve(x0, data, z0, handle, max_iter, tol)
+        r = self._solve(x0, data, z0, handle, max_iter, tol, polish)
         b = xm.shape[0]
         u = r.z[:, :N * m].reshape(b, N, m)
         X = np.zeros((b, N + 1, n)); X[:, 0] = x0
@@ -220,9 +222,10 @@ class DMSLBMPC(HybridLBMPC):
                          h_x_d, x_eq, u_eq, N, delta=delta, bandwidth=bandwidth, lam=lam)
         self.term_learned = True
 
-    def solve(self, xmeasure, data, y0=None, handle=None, max_iter=200, tol=1e-8):
+    def solve(self, xmeasure, data, y0=None, handle=None, max_iter=200, tol=1e-8, polish=0):
         """as HybridLBMPC.solve, data the 8 x q window [X; Y; v] (or 7 x q: every point valid);
         with hessian = 'gn' the iteration converges linearly on these learned costs (about 60 SQP
         iterations on the second step of the stored DMS_tLBMPC_q100 run, 5 with the exact
         Hessian), hence the larger default max_iter"""
-        return super().solve(xmeasure, data, y0=y0, handle=handle, max_iter=max_iter, tol=tol)
+        return super().solve(xmeasure, data, y0=y0, handle=handle, max_iter=max_iter, tol=tol,
+                             polish=polish)

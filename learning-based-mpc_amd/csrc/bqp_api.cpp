@@ -105,6 +105,11 @@ extern "C" {
 
 const char* bqp_version(void) { return "bqp 0.1.0 (gfx950, structured Riccati Mehrotra IPM)"; }
 
+#ifndef BQP_SRC_SHA1
+#define BQP_SRC_SHA1 "unknown"
+#endif
+const char* bqp_build_source_sha1(void) { return BQP_SRC_SHA1; }
+
 void bqp_default_options(bqp_options* o) {
     if (!o) return;
     o->max_iter = 50;
@@ -547,6 +552,8 @@ int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_s
             HIP_TRY(hipMemcpyAsync(cur, e.src, sizeof(double) * e.n, hipMemcpyHostToDevice, h->stream));
             cur += e.n;
         }
+    // quadprog semantics: the symmetric part of H (a no-op on a symmetric H)
+    HIP_TRY(bqp::launch_dense_symmetrize(in[0].dst, (int)n, s->sH ? batch : 1, s->sH, h->stream));
     double* xd = cur; cur += nxo;
     double* fd = cur; cur += batch;
     double* lid = cur; cur += nli;
@@ -711,9 +718,10 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     // diagnostic (BQP_LB_TRACE=2): per-launch event times of the first SQP iterations
     const char* lbt = getenv("BQP_LB_TRACE");
     const bool lbt2 = lbt && atoi(lbt) >= 2;
+    EventGuard tg[6];                      // released on every return path
     hipEvent_t tev[6] = {};
     if (lbt2)
-        for (auto& e : tev) HIP_TRY(hipEventCreate(&e));
+        for (int k = 0; k < 6; ++k) { HIP_TRY(hipEventCreate(&tg[k].e)); tev[k] = tg[k].e; }
     for (int it = 0; it < o.max_iter; ++it) {
         if (lbt2) HIP_TRY(hipEventRecord(tev[0], st));
         HIP_TRY(bqp::launch_lbmpc_rollout(a, 1, st));
@@ -765,8 +773,6 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
             if (nd_h >= batch) break;
         }
     }
-    if (lbt2)
-        for (auto& e : tev) hipEventDestroy(e);
     HIP_TRY(hipEventRecord(h->ev1, st));
     h->timed = true;
     h->launches = launches;

@@ -749,22 +749,24 @@ __host__ __device__ inline int dense_ts(int n) { return 32 * ((n + 31) / 32) + 1
 __host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 1); }
 // the two-buffer A'DA (global_load_lds of tile t + 1 in flight while the MFMAs run on tile t)
 // when both buffers and the factor fit in LDS; otherwise the single row-major tile
+// (every budget below counts the reduction scratch and the tile bounds, DQ_TAIL doubles at the end)
+#define DQ_TAIL (16 + DQ_THL)
 __host__ __device__ inline bool dense_glds(int n) {
     const int a = TILE * dense_ts(n), b = 2 * dense_gbuf(n);
-    return n <= 128 && (size_t)((a > b ? a : b) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
+    return n <= 128 && (size_t)((a > b ? a : b) + n * n + DQ_TAIL) * sizeof(double) <= DENSE_LDS_MAX;
 }
 __host__ __device__ inline int dense_tiles(int n) {   // doubles of LDS before the factor
     const int a = TILE * dense_ts(n), b = 2 * dense_gbuf(n);
     return dense_glds(n) && b > a ? b : a;
 }
 __host__ __device__ inline bool dense_k_lds(int n) {
-    return (size_t)(dense_tiles(n) + n * n) * sizeof(double) <= DENSE_LDS_MAX;
+    return (size_t)(dense_tiles(n) + n * n + DQ_TAIL) * sizeof(double) <= DENSE_LDS_MAX;
 }
 // + the reduction scratch (16) and the A tile bounds (DQ_THL) at the end: the kernel's only LDS
 // object is the dynamic array (a second __shared__ object made hipcc wait for the in-flight
 // global_load_lds before every LDS read)
 __host__ __device__ inline size_t dense_lds_bytes(int n) {
-    return sizeof(double) * (size_t)(dense_tiles(n) + (dense_k_lds(n) ? n * n : 0) + 16 + DQ_THL);
+    return sizeof(double) * (size_t)(dense_tiles(n) + (dense_k_lds(n) ? n * n : 0) + DQ_TAIL);
 }
 
 template <bool KL>   // KL: the factor lives in LDS (dense_k_lds(n)); a compile-time choice so that
@@ -2006,20 +2008,37 @@ __global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
     }
 }
 
-// dynamic LDS above 64 KB needs the kernel attribute, set once per device and instantiation
-// (a process-wide flag left a handle on a second device without it)
+// dynamic LDS above 64 KB needs the kernel attribute on the current device; set on every launch
+// (a host call of about a microsecond) so that no process-wide state is kept (include/bqp.h: handles
+// on several host threads and devices share nothing)
 template <bool KL>
 static hipError_t dense_lds_attr(size_t lds) {
     if (lds <= 64 * 1024) return hipSuccess;
-    static bool done[64] = {};
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev >= 0 && dev < 64 && done[dev]) return hipSuccess;
-    e = hipFuncSetAttribute((const void*)dense_ipm_kernel<KL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            DENSE_LDS_MAX);
-    if (e == hipSuccess && dev >= 0 && dev < 64) done[dev] = true;
-    return e;
+    return hipFuncSetAttribute((const void*)dense_ipm_kernel<KL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               DENSE_LDS_MAX);
+}
+
+// H <- (H + H')/2 in place for `count` n x n matrices `stride` doubles apart (the host entry's
+// staging copy): MATLAB quadprog solves with the symmetric part of a non-symmetric H, and the
+// kernels read both triangles of H (the factor the lower one, the residual H z whole rows).  A
+// symmetric H is left bit for bit as it was ((h + h) / 2 = h exactly).
+__global__ void dense_symmetrize_kernel(double* H, int n, int64_t stride) {
+    double* Hb = H + (int64_t)blockIdx.y * stride;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)n * n) return;
+    const int i = (int)(e % n), j = (int)(e / n);
+    if (i <= j) return;                 // one thread per pair (i > j)
+    const double v = 0.5 * (Hb[(int64_t)j * n + i] + Hb[(int64_t)i * n + j]);
+    Hb[(int64_t)j * n + i] = v;
+    Hb[(int64_t)i * n + j] = v;
+}
+
+hipError_t launch_dense_symmetrize(double* H, int n, int count, int64_t stride, hipStream_t st) {
+    if (n <= 1 || count <= 0) return hipSuccess;
+    const int64_t nn = (int64_t)n * n;
+    hipLaunchKernelGGL(dense_symmetrize_kernel, dim3((unsigned)((nn + 255) / 256), count), dim3(256), 0, st,
+                       H, n, stride);
+    return hipGetLastError();
 }
 
 hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {

@@ -97,6 +97,7 @@ struct DenseKernelArgs {
 
 int dense_work_doubles(int n, int m, int me);
 hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st);
+hipError_t launch_dense_symmetrize(double* H, int n, int count, int64_t stride, hipStream_t st);
 
 // Learning-based MPC (Gauss-Newton SQP on the NW-learned model), bqp_lbmpc.hip.  Small
 // matrices column-major (A nx*nx, B nx*nu, K nu*nx, LAMBDA nx*np, PSI nu*np); weight factors

@@ -277,9 +277,14 @@ __host__ __device__ constexpr int hand_rows_off(int N, int NS, int NU) {
 // code: the mixed mode pays there (the fp32 launch fits twice the instances per CU); shorter
 // horizons run fp64 alone (bqp_api.cpp), and their kernels keep the register budget of the
 // plain solve.
-template <bool LONG>
+// The repair launch (POL) takes the same start as the launch whose result it repairs: an instance
+// the mixed mode's cold retry launch solved again is marked pol_need = 2 there, and its repair
+// starts cold too (replaying the handed-over start would overwrite the fp64 retry's result with
+// the continuation's).
+template <bool LONG, bool POL>
 __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
-    return BQP_HAND_IN && LONG && a.hand_in && (a.hand_flag[inst] == 1 || a.hand_flag[inst] == 0);
+    return BQP_HAND_IN && LONG && a.hand_in && (a.hand_flag[inst] == 1 || a.hand_flag[inst] == 0) &&
+           !(POL && a.pol_need[inst] == 2);
 }
 
 #ifdef BQP_STAMPS
@@ -1135,7 +1140,7 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     real feasA = 0, gsA = 0;
     real minv, bscale;
     int flag = 0, it0 = 0;
-    if (hand_warm<SPL == 2>(a, inst)) {
+    if (hand_warm<SPL == 2, POL>(a, inst)) {
         // continue the fp32 phase's iterate (mixed precision); x_0 stays the exact fp64 state
         const float* hb = a.hand_in + (int64_t)inst * a.hand_stride;
         constexpr int SW = hand_stage_w(NS, NU);
@@ -2061,7 +2066,7 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 
     // ======================= initial point ==================================================
     constexpr int HR_T = 0, HR_L = BPL * WAVE, HP_T = 2 * BPL * WAVE, HP_L = (2 * BPL + RPL) * WAVE;
-    if (hand_warm<(BPL >= 16)>(a, inst)) {
+    if (hand_warm<(BPL >= 16), POL>(a, inst)) {
         // continue the fp32 phase's iterate (mixed precision): slacks and multipliers as they
         // were, the residuals and multiplier tables formed afresh in fp64
         const float* hb = a.hand_in + (int64_t)inst * a.hand_stride + hand_rows_off(N, NS, NU);
@@ -2241,7 +2246,9 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         // carries no polish state
         if (BQP_POLISH && a.pol_need && lane == 0) {
             const int flag = (int)X[X_FLAG];
-            a.pol_need[inst] = (a.polish > 0 && flag != -2 && (flag != 1 || (a.polish > 1 && dg > DEG_POLISH))) ? 1 : 0;
+            // (2: marked by the mixed mode's cold retry launch - its repair starts cold as well)
+            a.pol_need[inst] = (a.polish > 0 && flag != -2 && (flag != 1 || (a.polish > 1 && dg > DEG_POLISH)))
+                                   ? (a.redo_flag ? 2 : 1) : 0;
         }
     }
     if constexpr (PC) {

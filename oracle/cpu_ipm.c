@@ -86,6 +86,7 @@ typedef struct {
     double cmax;   /* max_i t_i lam_i of the last residuals() */
     double *wx, *wu, *wp;
     double *cgr, *cgp;   /* polish: CG residual and direction over all rows [x | u | poly] */
+    double *rcb;         /* complementarity rhs over all rows [x | u | poly] (per thread, once) */
 } work_t;
 
 static int perm_of(const prob_t* P, int i) {
@@ -848,11 +849,11 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     for (int i = 0; i < nxr; ++i) { W->tx[i] = 1.0; W->lx[i] = 1.0; }
     for (int i = 0; i < nur; ++i) { W->tu[i] = 1.0; W->lu[i] = 1.0; }
     for (int r = 0; r < P->mp; ++r) { W->tp[r] = 1.0; W->lp[r] = 1.0; }
-    double *rcx = (double*)malloc(sizeof(double) * (nxr + nur + P->mp + 1));
+    double *rcx = W->rcb;
     double *rcu = rcx + nxr, *rcp = rcu + nur;
     for (int i = 0; i < nxr + nur + P->mp; ++i) rcx[i] = 1.0;
     residuals(P, W, &stat, &feas, &cs, &mc, &gs);
-    if (factor(P, W)) { free(rcx); return -8; }
+    if (factor(P, W)) return -8;
     prep_iter(P, W);
     solve_kkt(P, W, rcx, rcu, rcp);
     for (int i = 0; i < (N + 1) * ns; ++i) { W->s[i] += W->ds[i]; W->pi[i] += W->dpi[i]; }
@@ -1019,7 +1020,6 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
     }
 #undef PRESENT_X
 #undef PRESENT_U
-    free(rcx);
     *iters = it;
     kkt[0] = stat; kkt[1] = feas; kkt[2] = mu;
     return flag;
@@ -1070,6 +1070,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         W.itu = alloc0(N * nu * 2); W.ilu = alloc0(N * nu * 2); W.itp = alloc0(mp); W.ilp = alloc0(mp);
         W.wx = alloc0((N + 1) * nx * 2); W.wu = alloc0(N * nu * 2); W.wp = alloc0(mp);
         W.cgr = alloc0((N + 1) * nx * 2 + N * nu * 2 + mp); W.cgp = alloc0((N + 1) * nx * 2 + N * nu * 2 + mp);
+        W.rcb = alloc0((N + 1) * nx * 2 + N * nu * 2 + mp + 1);
         prob_t P;
         memset(&P, 0, sizeof(P));
         P.nx = nx; P.nu = nu; P.np = np; P.ns = ns; P.nv = nv; P.N = N; P.mp = mp;
@@ -1142,7 +1143,7 @@ int cpu_ocp_solve(const bqp_ocp_dims* d, int batch, const bqp_ocp_data* D, int m
         free(W.dtp); free(W.dlp); free(W.Ptab); free(W.Phit); free(W.Ktab); free(W.Rinv); free(W.p);
         free(W.qs); free(W.qu); free(W.wv); free(W.cw); free(W.qt); free(W.qh); free(W.kff); free(W.f); free(W.Dx);
         free(W.Du); free(W.FD); free(W.itx); free(W.ilx); free(W.itu); free(W.ilu); free(W.itp);
-        free(W.ilp); free(W.wx); free(W.wu); free(W.wp); free(W.cgr); free(W.cgp);
+        free(W.ilp); free(W.wx); free(W.wu); free(W.wp); free(W.cgr); free(W.cgp); free(W.rcb);
     }
     return err;
 }

@@ -17,15 +17,20 @@ def _loop(mg, x0, steps, **kw):
 
 
 def test_cpu_loop_vs_stored_q100(mg):
+    """the whole stored run (499 steps, DMS_LBMPC_casadi.m:81; ~20 s on one core): slow states
+    7.4e-8, all states 1.1e-4 in the transient, 3.6e-7 from step 200 on (round 5; the same loop
+    over every stored learned run: tests/test_gpu_lbmpc_dms.py)"""
     st = golden('dms_lbmpc_loops.npz')['DMS_tLBMPC_q100']
-    T = 25
-    X, U, its, flags = _loop(mg, X_INIT[None], T)
+    T = len(st) - 1
+    X, U, its, flags = _loop(mg, X_INIT[None], T, threads=1)
     assert (flags == 1).all()
     e = np.abs(X[0] - st[:T + 1])
-    print('C loop vs DMS_tLBMPC_q100: slow %.2e, all %.2e, SQP iterations %s'
-          % (e[:, :2].max(), e.max(), its[0].tolist()))
-    assert e[:, :2].max() < 1e-7
-    assert e.max() < 1e-4
+    print('C loop vs DMS_tLBMPC_q100 over %d steps: slow %.2e, all %.2e, k >= 200 %.2e; SQP '
+          'iterations mean %.2f max %d' % (T, e[:, :2].max(), e.max(), e[200:].max(), its.mean(),
+                                           its.max()))
+    assert e[:, :2].max() < 1e-6
+    assert e.max() < 5e-4
+    assert e[200:].max() < 1e-5
 
 
 def test_cpu_loop_vs_numpy_oracle(mg):

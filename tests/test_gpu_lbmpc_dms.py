@@ -31,17 +31,24 @@ X_INIT = np.array([0.15, 1.2875, 1.1547, 0.0])
 
 def test_dms_lbmpc_loop_vs_stored_q100(mg):
     """DMS_LBMPC_casadi.m as written (q = 100, 8 x q window): the GPU loop regenerates the stored
-    plant trajectory DMS_tLBMPC_q100.mat - the learned correction moves x4 at step 2 by 1.1 away
-    from the nominal (LMPC) loop, and the loop follows the stored run (measured: slow states
-    1.0e-8, all states 1.1e-5 over 25 steps, profiles/r03_learned/)"""
+    plant trajectory DMS_tLBMPC_q100.mat over its whole length (499 steps,
+    DMS_LBMPC_casadi.m:81 mpciterations = 500) - the learned correction moves x4 at step 2 by 1.1
+    away from the nominal (LMPC) loop.  The C restatement's loop (oracle/cpu_lbmpc.c) gives slow
+    states 7.4e-8, all states 1.1e-4 in the transient (x4 = 1000 delta u amplifies the IPOPT
+    tolerance of the stored moves), 3.6e-7 from step 200 on; the GPU loop is held to the same
+    bars."""
     import bqp
     st = golden('dms_lbmpc_loops.npz')['DMS_tLBMPC_q100']
-    T = 25
+    T = len(st) - 1
     r = bqp.closed_loop_sqp(_mpc(mg), X_INIT, T, learning=dict(q=100, mask=1))
     assert (r.exitflag == 1).all(), r.exitflag
     e = np.abs(r.X[0] - st[:T + 1])
-    assert e[:, :2].max() < 1e-7, e[:, :2].max()
-    assert e.max() < 3e-5, e.max(axis=1)
+    print('DMS_tLBMPC_q100 over %d steps: slow %.2e, all %.2e, k >= 200 %.2e; SQP iterations mean '
+          '%.2f max %d' % (T, e[:, :2].max(), e.max(), e[200:].max(), r.iterations.mean(),
+                           r.iterations.max()))
+    assert e[:, :2].max() < 1e-6, e[:, :2].max()
+    assert e.max() < 5e-4, e.max(axis=1)
+    assert e[200:].max() < 1e-5
     assert abs(r.X[0, 2, 3] - 3.0406) > 1.0
     # the logged learned one-step predictions: x_eq + A dx + B du + g with the window before the
     # update (DMS_LBMPC_casadi.m:199)
@@ -86,15 +93,20 @@ STORED = [('DMS_tLBMPC_q10', 100, 10, 1), ('DMS_tLBMPC_q50', 100, 50, 1),
 @pytest.mark.parametrize('name,N,q,mask', STORED)
 def test_stored_learned_loops(mg, name, N, q, mask):
     """DMS_LBMPC_casadi.m with the horizon and window of each stored run (mask 0: a 7-row window
-    whose zero points count, the variant that made DMS_tLBMPC.mat and the q = 500 run): 15 steps
-    (past the q = 10 window's wrap) against the stored plant trajectory"""
+    whose zero points count, the variant that made DMS_tLBMPC.mat and the q = 500 run) over the
+    stored run's whole length (499 steps).  The C restatement's loop over the
+    same runs (round 5): slow states <= 3.2e-7, all states <= 1.9e-4 (transient), <= 1.6e-6 from
+    step 200 on"""
     import bqp
     st = golden('dms_lbmpc_loops.npz')[name]
-    T = 15
+    T = len(st) - 1
     r = bqp.closed_loop_sqp(_mpc(mg, N=N), X_INIT, T, learning=dict(q=q, mask=mask))
     assert (r.exitflag == 1).all(), r.exitflag
     e = np.abs(r.X[0] - st[:T + 1])
-    assert e[:, :2].max() < 1e-7 and e.max() < 5e-5, e.max(axis=1)
+    print('%s over %d steps: slow %.2e, all %.2e, k >= 200 %.2e; SQP iterations mean %.2f max %d'
+          % (name, T, e[:, :2].max(), e.max(), e[200:].max(), r.iterations.mean(), r.iterations.max()))
+    assert e[:, :2].max() < 1e-6 and e.max() < 5e-4, e.max(axis=1)
+    assert e[200:].max() < 1e-5
 
 
 def test_dms_lbmpc_loop_vs_c_restatement(mg):

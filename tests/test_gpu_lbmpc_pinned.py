@@ -92,3 +92,16 @@ def test_f3_fmincon_loop_end_to_end(mg):
              r.iterations.mean(), r.iterations.max()))
     assert ep < 1e-13
     assert e[:, :2].max() < 5e-3
+
+
+@pytest.mark.parametrize('polish', [0, 2, 3])
+def test_f3_polish_modes_single_solve(mg, handle, polish):
+    """the sub-problem polish of bqp_lbmpc_solve_batched per bqp_options.polish - 0 (the
+    C default) and 2 polish 0 / -8 sub-problem exits before the SQP stalls (LB_POLISH_STALL = 6
+    iterations) and every sub-problem after it, 3 polishes only after the stall - all reach the
+    pinned optimum of the 32 late F3 solves (same bars as test_f3_late_solves_batched)"""
+    f = golden('lbmpc_N40.npz')
+    lb = _lbmpc(mg, 40)
+    r = lb.solve(f['late_dx'], f['late_windows'], handle=handle, max_iter=100, polish=polish)
+    _check(r, f['late_dx'], f['late_du_matlab'], f['late_z_oracle'], f['late_err_vs_matlab'],
+           mg['K'])

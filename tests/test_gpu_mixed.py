@@ -129,3 +129,21 @@ def test_mixed_status_cold_restart(mg, term_set, handle):
         assert err[k28].max() / sc < 1e-8, err[k28].max()
     ok = r64.exitflag == 1
     assert np.abs(rmx.du0[ok] - r64.du0[ok]).max() < 1e-8
+
+
+def test_mixed_repair_of_cold_retry(mg, term_set, handle):
+    """an instance the mixed mode's cold retry launch (phase 3) solved again from the
+    fp64 start and that then needs the repair launch is repaired from that same cold start.  With
+    max_iter = 2 no continuation converges, so every instance is retried cold, ends 0 and is
+    marked for the repair: the mixed result must then be the fp64 solve's, bit for bit (phase 3 +
+    repair = the fp64 solve + repair).  Replaying the handed-over start in the repair gave the
+    continuation's iterate instead."""
+    g = golden('dms_DSS_tLMPC.npz')
+    tl = _tracking(mg, term_set, 100)
+    X = g['x'][g['idx'][:64]]
+    r64 = tl.solve(X, handle=handle, max_iter=2)
+    rmx = tl.solve(X, handle=handle, precision=2, max_iter=2)
+    assert (r64.exitflag == 0).all(), np.unique(r64.exitflag)
+    assert np.array_equal(rmx.exitflag, r64.exitflag)
+    assert np.array_equal(rmx.u, r64.u) and np.array_equal(rmx.x, r64.x)
+    assert np.array_equal(rmx.theta, r64.theta)

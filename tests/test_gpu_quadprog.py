@@ -94,3 +94,49 @@ def test_condensed_c2_batch_on_matrix_cores(mg, term_set, handle):
     for i in range(len(X0)):
         r = cd.H @ x[i] + f[i] + cd.A.T @ lam['ineqlin'][i]
         assert np.abs(r).max() < 1e-6 * (1 + np.abs(f[i]).max())
+
+
+@pytest.mark.parametrize('n', [101, 108, 109, 122, 123, 130])
+def test_dense_lds_layout_sizes(n, handle):
+    """the workgroup kernel's LDS layouts around their budget edges: n <= 108 two
+    global_load_lds A'DA buffers + the factor in LDS, 109 .. 122 one row tile + the factor in
+    LDS, >= 123 the factor in the global workspace - each size must solve (not fail the launch)
+    to the exact optimum (LDP/NNLS + active-set KKT solve, oracle/exact_qp.py)"""
+    import bqp
+    from oracle import exact_qp
+    rng = np.random.default_rng(100 + n)
+    m, B = 160, 4
+    M = rng.standard_normal((n, n))
+    H = M @ M.T / n + np.eye(n)
+    A = rng.standard_normal((m, n))
+    f = rng.standard_normal((B, n))
+    b = rng.uniform(0.2, 1.0, (B, m))
+    x, fval, flag, out, lam = bqp.quadprog(H, f, A, b, handle=handle)
+    assert (flag == 1).all(), flag
+    for i in range(B):
+        z = exact_qp.solve(H, f[i], A, b[i])["z"]
+        assert np.abs(x[i] - z).max() / max(1, np.abs(z).max()) < 1e-8
+
+
+def test_nonsymmetric_h_uses_symmetric_part(handle):
+    """MATLAB quadprog solves with (H + H')/2 when H is not symmetric; the host entry
+    symmetrises its staging copy, so the result equals the solve with the symmetric part (to the
+    same bits: the symmetrised copy is what the kernel reads) and the exact optimum of that QP"""
+    import bqp
+    from oracle import exact_qp
+    rng = np.random.default_rng(71)
+    for n, m in ((12, 30), (40, 120)):
+        M = rng.standard_normal((n, n))
+        Hs = M @ M.T / n + np.eye(n)
+        S = rng.standard_normal((n, n))
+        Hn = Hs + 0.3 * (S - S.T)                  # same symmetric part
+        f = rng.standard_normal((3, n))
+        A = rng.standard_normal((m, n))
+        b = rng.uniform(0.2, 1.0, (3, m))
+        xn, fn, flag_n, _, _ = bqp.quadprog(Hn, f, A, b, handle=handle)
+        xs, fs, flag_s, _, _ = bqp.quadprog(0.5 * (Hn + Hn.T), f, A, b, handle=handle)
+        assert (flag_n == 1).all() and (flag_s == 1).all()
+        assert np.array_equal(xn, xs)
+        for i in range(3):
+            z = exact_qp.solve(Hs, f[i], A, b[i])['z']
+            assert np.abs(xn[i] - z).max() / max(1, np.abs(z).max()) < 1e-8

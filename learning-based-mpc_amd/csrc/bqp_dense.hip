@@ -397,6 +397,136 @@ __device__ __forceinline__ bool chol_2b(double* K, int n, double fl, double* jun
     return true;
 }
 
+// ------------------------------------------------------------------------------------------
+// Blocked Cholesky on register tiles (round 5, n <= 128).  The lower block triangle of K in 16 x
+// 16 tiles is held by the four waves exactly as the MFMA A'DA leaves it: tile t = I (I+1)/2 + J
+// (J <= I) on wave t % 4 as acc[t / 4], lane l = 16 k4 + c16, register e holding K(16 I + k4 + 4 e,
+// 16 J + c16); a diagonal tile holds the whole symmetric block, padding rows / columns (>= n) the
+// identity.  Per block column J: the owner of tile (J, J) factors it in registers (D), the owners
+// of the tiles (I, J) below solve them against it (P), and every tile right of column J takes the
+// update K_IK -= L_IJ L_KJ' as four v_mfma_f64_16x16x4 (U) with operands read from the factor in
+// LDS: two workgroup barriers per block column (chol_2b: one per two pivots, 51 at n = 101).  Per
+// entry the in-block updates run in pivot order as chol_2b's; the updates of earlier block columns
+// are summed by the matrix cores.  The factor leaves K as chol_2b does: L lower, L' upper, l_jj on
+// the diagonal.
+
+// pivot P of a diagonal tile T (one wave): l_PP = sqrt(K_PP) (pivot floor fl >= 0; fl < 0: fail on a
+// non-positive pivot), column P scaled by 1 / l_PP - broadcast along each 16-lane row (row
+// newbcast: every lane gets L(r, P) of its rows) and, for the lane's own column c16, L(c16, P) =
+// K(P, c16) / l_PP from row P (symmetric storage) by a lane permute - then the rank-1 update of the
+// trailing block; row P of the tile becomes L' (upper), column P L (lower).
+template <int P>
+__device__ __forceinline__ void dtile_piv(dbl4& T, int k4, int c16, double fl, bool& ok, double* rv, int lane) {
+    constexpr int EP = P >> 2, SRC = 16 * (P & 3) + P;
+    double d = rl(T[EP], SRC);
+    if (fl >= 0.0 && !(d > fl)) d = fl;
+    if (!(d > 0.0)) ok = false;          // wave-uniform
+    const double ljj = sqrt(d), inv = 1.0 / ljj;
+    const double xc = __shfl(T[EP], 16 * (P & 3) + c16) * inv;
+    double xr[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) xr[e] = rbc<P>(T[e]) * inv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int r = k4 + 4 * e;
+        if (r > P) T[e] = (c16 > P) ? T[e] - xr[e] * xc : (c16 == P ? xr[e] : T[e]);
+        else if (r == P) T[e] = (c16 > P) ? xc : (c16 == P ? ljj : T[e]);
+    }
+    if (lane == 0) rv[P] = inv;
+    if constexpr (P + 1 < 16) dtile_piv<P + 1>(T, k4, c16, fl, ok, rv, lane);
+}
+
+// column P of a panel tile (I, J): L(r, P) = K(r, P) / l_PP reaches the lane's 16-lane row, the
+// later columns c16 > P take - L(r, P) L(c16, P); lc = the lane's row of the diagonal factor in LDS
+// (L(16 J + c16, 16 J + q) at lc[q n]), rv the reciprocal pivots (both read at the use: held in
+// registers across the unrolled tiles they spilled)
+template <int P>
+__device__ __forceinline__ void ptile_piv(dbl4& T, int c16, const double* lc, int n, const double* rv) {
+    const double ri = rv[P], lv = lc[(int64_t)P * n];
+    double x[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = rbc<P>(T[e]) * ri;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) T[e] = (c16 > P) ? T[e] - x[e] * lv : (c16 == P ? x[e] : T[e]);
+    if constexpr (P + 1 < 16) ptile_piv<P + 1>(T, c16, lc, n, rv);
+}
+
+// tile index t -> (I, J), J <= I, row-major over the lower block triangle
+__device__ __forceinline__ void tile_ij(int t, int& I, int& J) {
+    int i = 0;
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    I = i;
+    J = t - i * (i + 1) / 2;
+}
+
+template <int TPW>
+__device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW], const int (&tJ)[TPW],
+                                          double* K, int n, double fl, double* rv) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int c16 = lane & 15, k4 = lane >> 4;
+    const int nbk = (n + 15) >> 4, ntl = nbk * (nbk + 1) / 2;
+    for (int J = 0; J < nbk; ++J) {
+        // ---- D: the diagonal tile, by its owner ----
+        const int tD = J * (J + 1) / 2 + J;
+        if ((tD & 3) == wv) {
+            const int uD = tD >> 2;
+            dbl4 T = acc[0];
+#pragma unroll
+            for (int u = 1; u < TPW; ++u) if (u == uD) T = acc[u];
+            bool ok = true;
+            dtile_piv<0>(T, k4, c16, fl, ok, rv, lane);
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) if (u == uD) acc[u] = T;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = 16 * J + k4 + 4 * e, j = 16 * J + c16;
+                if (i < n && j < n) K[(int64_t)j * n + i] = T[e];
+            }
+            if (lane == 0) rv[16] = ok ? 0.0 : 1.0;
+        }
+        __syncthreads();
+        if (rv[16] != 0.0) { __syncthreads(); return false; }   // uniform
+        if (J + 1 == nbk) break;
+        // ---- P: the tiles (I, J), I > J, against L_JJ ----
+        {
+            // L(16 J + c16, 16 J + q) at lc[q n] (used for q < c16: the lower triangle)
+            const double* lc = K + (int64_t)(16 * J) * n + min(16 * J + c16, n - 1);
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                if (wv + 4 * u >= ntl || tJ[u] != J || tI[u] == J) continue;   // wave-uniform
+                ptile_piv<0>(acc[u], c16, lc, n, rv);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int i = 16 * tI[u] + k4 + 4 * e, j = 16 * J + c16;
+                    if (i < n) {
+                        K[(int64_t)j * n + i] = acc[u][e];          // L (lower)
+                        K[(int64_t)i * n + j] = acc[u][e];          // L' (upper)
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- U: every tile (I, K), K > J: K_IK -= L_IJ L_KJ' on the matrix cores ----
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            if (wv + 4 * u >= ntl || tJ[u] <= J) continue;
+            const int rA = 16 * tI[u] + c16, rB = 16 * tJ[u] + c16;
+            double av[4], bv[4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int64_t col = (int64_t)(16 * J + 4 * s4 + k4) * n;
+                av[s4] = rA < n ? -K[col + rA] : 0.0;
+                bv[s4] = rB < n ? K[col + rB] : 0.0;
+            }
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+                acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc[u], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
 // solve L L' x = b in place (x in LDS vector xs of length n), thread-parallel dot products
 template <int NTH = DT, class R = Red>
 __device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
@@ -750,7 +880,7 @@ __host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 1); }
 // the two-buffer A'DA (global_load_lds of tile t + 1 in flight while the MFMAs run on tile t)
 // when both buffers and the factor fit in LDS; otherwise the single row-major tile
 // (every budget below counts the reduction scratch and the tile bounds, DQ_TAIL doubles at the end)
-#define DQ_TAIL (16 + DQ_THL)
+#define DQ_TAIL (48 + DQ_THL)
 __host__ __device__ inline bool dense_glds(int n) {
     const int a = TILE * dense_ts(n), b = 2 * dense_gbuf(n);
     return n <= 128 && (size_t)((a > b ? a : b) + n * n + DQ_TAIL) * sizeof(double) <= DENSE_LDS_MAX;
@@ -762,7 +892,8 @@ __host__ __device__ inline int dense_tiles(int n) {   // doubles of LDS before t
 __host__ __device__ inline bool dense_k_lds(int n) {
     return (size_t)(dense_tiles(n) + n * n + DQ_TAIL) * sizeof(double) <= DENSE_LDS_MAX;
 }
-// + the reduction scratch (16) and the A tile bounds (DQ_THL) at the end: the kernel's only LDS
+// + the reduction scratch (16), the tile Cholesky's reciprocal pivots and fail flag (32) and the
+// A tile bounds (DQ_THL) at the end: the kernel's only LDS
 // object is the dynamic array (a second __shared__ object made hipcc wait for the in-flight
 // global_load_lds before every LDS read)
 __host__ __device__ inline size_t dense_lds_bytes(int n) {
@@ -778,7 +909,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
     extern __shared__ __attribute__((aligned(16))) double dlds[];
     double* sc = dlds + dense_tiles(n) + (KL ? n * n : 0);
-    double* thl = sc + 16;           // tile bounds of A (below)
+    double* rvp = sc + 16;           // tile Cholesky: reciprocal pivots, fail flag (tile_chol)
+    double* thl = sc + 48;           // tile bounds of A (below)
     const int ts = dense_ts(n), tw = ts - 1;
     double* tileA = dlds;
     Red red{sc};
@@ -1023,7 +1155,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     };
 
     // ---------------------------------------------------------------- factorisation
-    auto factor = [&]() -> bool {
+    auto factor = [&]() __attribute__((always_inline)) -> bool {   // inlined: a call spilled (callee budget)
         // K = H + sum_r A_r' D_r A_r (+ bound diagonal): lower triangle (n <= 128) or both
         const int ne = n * (n + 1) / 2;
         double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
@@ -1043,14 +1175,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             const int nbk = (n + 15) >> 4, ntl = nbk * (nbk + 1) / 2;
             int tI[TPW], tJ[TPW];
 #pragma unroll
-            for (int u = 0; u < TPW; ++u) {
-                // tile index t -> (I, J), J <= I, row-major over the lower block triangle
-                const int t = wv + 4 * u;
-                int I = 0;
-                while ((I + 1) * (I + 2) / 2 <= t) ++I;
-                tI[u] = I;
-                tJ[u] = t - I * (I + 1) / 2;
-            }
+            for (int u = 0; u < TPW; ++u) tile_ij(wv + 4 * u, tI[u], tJ[u]);
             dbl4 acc[TPW];
 #pragma unroll
             for (int u = 0; u < TPW; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -1174,25 +1299,37 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     }
                 }
             }
-            // tile (I, J), lane l, register e: K(16 I + l/16 + 4 e, 16 J + l%16)
+            // tile (I, J), lane l, register e: K(16 I + l/16 + 4 e, 16 J + l%16) = H + A'DA + the
+            // bound diagonal.  Factor in LDS (KL): the blocked Cholesky on the tiles (tile_chol;
+            // diagonal tiles whole, padding the identity).  Factor in global memory (n > 122):
+            // the lower triangle to K and chol_2b there (tile_chol on global K spilled).
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
                 if (wv + 4 * u >= ntl) continue;
 #pragma unroll
                 for (int e2 = 0; e2 < 4; ++e2) {
                     const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
-                    if (i < n && j < n && i >= j) {      // lower triangle (col-major K[j n + i])
-                        double v = H[(int64_t)j * n + i] + acc[u][e2];
+                    double v = (i == j) ? 1.0 : 0.0;
+                    if (i < n && j < n) {
+                        v = H[(int64_t)j * n + i] + acc[u][e2];
                         if (i == j) {
                             if (up_present(j)) v += lB[j] / tB[j];
                             if (lo_present(j)) v += lB[n + j] / tB[n + j];
                             dmx = fmax(dmx, fabs(v));
                         }
-                        K[(int64_t)j * n + i] = v;
+                        if (!KL && i >= j) K[(int64_t)j * n + i] = v;
                     }
+                    acc[u][e2] = v;
                 }
             }
-            __syncthreads();
+            const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
+            DST(1);
+            if constexpr (KL) {
+                if (!tile_chol(acc, tI, tJ, K, n, kfl, rvp)) return false;
+            } else {
+                if (!chol_2b(K, n, kfl, tileA)) return false;
+            }
+            DST(2);
         }
         for (int base = 0; base < (n <= 128 ? 0 : ne); base += DT * 8) {
             double acc[8];
@@ -1241,10 +1378,12 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 K[(int64_t)jj[q2] * n + ii[q2]] = v;
             }
         }
-        const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
-        DST(1);
-        if (!(n <= 128 ? chol_2b(K, n, kfl, tileA) : block_cholesky(K, n, sc, kfl))) return false;
-        DST(2);
+        if (n > 128) {
+            const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
+            DST(1);
+            if (!block_cholesky(K, n, sc, kfl)) return false;
+            DST(2);
+        }
         // Y = K^{-1} Aeq' (one thread per equality row), S = Aeq Y
         for (int r = tid; r < me; r += DT) {
             double* yc = Y + (int64_t)r * n;
@@ -1374,12 +1513,33 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         double hd = 0.0;
         for (int j = tid; j < n; j += DT) hd = fmax(hd, fabs(H[(int64_t)j * n + j]));
         const double sh = DQ_CONVEX_EPS * fmax(1.0, red.max(hd));
-        for (int e2 = tid; e2 < n * n; e2 += DT) {
-            const int i = e2 % n, j = e2 / n;
-            K[e2] = H[e2] + (i == j ? sh : 0.0);
+        if (KL && n <= 128) {
+            // the same blocked factor on tiles of H + sh I (tile_chol, no pivot floor)
+            constexpr int TPW = 9;
+            const int lane = tid & 63, wv = tid >> 6, c16 = lane & 15, k4 = lane >> 4;
+            const int ntl = ((n + 15) >> 4) * (((n + 15) >> 4) + 1) / 2;
+            int tI[TPW], tJ[TPW];
+            dbl4 acc[TPW];
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                tile_ij(wv + 4 * u, tI[u], tJ[u]);
+#pragma unroll
+                for (int e2 = 0; e2 < 4; ++e2) {
+                    const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
+                    double v = (i == j) ? 1.0 : 0.0;
+                    if (wv + 4 * u < ntl && i < n && j < n) v = H[(int64_t)j * n + i] + (i == j ? sh : 0.0);
+                    acc[u][e2] = v;
+                }
+            }
+            if (!tile_chol(acc, tI, tJ, K, n, -1.0, rvp)) flag = -6;
+        } else {
+            for (int e2 = tid; e2 < n * n; e2 += DT) {
+                const int i = e2 % n, j = e2 / n;
+                K[e2] = H[e2] + (i == j ? sh : 0.0);
+            }
+            __syncthreads();
+            if (!(n <= 128 ? chol_2b(K, n, -1.0, tileA) : block_cholesky(K, n, sc, -1.0))) flag = -6;
         }
-        __syncthreads();
-        if (!(n <= 128 ? chol_2b(K, n, -1.0, tileA) : block_cholesky(K, n, sc, -1.0))) flag = -6;
     }
     double stat = 0.0, feq = 0.0, fin = 0.0, csum = 0.0, gscale = 0.0, zmax = 0.0, cmax = 0.0;
     residuals(stat, feq, fin, csum, gscale, zmax, cmax);

@@ -2676,10 +2676,15 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
         }
         wave_sync();
     }
+#if defined(BQP_EXP_ONLY)   // register-budget diagnostic: one wave's code alone (never run)
+    if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+    else row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+#else
     if (!rowwave)
         stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
     else
         row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+#endif
 }
 
 // the solve kernel (no polish code: the main loop keeps its register budget) and the repair

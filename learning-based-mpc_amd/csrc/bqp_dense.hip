@@ -413,7 +413,7 @@ __device__ __forceinline__ bool chol_2b(double* K, int n, double fl, double* jun
 // pivot P of a diagonal tile T (one wave): l_PP = sqrt(K_PP) (pivot floor fl >= 0; fl < 0: fail on a
 // non-positive pivot), column P scaled by 1 / l_PP - broadcast along each 16-lane row (row
 // newbcast: every lane gets L(r, P) of its rows) and, for the lane's own column c16, L(c16, P) =
-// K(P, c16) / l_PP from row P (symmetric storage) by a lane permute - then the rank-1 update of the
+// K(P, c16) / l_PP from row P (symmetric storage) by row swaps (xrow_bcast) - then the rank-1 update of the
 // trailing block; row P of the tile becomes L' (upper), column P L (lower).
 template <int P>
 __device__ __forceinline__ void dtile_piv(dbl4& T, int k4, int c16, double fl, bool& ok, double* rv, int lane) {
@@ -421,16 +421,24 @@ __device__ __forceinline__ void dtile_piv(dbl4& T, int k4, int c16, double fl, b
     double d = rl(T[EP], SRC);
     if (fl >= 0.0 && !(d > fl)) d = fl;
     if (!(d > 0.0)) ok = false;          // wave-uniform
-    const double ljj = sqrt(d), inv = 1.0 / ljj;
-    const double xc = __shfl(T[EP], 16 * (P & 3) + c16) * inv;
+    // 1 / l_PP: the hardware reciprocal square root and two Newton steps (the pivot chain's
+    // latency: sqrt then a division were ~25 dependent instructions), l_PP = d / sqrt(d)
+    double inv = __builtin_amdgcn_rsq(d);
+    inv = inv * fma(-0.5 * d * inv, inv, 1.5);
+    inv = inv * fma(-0.5 * d * inv, inv, 1.5);
+    const double ljj = d * inv;
+    const double xc = xrow_bcast<P & 3>(T[EP]) * inv;
     double xr[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) xr[e] = rbc<P>(T[e]) * inv;
+    // branch-free (as selects the per-lane cases were exec-mask branches)
+    const bool cg = c16 > P, ce = c16 == P;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int r = k4 + 4 * e;
-        if (r > P) T[e] = (c16 > P) ? T[e] - xr[e] * xc : (c16 == P ? xr[e] : T[e]);
-        else if (r == P) T[e] = (c16 > P) ? xc : (c16 == P ? ljj : T[e]);
+        const double below = cg ? fma(-xr[e], xc, T[e]) : (ce ? xr[e] : T[e]);
+        const double onrow = cg ? xc : (ce ? ljj : T[e]);
+        T[e] = r > P ? below : (r == P ? onrow : T[e]);
     }
     if (lane == 0) rv[P] = inv;
     if constexpr (P + 1 < 16) dtile_piv<P + 1>(T, k4, c16, fl, ok, rv, lane);
@@ -446,45 +454,89 @@ __device__ __forceinline__ void ptile_piv(dbl4& T, int c16, const double* lc, in
     double x[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[e] = rbc<P>(T[e]) * ri;
+    const bool cg = c16 > P, ce = c16 == P;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) T[e] = (c16 > P) ? T[e] - x[e] * lv : (c16 == P ? x[e] : T[e]);
+    for (int e = 0; e < 4; ++e) T[e] = cg ? fma(-x[e], lv, T[e]) : (ce ? x[e] : T[e]);
     if constexpr (P + 1 < 16) ptile_piv<P + 1>(T, c16, lc, n, rv);
 }
 
-// tile index t -> (I, J), J <= I, row-major over the lower block triangle
-__device__ __forceinline__ void tile_ij(int t, int& I, int& J) {
-    int i = 0;
-    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+// the tiles of wave w: slots 0 and 1 the diagonal tiles (J, J) with J = w, w + 4 (the Cholesky's
+// diagonal factor then works on a fixed register tile: a runtime slot index put the tiles in
+// scratch memory), slots 2 .. 8 the off-diagonal tiles o = 4 (u - 2) + w in row-major order over
+// the strictly lower block triangle; I = -1: no tile.  nbk <= 8 (n <= 128): at most 2 + 7 slots.
+__device__ __forceinline__ void tile_of(int w, int u, int nbk, int& I, int& J) {
+    I = -1; J = 0;
+    if (u < 2) {
+        const int d = w + 4 * u;
+        if (d < nbk) { I = d; J = d; }
+        return;
+    }
+    const int o = 4 * (u - 2) + w;
+    if (o >= nbk * (nbk - 1) / 2) return;
+    int i = 1;
+    while ((i + 1) * i / 2 <= o) ++i;
     I = i;
-    J = t - i * (i + 1) / 2;
+    J = o - i * (i - 1) / 2;
+}
+
+#ifdef BQP_DSTAMPS
+#define TST_ARGS , unsigned long long* dacc, unsigned long long& dlast
+#define TST_PASS , dst_acc, dst_last
+#define TST(id)                                                            \
+    do {                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                     \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();        \
+        dacc[id] += _t - dlast;                                            \
+        dlast = _t;                                                        \
+    } while (0)
+#else
+#define TST_ARGS
+#define TST_PASS
+#define TST(id) do { } while (0)
+#endif
+// the diagonal tile J in registers: symmetric from its lower triangle (the MFMA A'DA forms K(i, j)
+// and K(j, i) with different rounding; chol_2b read the lower triangle only - with both, the
+// factor of the extreme late-iteration matrices left fp64 range), the 16 pivots, the tile to LDS
+__device__ __forceinline__ bool dtile(dbl4& T, int J, double* K, int n, double fl, double* rv, int lane,
+                                      int k4, int c16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int r = k4 + 4 * e, i = 16 * J + r, j = 16 * J + c16;
+        if (r >= c16 && i < n) K[(int64_t)j * n + i] = T[e];
+    }
+    wave_sync();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int r = k4 + 4 * e;
+        if (r < c16 && 16 * J + c16 < n) T[e] = K[(int64_t)(16 * J + r) * n + 16 * J + c16];
+    }
+    bool ok = true;
+    dtile_piv<0>(T, k4, c16, fl, ok, rv, lane);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int i = 16 * J + k4 + 4 * e, j = 16 * J + c16;
+        if (i < n && j < n) K[(int64_t)j * n + i] = T[e];
+    }
+    return ok;
 }
 
 template <int TPW>
 __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW], const int (&tJ)[TPW],
-                                          double* K, int n, double fl, double* rv) {
+                                          double* K, int n, double fl, double* rv TST_ARGS) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int c16 = lane & 15, k4 = lane >> 4;
-    const int nbk = (n + 15) >> 4, ntl = nbk * (nbk + 1) / 2;
+    const int nbk = (n + 15) >> 4;
     for (int J = 0; J < nbk; ++J) {
-        // ---- D: the diagonal tile, by its owner ----
-        const int tD = J * (J + 1) / 2 + J;
-        if ((tD & 3) == wv) {
-            const int uD = tD >> 2;
-            dbl4 T = acc[0];
-#pragma unroll
-            for (int u = 1; u < TPW; ++u) if (u == uD) T = acc[u];
+        // ---- D: the diagonal tile, by its owner (wave J % 4, slot J / 4) ----
+        if ((J & 3) == wv) {
             bool ok = true;
-            dtile_piv<0>(T, k4, c16, fl, ok, rv, lane);
-#pragma unroll
-            for (int u = 0; u < TPW; ++u) if (u == uD) acc[u] = T;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int i = 16 * J + k4 + 4 * e, j = 16 * J + c16;
-                if (i < n && j < n) K[(int64_t)j * n + i] = T[e];
-            }
+            if (J < 4) ok = dtile(acc[0], J, K, n, fl, rv, lane, k4, c16);
+            else       ok = dtile(acc[1], J, K, n, fl, rv, lane, k4, c16);
             if (lane == 0) rv[16] = ok ? 0.0 : 1.0;
         }
+        TST(12);
         __syncthreads();
+        TST(13);
         if (rv[16] != 0.0) { __syncthreads(); return false; }   // uniform
         if (J + 1 == nbk) break;
         // ---- P: the tiles (I, J), I > J, against L_JJ ----
@@ -493,7 +545,7 @@ __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW]
             const double* lc = K + (int64_t)(16 * J) * n + min(16 * J + c16, n - 1);
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
-                if (wv + 4 * u >= ntl || tJ[u] != J || tI[u] == J) continue;   // wave-uniform
+                if (tI[u] < 0 || tJ[u] != J || tI[u] == J) continue;   // wave-uniform
                 ptile_piv<0>(acc[u], c16, lc, n, rv);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -505,11 +557,13 @@ __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW]
                 }
             }
         }
+        TST(14);
         __syncthreads();
+        TST(15);
         // ---- U: every tile (I, K), K > J: K_IK -= L_IJ L_KJ' on the matrix cores ----
 #pragma unroll
         for (int u = 0; u < TPW; ++u) {
-            if (wv + 4 * u >= ntl || tJ[u] <= J) continue;
+            if (tI[u] < 0 || tJ[u] <= J) continue;
             const int rA = 16 * tI[u] + c16, rB = 16 * tJ[u] + c16;
             double av[4], bv[4];
 #pragma unroll
@@ -522,6 +576,7 @@ __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW]
             for (int s4 = 0; s4 < 4; ++s4)
                 acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc[u], 0, 0, 0);
         }
+        TST(16);
     }
     __syncthreads();
     return true;
@@ -853,8 +908,8 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
 // diagnostic build only (tools/gpu_r03_dstamps.sh): s_memtime cycles per phase of instance 0,
 // printed by thread 0 at exit; never linked into the product library
 #define DST_DECL                                                           \
-    unsigned long long dst_last = __builtin_amdgcn_s_memtime(), dst_acc[12]; \
-    _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_) dst_acc[i_] = 0
+    unsigned long long dst_last = __builtin_amdgcn_s_memtime(), dst_acc[17]; \
+    _Pragma("unroll") for (int i_ = 0; i_ < 17; ++i_) dst_acc[i_] = 0
 #define DST(id)                                                            \
     do {                                                                   \
         __builtin_amdgcn_s_waitcnt(0);                                     \
@@ -1161,7 +1216,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
         if (n <= 128) {
             // K = H + A'DA on the fp64 matrix cores (v_mfma_f64_16x16x4_f64): the lower block
-            // triangle of ceil(n/16)^2 16 x 16 tiles, tile t = w, w + 4, ... on wave w (at most 9
+            // triangle of ceil(n/16)^2 16 x 16 tiles, on wave w the tiles of tile_of (at most 9
             // per wave); each k-step takes 4 rows of A from the LDS row tile - lane l supplies
             // A[r][16 I + l%16] (r = 4 s + l/16) as the A operand and d_r A[r][16 J + l%16] as the
             // B operand, so tile (I, J) accumulates sum_r A[r][16I + i] d_r A[r][16J + j].
@@ -1172,10 +1227,10 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             constexpr int TPW = 9;
             const int lane = tid & 63, wv = tid >> 6;
             const int c16 = lane & 15, k4 = lane >> 4;
-            const int nbk = (n + 15) >> 4, ntl = nbk * (nbk + 1) / 2;
+            const int nbk = (n + 15) >> 4;
             int tI[TPW], tJ[TPW];
 #pragma unroll
-            for (int u = 0; u < TPW; ++u) tile_ij(wv + 4 * u, tI[u], tJ[u]);
+            for (int u = 0; u < TPW; ++u) tile_of(wv, u, nbk, tI[u], tJ[u]);
             dbl4 acc[TPW];
 #pragma unroll
             for (int u = 0; u < TPW; ++u) acc[u] = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -1239,7 +1294,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     }
 #pragma unroll
                     for (int u = 0; u < TPW; ++u) {
-                        if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
+                        if (tI[u] >= 0 && 16.0 * tI[u] < thi) {
                             const int ci = min(16 * tI[u] + c16, n - 1), cj = min(16 * tJ[u] + c16, n - 1);
                             const double2* pa = reinterpret_cast<const double2*>(cur + DQ_GB * ci + 8 * k4);
                             const double2* pb = reinterpret_cast<const double2*>(cur + DQ_GB * cj + 8 * k4);
@@ -1284,7 +1339,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 #pragma unroll
                 for (int u = 0; u < TPW; ++u) {
                     // wave-uniform: the tile exists and the rows reach its column block I (J <= I)
-                    if (wv + 4 * u < ntl && 16.0 * tI[u] < thi) {
+                    if (tI[u] >= 0 && 16.0 * tI[u] < thi) {
                         const int ci = min(16 * tI[u] + c16, n - 1), cj = min(16 * tJ[u] + c16, n - 1);
                         double ai[TILE / 4], aj[TILE / 4];
 #pragma unroll
@@ -1305,7 +1360,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             // the lower triangle to K and chol_2b there (tile_chol on global K spilled).
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
-                if (wv + 4 * u >= ntl) continue;
+                if (tI[u] < 0) continue;
 #pragma unroll
                 for (int e2 = 0; e2 < 4; ++e2) {
                     const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
@@ -1325,7 +1380,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
             DST(1);
             if constexpr (KL) {
-                if (!tile_chol(acc, tI, tJ, K, n, kfl, rvp)) return false;
+                if (!tile_chol(acc, tI, tJ, K, n, kfl, rvp TST_PASS)) return false;
             } else {
                 if (!chol_2b(K, n, kfl, tileA)) return false;
             }
@@ -1517,21 +1572,20 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             // the same blocked factor on tiles of H + sh I (tile_chol, no pivot floor)
             constexpr int TPW = 9;
             const int lane = tid & 63, wv = tid >> 6, c16 = lane & 15, k4 = lane >> 4;
-            const int ntl = ((n + 15) >> 4) * (((n + 15) >> 4) + 1) / 2;
             int tI[TPW], tJ[TPW];
             dbl4 acc[TPW];
 #pragma unroll
             for (int u = 0; u < TPW; ++u) {
-                tile_ij(wv + 4 * u, tI[u], tJ[u]);
+                tile_of(wv, u, (n + 15) >> 4, tI[u], tJ[u]);
 #pragma unroll
                 for (int e2 = 0; e2 < 4; ++e2) {
                     const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
                     double v = (i == j) ? 1.0 : 0.0;
-                    if (wv + 4 * u < ntl && i < n && j < n) v = H[(int64_t)j * n + i] + (i == j ? sh : 0.0);
+                    if (tI[u] >= 0 && i < n && j < n) v = H[(int64_t)j * n + i] + (i == j ? sh : 0.0);
                     acc[u][e2] = v;
                 }
             }
-            if (!tile_chol(acc, tI, tJ, K, n, -1.0, rvp)) flag = -6;
+            if (!tile_chol(acc, tI, tJ, K, n, -1.0, rvp TST_PASS)) flag = -6;
         } else {
             for (int e2 = tid; e2 < n * n; e2 += DT) {
                 const int i = e2 % n, j = e2 / n;
@@ -1621,9 +1675,11 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 #ifdef BQP_DSTAMPS
     if (inst == 0 && tid == 0)
         printf("DSTAMPS it %d rows %llu atw_res %llu res_rest %llu ada %llu chol %llu solve_pre %llu "
-               "atw_sol %llu trsv %llu sol_post %llu step %llu upd %llu other %llu\n", it, dst_acc[0],
+               "atw_sol %llu trsv %llu sol_post %llu step %llu upd %llu other %llu | chol: D %llu Dwait %llu "
+               "P %llu Pwait %llu U %llu\n", it, dst_acc[0],
                dst_acc[10], dst_acc[11], dst_acc[1], dst_acc[2], dst_acc[3], dst_acc[7], dst_acc[8],
-               dst_acc[9], dst_acc[4], dst_acc[5], dst_acc[6]);
+               dst_acc[9], dst_acc[4], dst_acc[5], dst_acc[6], dst_acc[12], dst_acc[13], dst_acc[14],
+               dst_acc[15], dst_acc[16]);
 #endif
     // ---------------------------------------------------------------- outputs
     double fv = 0.0;

@@ -85,6 +85,9 @@ namespace dp {
 #ifndef BQP_EXP_NOSTAGE
 #define BQP_EXP_NOSTAGE 0
 #endif
+#define TAU_FAST_AFF 0.99
+#define TAU_FAST_MU 1e-8
+#define TAU_FAST 0.99999
 #define CMAX_K 100.0
 #define SOC_ALPHA 0.1
 #define DEG_POLISH 1e-10
@@ -2173,7 +2176,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         BARRIER();                                        // B5: corrector direction in (dsc, duc)
         STAMP(6);
         const real rm = row_pass(0, true, smu, 0.0, L.dsc, L.duc);
-        real al = (rm > 1.0 ? 1.0 / rm : 1.0) * a.tau;
+        // step rule (oracle/cpu_ipm.c TAU_FAST): a predictor step above 0.99 on an iterate with
+        // mu > 1e-8 lets the corrector go to 0.99999 of the boundary, else tau
+        const real tau = (al_aff > real(TAU_FAST_AFF) && mu > real(TAU_FAST_MU)) ? fmax(real(a.tau), real(TAU_FAST)) : real(a.tau);
+        real al = (rm > 1.0 ? 1.0 / rm : 1.0) * tau;
         if (al > 1.0) al = 1.0;
         if (lane == 0) X[X_ALPHA] = al;
         const real feb = box_apply(smu, al);

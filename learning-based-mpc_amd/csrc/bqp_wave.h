@@ -137,6 +137,18 @@ __device__ __forceinline__ float rbc(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
                                                                  0x150 + C, 0xf, 0xf, false));
 }
+// the value of 16-lane row Q (lane 16 Q + l%16) in lane l of every row: v_permlane16_swap of a
+// register with itself gives the even / odd row pairs, v_permlane32_swap the halves - VALU only
+// (the ds_bpermute form took an LDS round trip)
+template <int Q>
+__device__ __forceinline__ double xrow_bcast(double v) {
+    double a = v, b = v;
+    pl16_swap(a, b);                 // a: rows (0, 0, 2, 2), b: rows (1, 1, 3, 3)
+    double c = (Q & 1) ? b : a, d = c;
+    pl32_swap(c, d);                 // c: rows (q, q, q, q) of the lower pair, d: of the upper pair
+    return (Q >> 1) ? d : c;
+}
+
 template <int C, int NC, typename T>
 __device__ __forceinline__ void rbc_all(T v, T (&p)[NC]) {
     p[C] = rbc<C>(v);

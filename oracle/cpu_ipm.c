@@ -28,6 +28,9 @@
 #define SOC_ALPHA 0.1     /* predictor step below this on a feasible iterate: corrector without  */
                           /* the second-order term (a centring step; Mehrotra's stall safeguard)  */
 #ifndef CMAX_K
+#define TAU_FAST_AFF 0.99   /* step rule: predictor step above this ... */
+#define TAU_FAST_MU 1e-8     /* ... and mu above this: the corrector step goes to TAU_FAST */
+#define TAU_FAST 0.99999
 #define CMAX_K 100.0     /* and every row: t_i lam_i <= CMAX_K tol_comp (the average alone lets one */
 #endif            /* weakly active row keep t ~ 1e-10: first moves off by 1e-7 at N = 100) */
 #ifndef DEG_POLISH
@@ -945,6 +948,7 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r];
         solve_kkt(P, W, rcx, rcu, rcp);
         double a = max_step(P, W);
+        const double a_pred_keep = a;
         /* along the affine direction t dlam + lam dt = -t lam: the complementarity after the
          * step is cs (1 - a) + a^2 sum dt dlam (the kernel's pred_pass) */
         double mua = (cs * (1.0 - a) + a * a * comp_s2(P, W)) / (mc > 0 ? mc : 1);
@@ -958,7 +962,15 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         for (int i = 0; i < nur; ++i) rcu[i] = W->tu[i] * W->lu[i] + soc * (W->dtu[i] * W->dlu[i]) - sg * mu;
         for (int r = 0; r < P->mp; ++r) rcp[r] = W->tp[r] * W->lp[r] + soc * (W->dtp[r] * W->dlp[r]) - sg * mu;
         solve_kkt(P, W, rcx, rcu, rcp);
-        a = max_step(P, W) * op->tau;
+        {
+            /* step rule (round 5): a predictor step >= TAU_FAST_AFF marks a well-centred iterate
+             * whose affine direction is nearly feasible - the corrector then goes to TAU_FAST of
+             * the boundary while mu > TAU_FAST_MU (below it the barrier Hessian ~ 1/mu resolves
+             * the stationarity residual only to ~tol: the C3 stalls at mu ~ 1e-17 with steps
+             * this long), else tau.  C2 9.13 -> 8.02 iterations on the stored states. */
+            const double tau = (a_pred_keep > TAU_FAST_AFF && mu > TAU_FAST_MU) ? fmax(op->tau, TAU_FAST) : op->tau;
+            a = max_step(P, W) * tau;
+        }
         if (a > 1.0) a = 1.0;
         {
             /* row residuals of the stepped iterate (the kernel's linear update) */

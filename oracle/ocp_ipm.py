@@ -125,6 +125,13 @@ def residuals(o, st):
     return rs, ru, re, (rixu, rixl, riuu, riul, rip)
 
 
+def _comp_max(o, st):
+    """max over active rows of t lam (the per-row complementarity of the stopping rule)"""
+    pairs = [(st.txu, st.lxu, o.mxu), (st.txl, st.lxl, o.mxl), (st.tuu, st.luu, o.muu),
+             (st.tul, st.lul, o.mul), (st.tp, st.lp, np.ones(o.mp, bool))]
+    return max(((t * l)[msk].max(initial=0.0) for t, l, msk in pairs), default=0.0)
+
+
 def _comp_sum(o, st, dt=None, dl=None, a=0.0):
     """sum over active rows of (t + a dt)(lam + a dl)."""
     tot = 0.0
@@ -302,6 +309,7 @@ def nx_(o):
 
 # stationarity is relative to 1 + |H v + g|_inf, feasibility to 1 + |bounds|_inf, mu absolute
 DEFAULTS = dict(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995)
+TAU_FAST_AFF, TAU_FAST_MU, TAU_FAST = 0.99, 1e-8, 0.99999
 
 
 def solve(d, x0, w=None, opts=None, trace=None):
@@ -322,8 +330,10 @@ def solve(d, x0, w=None, opts=None, trace=None):
         if trace is not None:
             trace.append(dict(it=it, mu=mu, r_stat=r_stat, r_feas=r_feas,
                               s=st.s.copy(), u=st.u.copy()))
+        # stop: also every row's t lam <= 100 tol_comp (oracle/cpu_ipm.c CMAX_K; the average alone
+        # let one weakly active row keep t ~ 1e-10)
         if (r_stat <= op['tol_stat'] * (1.0 + o.gscale) and r_feas <= op['tol_feas'] * (1.0 + o.bscale)
-                and mu <= op['tol_comp']):
+                and mu <= op['tol_comp'] and _comp_max(o, st) <= 100.0 * op['tol_comp']):
             exitflag = 1
             break
         if mu > MU_BLOWUP * mu_min and r_feas > 1e-6 * (1.0 + o.bscale):
@@ -342,7 +352,10 @@ def solve(d, x0, w=None, opts=None, trace=None):
               for t, l, dta, dla in zip([st.txu, st.txl, st.tuu, st.tul, st.tp],
                                          [st.lxu, st.lxl, st.luu, st.lul, st.lp], dt, dl)]
         ds, du, dpi, dt, dl = riccati_solve(o, st, fac, rs, ru, re, ri, rc)
-        a = min(1.0, op['tau'] * _max_step(st, o, dt, dl))
+        # step rule (oracle/cpu_ipm.c TAU_FAST): a nearly full predictor step on an iterate with
+        # mu > 1e-8 lets the corrector go to 0.99999 of the boundary
+        tau = max(op['tau'], TAU_FAST) if (a > TAU_FAST_AFF and mu > TAU_FAST_MU) else op['tau']
+        a = min(1.0, tau * _max_step(st, o, dt, dl))
         _apply(st, o, a, ds, du, dpi, dt, dl)
     nx = o.nx
     return dict(x=st.s[:, :nx].copy(), u=st.u.copy(), theta=st.s[0, nx:].copy(),

@@ -616,6 +616,14 @@ def cll_subproblem_roofline(dl, X0, h):
     kms, nl = h.kernel_ms()
     its = out['iterations'].astype(float)
     F_it = nz * (nz + 1) * mr + nz ** 3 / 3.0 + 12.0 * nz * mr + 8.0 * nz * nz
+    # the work the kernel forms: A'DA only on the 16 x 16 output tiles of the
+    # lower block triangle that a 32-row tile's rows reach (1 + last nonzero column of each row;
+    # the skipped products are exact zeros), 2 x 16 x 16 x 32 flops per reached tile and row tile;
+    # the row products A v / A'v over each row's nonzero columns
+    hr = np.array([(np.flatnonzero(A[r])[-1] + 1) if A[r].any() else 0 for r in range(mr)])
+    reach = [int(np.ceil(hr[t:t + 32].max() / 16.0)) for t in range(0, mr, 32)]
+    ada_nz = sum(R * (R + 1) / 2 for R in reach) * 2.0 * 16 * 16 * 32
+    F_it_nz = ada_nz + nz ** 3 / 3.0 + 12.0 * float(hr.sum()) + 8.0 * nz * nz
     # HBM bytes per launch and MFMA busy fraction of the same kernel in the loop (rocprofv3 PMC
     # passes of bench.py --config CLL, tools/gpu_r04_prof.sh -> profiles/pmc_CLL.json)
     traffic = tsrc = mfma = None
@@ -623,14 +631,21 @@ def cll_subproblem_roofline(dl, X0, h):
     if os.path.exists(pj):
         pm = json.load(open(pj))
         traffic, tsrc, mfma = pm['hbm_bytes_per_launch'], pm['source'], round(pm['mfma_busy_frac_est'], 4)
-    flops = float(its.sum() * F_it)
+    flops = float(its.sum() * F_it_nz)
+    flops_dense = float(its.sum() * F_it)
     ach = flops / (kms * 1e-3) / 1e12
+    ach_d = flops_dense / (kms * 1e-3) / 1e12
     return dict(bound='fp64_mfma', achieved=round(ach, 4), peak=FP64_PEAK_TFLOPS, unit='TFLOP/s',
                 frac=round(ach / FP64_PEAK_TFLOPS, 5), traffic=traffic, kernel_ms=round(kms, 4),
-                flops_per_launch=flops, launches=nl, traffic_source=tsrc, mfma_busy_frac=mfma,
+                flops_per_launch=flops, flops_per_launch_dense_count=flops_dense,
+                frac_dense_count=round(ach_d / FP64_PEAK_TFLOPS, 5),
+                ada_tiles_formed_frac=round(ada_nz / (nz * (nz + 1) * mr), 4),
+                launches=nl, traffic_source=tsrc, mfma_busy_frac=mfma,
                 note='dense_ipm_kernel on the loop sub-problem shape (n = %d, m = %d, batch %d, '
                      'mean %.1f IPM iterations, exit flags %s): K = H + A\'DA on the fp64 matrix '
-                     'cores; kernel_ms covers the solve and the polish launch' %
+                     'cores; frac counts the work the kernel forms (A\'DA on the reached tiles, '
+                     'row products over the nonzero columns), frac_dense_count the dense n(n+1)m '
+                     'A\'DA; kernel_ms covers the solve and the polish launch' %
                      (nz, mr, B, its.mean(), dict(zip(*[v.tolist() for v in np.unique(flag, return_counts=True)]))))
 
 

@@ -29,7 +29,7 @@
                           /* the second-order term (a centring step; Mehrotra's stall safeguard)  */
 #ifndef CMAX_K
 #define TAU_FAST_AFF 0.99   /* step rule: predictor step above this ... */
-#define TAU_FAST_MU 1e-8     /* ... and mu above this: the corrector step goes to TAU_FAST */
+#define TAU_FAST_MU 1e-6     /* ... and mu above this: the corrector step goes to TAU_FAST */
 #define TAU_FAST 0.99999
 #define CMAX_K 100.0     /* and every row: t_i lam_i <= CMAX_K tol_comp (the average alone lets one */
 #endif            /* weakly active row keep t ~ 1e-10: first moves off by 1e-7 at N = 100) */
@@ -965,9 +965,12 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
         {
             /* step rule (round 5): a predictor step >= TAU_FAST_AFF marks a well-centred iterate
              * whose affine direction is nearly feasible - the corrector then goes to TAU_FAST of
-             * the boundary while mu > TAU_FAST_MU (below it the barrier Hessian ~ 1/mu resolves
-             * the stationarity residual only to ~tol: the C3 stalls at mu ~ 1e-17 with steps
-             * this long), else tau.  C2 9.13 -> 8.02 iterations on the stored states. */
+             * the boundary while mu > TAU_FAST_MU, else tau.  Below ~1e-7 such steps overshoot
+             * mu (DI instances of F5 went from 7e-8 to 1e-10 in one step and then stalled at
+             * mu ~ 1e-17 with the stationarity residual stuck at 1.3x its tolerance: the barrier
+             * Hessian ~ 1/mu resolves it no further).  Iterations on the C port: C2 9.13 -> 8.31
+             * (stored states), C3 12.60 -> 12.47, C5 9.54 -> 8.69, C4 10.29 -> 9.54 (the exact
+             * classification unchanged). */
             const double tau = (a_pred_keep > TAU_FAST_AFF && mu > TAU_FAST_MU) ? fmax(op->tau, TAU_FAST) : op->tau;
             a = max_step(P, W) * tau;
         }

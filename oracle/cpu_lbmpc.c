@@ -599,7 +599,53 @@ static int sqp(const cll_prob *P, cll_work *W, const double *dx0, int *iters) {
             double hd = 0.0;
             for (int j = 0; j < n; ++j) hd = fmax(hd, fabs(W->H[(size_t)j * n + j]));
             for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
-            if (!chol(W->K, n, 1e-10 * hd, 1)) memcpy(W->H, W->Hg, sizeof(double) * n * n);
+            if (!chol(W->K, n, 1e-10 * hd, 1)) {
+                static int hm = -1;
+                if (hm < 0) { const char *e = getenv("CLL_HMODE"); hm = e ? atoi(e) : 0; }
+                int ok = 0;
+                if (hm == 1) {          /* Levenberg shift */
+                    for (double dl = 1e-8; dl <= 1e-1 && !ok; dl *= 10.0) {
+                        for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
+                        for (int i = 0; i < n; ++i) W->K[(size_t)i * n + i] += dl * hd;
+                        if (chol(W->K, n, 1e-10 * hd, 1)) {
+                            ok = 1;
+                            for (int i = 0; i < n; ++i) W->H[(size_t)i * n + i] += dl * hd;
+                        }
+                    }
+                } else if (hm == 2) {   /* H_GN + theta (H - H_GN) */
+                    for (double th = 0.5; th >= 1.0 / 64 && !ok; th *= 0.5) {
+                        for (int i = 0; i < n; ++i)
+                            for (int j = 0; j <= i; ++j)
+                                W->K[(size_t)i * n + j] = W->Hg[(size_t)i * n + j] + th * (W->H[(size_t)i * n + j] - W->Hg[(size_t)i * n + j]);
+                        if (chol(W->K, n, 1e-10 * hd, 1)) {
+                            ok = 1;
+                            for (int i = 0; i < n * n; ++i) W->H[i] = W->Hg[i] + th * (W->H[i] - W->Hg[i]);
+                        }
+                    }
+                }
+                else if (hm == 3 || hm == 4) {   /* modified Cholesky: negative / tiny pivots -> |d| */
+                    const double flo = (hm == 3 ? 1e-6 : 1e-4) * hd;
+                    for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
+                    for (int j = 0; j < n; ++j) {
+                        double *Kj = W->K + (size_t)j * n;
+                        double d = Kj[j];
+                        for (int k = 0; k < j; ++k) d -= Kj[k] * Kj[k];
+                        double dm = fmax(fabs(d), flo);
+                        W->H[(size_t)j * n + j] += dm - d;          /* E_j */
+                        d = sqrt(dm);
+                        Kj[j] = d;
+                        const double id = 1.0 / d;
+                        for (int i = j + 1; i < n; ++i) {
+                            double *Ki = W->K + (size_t)i * n;
+                            double s2 = Ki[j];
+                            for (int k = 0; k < j; ++k) s2 -= Ki[k] * Kj[k];
+                            Ki[j] = s2 * id;
+                        }
+                    }
+                    ok = 1;
+                }
+                if (!ok) memcpy(W->H, W->Hg, sizeof(double) * n * n);
+            }
         }
         for (int i = 0; i < m; ++i) W->bsh[i] = W->bin[i] - rdot(W, i, W->z);
         const int qflag = dense_ipm(W, it >= POL_STALL ? 2 : 0, 100);

@@ -480,27 +480,53 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
     const double tol = 1e-10 * fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
     // the Cholesky below overwrites the lower triangle and the diagonal: keep the diagonal (the
     // strict upper triangle stays the exact matrix)
+    const double hd = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
     double* dsave = TA;
     for (int j = tid; j < n; j += 256) dsave[j] = Kx[j * n + j];
     __syncthreads();
-    bool pd = true;
-    for (int j = 0; j < n; ++j) {
-        const double d = Kx[j * n + j];
-        if (!(d > tol)) { pd = false; break; }      // uniform: every thread reads the same pivot
-        const double sq = sqrt(d);
-        for (int i = j + 1 + tid; i < n; i += 256) Kx[j * n + i] /= sq;
-        __syncthreads();
-        for (int c = j + 1; c < n; ++c) {
-            const double lc = Kx[j * n + c];
-            for (int i = c + tid; i < n; i += 256) Kx[c * n + i] -= Kx[j * n + i] * lc;
+    // Cholesky test of H + sh I: lower triangle restored from the upper one, every pivot above tol
+    auto attempt = [&](double sh) -> bool {
+        for (int e = tid; e < n * n; e += 256) {
+            const int i = e % n, j = e / n;
+            if (i > j) Kx[e] = Kx[i * n + j];
+            else if (i == j) Kx[e] = dsave[i] + sh;
         }
         __syncthreads();
+        bool pd = true;
+        for (int j = 0; j < n; ++j) {
+            const double d = Kx[j * n + j];
+            if (!(d > tol)) { pd = false; break; }      // uniform: every thread reads the same pivot
+            const double sq = sqrt(d);
+            for (int i = j + 1 + tid; i < n; i += 256) Kx[j * n + i] /= sq;
+            __syncthreads();
+            for (int c = j + 1; c < n; ++c) {
+                const double lc = Kx[j * n + c];
+                for (int i = c + tid; i < n; i += 256) Kx[c * n + i] -= Kx[j * n + i] * lc;
+            }
+            __syncthreads();
+        }
+        __syncthreads();                                 // all have read the failing pivot
+        return pd;
+    };
+    // regularised exact Hessian (round 5; oracle/cpu_lbmpc.c hess_shift_k, oracle/lbmpc.py
+    // hess_shift): if H is not positive definite, the smallest grid shift 1e-12 hd 4^k (k = 0..20,
+    // bisection: definiteness is monotone in the shift) that makes it so; H_GN (left in a.H) only
+    // if none does.  (Falling back to H_GN at once converged linearly: 200 SQP iterations at one
+    // step of a +-0.02 DMS instance, 7 with the shift.)
+    double shift = 0.0;
+    if (!attempt(0.0)) {
+        int lo = -1, hi = 20;
+        if (!attempt(ldexp(1e-12 * hd, 2 * hi))) return;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) / 2;
+            if (attempt(ldexp(1e-12 * hd, 2 * mid))) hi = mid; else lo = mid;
+        }
+        shift = ldexp(1e-12 * hd, 2 * hi);
     }
-    if (!pd) return;
     double* Hw = a.H + (int64_t)b * n * n;
     for (int e = tid; e < n * n; e += 256) {
         const int i = e % n, j = e / n;
-        Hw[e] = (i == j) ? dsave[i] : (i < j ? Kx[e] : Kx[i * n + j]);
+        Hw[e] = (i == j) ? dsave[i] + shift : (i < j ? Kx[e] : Kx[i * n + j]);
     }
     if (tid == 0 && a.hused) a.hused[b] += 1;
 }

@@ -289,6 +289,25 @@ static int chol(double *K, int n, double thr, int mode) {
     return 1;
 }
 
+/* regularised exact Hessian (round 5): smallest grid shift delta_k = 1e-12 hd 4^k, k = 0..20,
+ * with H + delta_k I positive definite (chol pivots above 1e-10 hd), by bisection over k; -1 if
+ * none.  Same grid, test and search in oracle/lbmpc.py (hess_shift) and bqp_lbmpc.hip. */
+#define HSHIFT(hd, k) ldexp(1e-12 * (hd), 2 * (k))
+static int hess_try(cll_work *W, int n, double hd, double sh) {
+    for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
+    for (int i = 0; i < n; ++i) W->K[(size_t)i * n + i] += sh;
+    return chol(W->K, n, 1e-10 * hd, 1);
+}
+static int hess_shift_k(cll_work *W, int n, double hd) {
+    int lo = -1, hi = 20;
+    if (!hess_try(W, n, hd, HSHIFT(hd, hi))) return -1;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) / 2;
+        if (hess_try(W, n, hd, HSHIFT(hd, mid))) hi = mid; else lo = mid;
+    }
+    return hi;
+}
+
 static void chol_solve(const double *L, int n, double *x) {
     for (int i = 0; i < n; ++i) {
         const double *Li = L + (size_t)i * n;
@@ -347,7 +366,7 @@ static double kdiag_max(const cll_work *W) {
 /* CLL_TRACE=1: per sub-problem exit diagnostics on stderr (read once) */
 static int cll_trace(void) {
     static int v = -1;
-    if (v < 0) v = getenv("CLL_TRACE") != NULL;
+    if (v < 0) { const char *e = getenv("CLL_TRACE"); v = e ? (atoi(e) > 1 ? atoi(e) : 1) : 0; }
     return v;
 }
 
@@ -600,51 +619,14 @@ static int sqp(const cll_prob *P, cll_work *W, const double *dx0, int *iters) {
             for (int j = 0; j < n; ++j) hd = fmax(hd, fabs(W->H[(size_t)j * n + j]));
             for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
             if (!chol(W->K, n, 1e-10 * hd, 1)) {
-                static int hm = -1;
-                if (hm < 0) { const char *e = getenv("CLL_HMODE"); hm = e ? atoi(e) : 0; }
-                int ok = 0;
-                if (hm == 1) {          /* Levenberg shift */
-                    for (double dl = 1e-8; dl <= 1e-1 && !ok; dl *= 10.0) {
-                        for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
-                        for (int i = 0; i < n; ++i) W->K[(size_t)i * n + i] += dl * hd;
-                        if (chol(W->K, n, 1e-10 * hd, 1)) {
-                            ok = 1;
-                            for (int i = 0; i < n; ++i) W->H[(size_t)i * n + i] += dl * hd;
-                        }
-                    }
-                } else if (hm == 2) {   /* H_GN + theta (H - H_GN) */
-                    for (double th = 0.5; th >= 1.0 / 64 && !ok; th *= 0.5) {
-                        for (int i = 0; i < n; ++i)
-                            for (int j = 0; j <= i; ++j)
-                                W->K[(size_t)i * n + j] = W->Hg[(size_t)i * n + j] + th * (W->H[(size_t)i * n + j] - W->Hg[(size_t)i * n + j]);
-                        if (chol(W->K, n, 1e-10 * hd, 1)) {
-                            ok = 1;
-                            for (int i = 0; i < n * n; ++i) W->H[i] = W->Hg[i] + th * (W->H[i] - W->Hg[i]);
-                        }
-                    }
-                }
-                else if (hm == 3 || hm == 4) {   /* modified Cholesky: negative / tiny pivots -> |d| */
-                    const double flo = (hm == 3 ? 1e-6 : 1e-4) * hd;
-                    for (int i = 0; i < n; ++i) memcpy(W->K + (size_t)i * n, W->H + (size_t)i * n, sizeof(double) * (i + 1));
-                    for (int j = 0; j < n; ++j) {
-                        double *Kj = W->K + (size_t)j * n;
-                        double d = Kj[j];
-                        for (int k = 0; k < j; ++k) d -= Kj[k] * Kj[k];
-                        double dm = fmax(fabs(d), flo);
-                        W->H[(size_t)j * n + j] += dm - d;          /* E_j */
-                        d = sqrt(dm);
-                        Kj[j] = d;
-                        const double id = 1.0 / d;
-                        for (int i = j + 1; i < n; ++i) {
-                            double *Ki = W->K + (size_t)i * n;
-                            double s2 = Ki[j];
-                            for (int k = 0; k < j; ++k) s2 -= Ki[k] * Kj[k];
-                            Ki[j] = s2 * id;
-                        }
-                    }
-                    ok = 1;
-                }
-                if (!ok) memcpy(W->H, W->Hg, sizeof(double) * n * n);
+                /* indefinite: the smallest shift delta_k = 1e-12 hd 4^k (k = 0 .. 20, found by
+                 * bisection - positive definiteness is monotone in the shift) for which H + delta
+                 * I passes the same test; Gauss-Newton only when even k = 20 fails (VERDICT r4
+                 * item 6: falling back to H_GN at once converged linearly - 200 SQP iterations on
+                 * a +-0.02 DMS instance whose exact Hessian is indefinite; 7 with the shift) */
+                const int k = hess_shift_k(W, n, hd);
+                if (k < 0) memcpy(W->H, W->Hg, sizeof(double) * n * n);
+                else for (int i = 0; i < n; ++i) W->H[(size_t)i * n + i] += HSHIFT(hd, k);
             }
         }
         for (int i = 0; i < m; ++i) W->bsh[i] = W->bin[i] - rdot(W, i, W->z);
@@ -660,6 +642,8 @@ static int sqp(const cll_prob *P, cll_work *W, const double *dx0, int *iters) {
         for (int j = 0; j < n; ++j) sl += W->f[j] * W->d[j];
         for (int i = 0; i < m; ++i) viol = fmax(viol, -W->bsh[i]);
         const int feas0 = viol <= 1e-9;
+        if (cll_trace() >= 2) fprintf(stderr, "sqp it %d qflag %d |d| %.3e stat %.3e (tol %.3e) J %.15e\n", it, qflag, dn,
+                                      st, tol_stat * (1.0 + fn), J0);
         const int qp_ok = qflag == 1 || ((qflag == 0 || qflag == -8) && isfinite(dn) && isfinite(st));
         if (qflag == -2 || !qp_ok) { flag = qflag == -2 ? -2 : -8; break; }
         if (feas0 && ((qflag == 1 && dn <= tol_step * (1.0 + zn) && st <= tol_stat * (1.0 + fn)) ||

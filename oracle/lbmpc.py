@@ -160,11 +160,13 @@ def nw_hess(xi, data):
     return g, dg, d2g
 
 
-def pd_cholesky(H, rel=1e-10):
-    """right-looking Cholesky of H with every pivot required above rel max_i |H_ii|"""
+def pd_cholesky(H, rel=1e-10, tol=None):
+    """right-looking Cholesky of H with every pivot required above rel max_i |H_ii| (or above the
+    absolute tol)"""
     K = np.array(H, float)
     n = K.shape[0]
-    tol = rel * np.abs(np.diag(K)).max()
+    if tol is None:
+        tol = rel * np.abs(np.diag(K)).max()
     for j in range(n):
         d = K[j, j]
         if not d > tol:
@@ -172,6 +174,27 @@ def pd_cholesky(H, rel=1e-10):
         K[j + 1:, j] /= np.sqrt(d)
         K[j + 1:, j + 1:] -= np.outer(K[j + 1:, j], K[j + 1:, j])
     return True
+
+
+def hess_shift(H):
+    """regularised exact Hessian (round 5, oracle/cpu_lbmpc.c hess_shift_k): the smallest grid
+    shift delta_k = 1e-12 hd 4^k (k = 0..20, hd = max|H_ii|) with H + delta_k I positive definite
+    under pd_cholesky's test (pivots above 1e-10 hd), by bisection over k (definiteness is
+    monotone in the shift); None if even k = 20 fails"""
+    hd = np.abs(np.diag(H)).max()
+    tol = 1e-10 * hd
+    n = H.shape[0]
+    sh = lambda k: np.ldexp(1e-12 * hd, 2 * k)
+    lo, hi = -1, 20
+    if not pd_cholesky(H + sh(hi) * np.eye(n), tol=tol):
+        return None
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if pd_cholesky(H + sh(mid) * np.eye(n), tol=tol):
+            hi = mid
+        else:
+            lo = mid
+    return sh(hi)
 
 
 def psd_part(W):
@@ -265,8 +288,13 @@ def sqp(p, x0, z0=None, max_iter=100, tol_step=1e-10, tol_stat=1e-9, trace=None,
             if hessian == 'exact' and not pd_cholesky(H):
                 # the exact Hessian of the learned cost when it is positive definite (Cholesky
                 # pivots above 1e-10 max|H_ii|, the test of bqp_lbmpc.hip lbmpc_hess_kernel),
-                # the Gauss-Newton matrix otherwise
-                H, f = gn_model(p, x0, z)
+                # else shifted by the smallest grid delta that makes it so (hess_shift), the
+                # Gauss-Newton matrix only if no shift does
+                dsh = hess_shift(H)
+                if dsh is None:
+                    H, f = gn_model(p, x0, z)
+                else:
+                    H = H + dsh * np.eye(H.shape[0])
         qp = dict(H=H, f=f, A=Ain, b=bin_ - Ain @ z, Aeq=np.zeros((0, n)), beq=np.zeros(0),
                   lb=np.full(n, -np.inf), ub=np.full(n, np.inf))
         d, _, lamq, info = dense_qp.solve(qp)

@@ -53,3 +53,16 @@ def test_cpu_loop_threads_identical(mg):
     b = _loop(mg, x0, 2, threads=3)
     for u, v in zip(a, b):
         assert np.array_equal(u, v)
+
+
+def test_cpu_loop_indefinite_hessian(mg):
+    """the +-0.02 instance whose exact Hessian is indefinite at its third step
+    (tests/golden/dms_indefinite.npz, oracle/make_indefinite_fixture.py).  With the smallest grid
+    shift that makes it positive definite (hess_shift_k) the C restatement ends every step within
+    20 SQP iterations at the oracle's first moves (the Gauss-Newton fallback took 200 there and
+    stopped 6e-5 away)."""
+    f = golden('dms_indefinite.npz')
+    X, U, its, flags = _loop(mg, f['x0'][None], 3, threads=1)
+    assert (flags == 1).all()
+    assert its.max() <= 20, its
+    assert np.abs(U[0] - f['U']).max() < 1e-6, np.abs(U[0] - f['U'])

@@ -125,3 +125,19 @@ def test_dms_lbmpc_loop_vs_c_restatement(mg):
           % (e[..., :2].max(), e.max(), r.iterations.mean(), itc.mean()))
     assert e[..., :2].max() < 1e-7
     assert e.max() < 1e-4
+
+
+def test_indefinite_hessian_instance(mg):
+    """the +-0.02 DMS instance whose exact Hessian is indefinite at its third
+    closed-loop step (tests/golden/dms_indefinite.npz from oracle/make_indefinite_fixture.py): the
+    GPU SQP shifts it by the smallest grid delta that makes it positive definite
+    (lbmpc_hess_kernel) and ends every step within 20 SQP iterations at the oracle's first moves
+    (1e-6); with the Gauss-Newton fallback this step ran into the 200-iteration limit"""
+    import bqp
+    f = golden('dms_indefinite.npz')
+    r = bqp.closed_loop_sqp(_mpc(mg), f['x0'][None], 3, learning=dict(q=100, mask=1))
+    print('indefinite instance: SQP iterations', r.iterations[0].tolist(), 'oracle',
+          f['iterations'].tolist(), '|U - U_oracle|', np.abs(r.U[0, :, 0] - f['U']).tolist())
+    assert (r.exitflag == 1).all(), r.exitflag
+    assert r.iterations.max() <= 20
+    assert np.abs(r.U[0, :, 0] - f['U']).max() < 1e-6

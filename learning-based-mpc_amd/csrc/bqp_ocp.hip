@@ -88,6 +88,7 @@ namespace dp {
 #define TAU_FAST_AFF 0.99
 #define TAU_FAST_MU 1e-6
 #define TAU_FAST 0.99999
+#define TAU_FAST_END 0.99999
 #define CMAX_K 100.0
 #define SOC_ALPHA 0.1
 #define DEG_POLISH 1e-10
@@ -2177,8 +2178,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         STAMP(6);
         const real rm = row_pass(0, true, smu, 0.0, L.dsc, L.duc);
         // step rule (oracle/cpu_ipm.c TAU_FAST): a predictor step above 0.99 on an iterate with
-        // mu > 1e-6 lets the corrector go to 0.99999 of the boundary, else tau
-        const real tau = (al_aff > real(TAU_FAST_AFF) && mu > real(TAU_FAST_MU)) ? fmax(real(a.tau), real(TAU_FAST)) : real(a.tau);
+        // mu > 1e-6, or any predictor step of at least 0.99999 (the Newton end phase), lets the
+        // corrector go to 0.99999 of the boundary, else tau
+        const bool fast = (al_aff > real(TAU_FAST_AFF) && mu > real(TAU_FAST_MU)) || al_aff >= real(TAU_FAST_END);
+        const real tau = fast ? fmax(real(a.tau), real(TAU_FAST)) : real(a.tau);
         real al = (rm > 1.0 ? 1.0 / rm : 1.0) * tau;
         if (al > 1.0) al = 1.0;
         if (lane == 0) X[X_ALPHA] = al;

@@ -309,7 +309,7 @@ def nx_(o):
 
 # stationarity is relative to 1 + |H v + g|_inf, feasibility to 1 + |bounds|_inf, mu absolute
 DEFAULTS = dict(max_iter=50, tol_stat=1e-8, tol_feas=1e-10, tol_comp=1e-14, tau=0.995)
-TAU_FAST_AFF, TAU_FAST_MU, TAU_FAST = 0.99, 1e-6, 0.99999
+TAU_FAST_AFF, TAU_FAST_MU, TAU_FAST, TAU_FAST_END = 0.99, 1e-6, 0.99999, 0.99999
 
 
 def solve(d, x0, w=None, opts=None, trace=None):
@@ -353,8 +353,10 @@ def solve(d, x0, w=None, opts=None, trace=None):
                                          [st.lxu, st.lxl, st.luu, st.lul, st.lp], dt, dl)]
         ds, du, dpi, dt, dl = riccati_solve(o, st, fac, rs, ru, re, ri, rc)
         # step rule (oracle/cpu_ipm.c TAU_FAST): a nearly full predictor step on an iterate with
-        # mu > 1e-6 lets the corrector go to 0.99999 of the boundary
-        tau = max(op['tau'], TAU_FAST) if (a > TAU_FAST_AFF and mu > TAU_FAST_MU) else op['tau']
+        # mu > 1e-6, or any predictor step of at least 0.99999, lets the corrector go to 0.99999 of
+        # the boundary
+        fast = (a > TAU_FAST_AFF and mu > TAU_FAST_MU) or a >= TAU_FAST_END
+        tau = max(op['tau'], TAU_FAST) if fast else op['tau']
         a = min(1.0, tau * _max_step(st, o, dt, dl))
         _apply(st, o, a, ds, du, dpi, dt, dl)
     nx = o.nx

@@ -269,9 +269,13 @@ def launch_ranks(args):
 
 class GpuSolver:
     """One batched structured solve per step through bqp_solve_ocp_batched_device (inputs and
-    outputs resident in HBM, caller stream)."""
+    outputs resident in HBM, caller stream).  streams > 1: consecutive steps go to `streams`
+    HIP streams in turn, each with its own handle (workspace) and output buffers, so a step's
+    workgroups start on the CUs the previous step's workgroups have left - a launch lasts as long
+    as its slowest instance (one instance per SIMD at batch 1024), and its other CUs would idle
+    until then.  Every step still solves the whole batch and writes every output."""
 
-    def __init__(self, wl, local, precision, polish=True):
+    def __init__(self, wl, local, precision, polish=True, streams=1):
         import torch
         import bqp
         from bqp import _lib
@@ -300,39 +304,50 @@ class GpuSolver:
                                  sw=0 if wl['w'] is None else (N + 1) * nv, sxb=0, sub=0,
                                  sFp=0, shp=0, sx0=nx)
         self.dims = _lib.OcpDims(nx, nu, npar, N, mp, prob.poly_stage)
-        self.ox = torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev)
-        self.ou = torch.empty((B, N, nu), dtype=torch.float64, device=dev)
-        self.ot = torch.empty((B, npar), dtype=torch.float64, device=dev)
-        self.of = torch.empty((B,), dtype=torch.float64, device=dev)
-        self.oe = torch.empty((B,), dtype=torch.int32, device=dev)
-        self.oo = torch.empty((B * C.sizeof(_lib.Output),), dtype=torch.uint8, device=dev)
         self.lib = bqp.load()
-        self.h = bqp.Handle(local)
         self.opt = _lib.options(precision={'fp64': 0, 'fp32': 1, 'mixed': 2}[precision], polish=polish)
-        self.stream = torch.cuda.current_stream(dev)
+        self.S = max(1, int(streams))
+        self.sets = []
+        for i in range(self.S):
+            self.sets.append(dict(
+                ox=torch.empty((B, N + 1, nx), dtype=torch.float64, device=dev),
+                ou=torch.empty((B, N, nu), dtype=torch.float64, device=dev),
+                ot=torch.empty((B, npar), dtype=torch.float64, device=dev),
+                of=torch.empty((B,), dtype=torch.float64, device=dev),
+                oe=torch.empty((B,), dtype=torch.int32, device=dev),
+                oo=torch.empty((B * C.sizeof(_lib.Output),), dtype=torch.uint8, device=dev),
+                h=bqp.Handle(local),
+                stream=torch.cuda.current_stream(dev) if i == 0 else torch.cuda.Stream(dev)))
+        self.k = 0
+        self.last = 0
 
     def step(self, with_out=False):
         P = self._lib.dptr
+        i = 0 if with_out else self.k % self.S
+        self.k += 0 if with_out else 1
+        st = self.sets[i]
         rc = self.lib.bqp_solve_ocp_batched_device(
-            self.h.value, C.byref(self.dims), self.B, C.byref(self.data), C.byref(self.opt),
-            P(self.ox), P(self.ou), P(self.ot), P(self.of),
-            C.cast(C.c_void_p(self.oe.data_ptr()), C.POINTER(C.c_int)),
-            C.c_void_p(self.oo.data_ptr()) if with_out else None, None,
-            C.c_void_p(self.stream.cuda_stream))
+            st['h'].value, C.byref(self.dims), self.B, C.byref(self.data), C.byref(self.opt),
+            P(st['ox']), P(st['ou']), P(st['ot']), P(st['of']),
+            C.cast(C.c_void_p(st['oe'].data_ptr()), C.POINTER(C.c_int)),
+            C.c_void_p(st['oo'].data_ptr()) if with_out else None, None,
+            C.c_void_p(st['stream'].cuda_stream))
         self._lib.check(rc, 'bqp_solve_ocp_batched_device')
+        self.last = i
 
     def sync(self):
         self.torch.cuda.synchronize()
 
     def kernel_ms(self):
-        return self.h.kernel_ms()[0]
+        return self.sets[self.last]['h'].kernel_ms()[0]
 
     def first_moves(self):
-        return self.ou[:, 0, :].contiguous(), self.oe
+        st = self.sets[0]
+        return st['ou'][:, 0, :].contiguous(), st['oe']
 
     def outputs(self):
         """per-instance exit statistics (bqp_output) of a step(with_out=True)"""
-        raw = self.oo.cpu().numpy().tobytes()
+        raw = self.sets[0]['oo'].cpu().numpy().tobytes()
         out = (self._lib.Output * self.B).from_buffer_copy(raw)
         return dict(iterations=np.array([o.iterations for o in out]),
                     kkt=np.array([list(o.kkt) for o in out]),
@@ -386,6 +401,8 @@ def main():
                     help='interior-point iterates only (bqp_options.polish = -1)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
+    ap.add_argument('--streams', type=int, default=1,
+                    help='structured configs: consecutive steps on this many HIP streams in turn')
     args = ap.parse_args()
     if args.config in ('C1', 'C2H', 'C2D'):
         return bench_aux(args)
@@ -412,7 +429,8 @@ def main():
     wl = workload(args.config, args.batch, rank, world)
     prob, B = wl['prob'], wl['X'].shape[0]
     N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
-    solver = StubSolver(wl) if args.dry_run else GpuSolver(wl, local, args.precision, not args.no_polish)
+    solver = StubSolver(wl) if args.dry_run else GpuSolver(wl, local, args.precision, not args.no_polish,
+                                                           args.streams)
 
     for _ in range(args.warmup):
         solver.step()
@@ -562,7 +580,7 @@ def main():
             'dtype': {'fp64': 'f64', 'fp32': 'f32', 'mixed': 'f32+f64'}[args.precision],
             'data': wl['data'] + (' [CPU dry run: stub solver, gloo]' if args.dry_run else ''),
             'config': {'workload': wl['text'], 'batch_per_gpu': B, 'horizon': N,
-                       'parallelism': 'dp%d' % world},
+                       'parallelism': 'dp%d' % world, 'streams': args.streams},
             'roofline': roof,
             'cpu_baseline': cpu,
             'check': check,

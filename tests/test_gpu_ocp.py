@@ -53,9 +53,11 @@ def test_f1_matches_cpu_restatement(mg, term_set, handle):
     assert np.median(np.abs(r.u - c['u']).max(axis=(1, 2))) < 1e-11
     # the stop test (mu <= 1e-14) can flip where mu sits at the threshold within round-off of
     # the two implementations (their row sums associate differently; mu stalls at the round-off
-    # floor for an iteration or two there): measured >= 94 % equal, the rest +-1 (one +-2)
-    assert np.abs(r.iterations - c['iterations']).max() <= 2
-    assert np.mean(r.iterations == c['iterations']) > 0.9
+    # floor for an iteration or two there), and so can the step rule's threshold on the
+    # predictor step (0.99999 in the Newton end phase, round 5): measured 92 % equal, the rest
+    # +-1 (one +-3), every instance at the same solution (above)
+    assert np.abs(r.iterations - c['iterations']).max() <= 3
+    assert np.mean(r.iterations == c['iterations']) > 0.85
 
 
 @pytest.mark.parametrize('N', [2, 3, 7, 21, 33])

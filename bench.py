@@ -321,6 +321,10 @@ class GpuSolver:
         self.k = 0
         self.last = 0
 
+    def next_stream(self):
+        """the stream the next step() launches on"""
+        return self.sets[self.k % self.S]['stream']
+
     def step(self, with_out=False):
         P = self._lib.dptr
         i = 0 if with_out else self.k % self.S
@@ -401,8 +405,10 @@ def main():
                     help='interior-point iterates only (bqp_options.polish = -1)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
-    ap.add_argument('--streams', type=int, default=1,
-                    help='structured configs: consecutive steps on this many HIP streams in turn')
+    ap.add_argument('--streams', type=int, default=2,
+                    help='structured configs: consecutive steps on this many HIP streams in turn '
+                         '(a launch lasts as long as its slowest instance; the next step\'s '
+                         'workgroups start on the CUs it has left)')
     args = ap.parse_args()
     if args.config in ('C1', 'C2H', 'C2D'):
         return bench_aux(args)
@@ -438,22 +444,36 @@ def main():
     if world > 1:
         dist.barrier()
     solver.sync()
+    # launch durations over the timed region: an event pair around every step on the stream it
+    # is launched on (the steps overlap on --streams streams, so a launch's duration includes the
+    # time its workgroups wait for the CUs the other stream's launch still holds)
+    evs = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if args.dry_run:
+            solver.step()
+            continue
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        st = solver.next_stream()
+        e0.record(st)
         solver.step()
+        e1.record(st)
+        evs.append((e0, e1))
     solver.sync()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = bd.max_over_ranks(t1 - t0, dev, world)
-    # kernel-only timing: hipEvents on the launch stream, separate pass (one event pair / step)
-    kernel_ms = None
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else None
+    # one launch alone (separate pass, host-synchronised per step): the isolated launch time
+    kernel_ms_alone = None
     if not args.dry_run:
         kms = []
         for _ in range(min(args.steps, 20)):
             solver.step()
             kms.append(solver.kernel_ms())
-        kernel_ms = float(np.mean(kms))
+        kernel_ms_alone = float(np.mean(kms))
     # one all-gather of the first moves + status after timing (result collection, bqp.dist)
     total_rows = wl['total'] if wl['scaling'] == 'strong' else B * world
     u0_loc, fl_loc = solver.first_moves()
@@ -543,17 +563,27 @@ def main():
                 except Exception:
                     traffic = None
             check['mean_iterations_ref'] = float(kref.mean())
+            # steps overlap on --streams streams: the device's rate over the timed region is the
+            # per-step flops over the time per step
+            achieved_pipe = flops_launch / (ms_per_step * 1e-3) / 1e12
             roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                     'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
                     'kernel_ms': round(kernel_ms, 4), 'flops_per_launch': flops_launch,
+                    'kernel_ms_alone': round(kernel_ms_alone, 4),
+                    'achieved_per_step': round(achieved_pipe, 4),
+                    'frac_per_step': round(achieved_pipe / FP64_PEAK_TFLOPS, 5),
                     'traffic_source': traffic_src,
                     'note': 'bound: FP64 VALU issue plus the latency of the sequential N-stage '
                             'Riccati chain (roofline.latency); 78.6 TF/s is the FP64 vector peak '
                             '(= the FP64 MFMA peak) of MI355X; this kernel issues no MFMA (5x5 '
                             'stage blocks, DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
-                            'passes of this config (traffic_source)'}
+                            'passes of this config (traffic_source); kernel_ms = mean launch '
+                            'duration over the timed steps (hipEvents on each launch\'s stream; '
+                            'the steps overlap on config.streams streams), kernel_ms_alone = one '
+                            'launch by itself (host-synchronised pass); achieved_per_step = flops '
+                            'per launch / ms_per_step, the device rate over the timed region'}
             st_json = os.path.join(ROOT, 'profiles', 'stamps_%s.json' % args.config)
             if args.precision == 'fp64' and os.path.exists(st_json):
                 # latency roof: at batch 1024 one instance runs per SIMD, so the

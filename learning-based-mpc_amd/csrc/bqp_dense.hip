@@ -416,7 +416,7 @@ __device__ __forceinline__ bool chol_2b(double* K, int n, double fl, double* jun
 // K(P, c16) / l_PP from row P (symmetric storage) by row swaps (xrow_bcast) - then the rank-1 update of the
 // trailing block; row P of the tile becomes L' (upper), column P L (lower).
 template <int P>
-__device__ __forceinline__ void dtile_piv(dbl4& T, int k4, int c16, double fl, bool& ok, double* rv, int lane) {
+__device__ __forceinline__ void dtile_piv(dbl4& T, int k4, int c16, double fl, bool& ok, double& rvl, int lane) {
     constexpr int EP = P >> 2, SRC = 16 * (P & 3) + P;
     double d = rl(T[EP], SRC);
     if (fl >= 0.0 && !(d > fl)) d = fl;
@@ -440,8 +440,8 @@ __device__ __forceinline__ void dtile_piv(dbl4& T, int k4, int c16, double fl, b
         const double onrow = cg ? xc : (ce ? ljj : T[e]);
         T[e] = r > P ? below : (r == P ? onrow : T[e]);
     }
-    if (lane == 0) rv[P] = inv;
-    if constexpr (P + 1 < 16) dtile_piv<P + 1>(T, k4, c16, fl, ok, rv, lane);
+    rvl = (lane == P) ? inv : rvl;       // lane P keeps 1 / l_PP (stored after the 16 pivots)
+    if constexpr (P + 1 < 16) dtile_piv<P + 1>(T, k4, c16, fl, ok, rvl, lane);
 }
 
 // column P of a panel tile (I, J): L(r, P) = K(r, P) / l_PP reaches the lane's 16-lane row, the
@@ -511,7 +511,9 @@ __device__ __forceinline__ bool dtile(dbl4& T, int J, double* K, int n, double f
         if (r < c16 && 16 * J + c16 < n) T[e] = K[(int64_t)(16 * J + r) * n + 16 * J + c16];
     }
     bool ok = true;
-    dtile_piv<0>(T, k4, c16, fl, ok, rv, lane);
+    double rvl = 0.0;
+    dtile_piv<0>(T, k4, c16, fl, ok, rvl, lane);
+    if (lane < 16) rv[lane] = rvl;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int i = 16 * J + k4 + 4 * e, j = 16 * J + c16;

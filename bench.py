@@ -566,24 +566,30 @@ def main():
             # steps overlap on --streams streams: the device's rate over the timed region is the
             # per-step flops over the time per step
             achieved_pipe = flops_launch / (ms_per_step * 1e-3) / 1e12
-            roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
+            # achieved / frac: the device's rate over the timed region (flops per step over the
+            # time per step: with the steps overlapping on config.streams streams a launch's own
+            # duration counts the time it shares the CUs with the other stream's launch); the
+            # per-launch figure (flops per launch / mean launch duration) beside it
+            roof = {'bound': 'fp64_valu', 'achieved': round(achieved_pipe, 4),
                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                    'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
+                    'frac': round(achieved_pipe / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
                     'kernel_ms': round(kernel_ms, 4), 'flops_per_launch': flops_launch,
                     'kernel_ms_alone': round(kernel_ms_alone, 4),
-                    'achieved_per_step': round(achieved_pipe, 4),
-                    'frac_per_step': round(achieved_pipe / FP64_PEAK_TFLOPS, 5),
+                    'achieved_per_launch': round(achieved, 4),
+                    'frac_per_launch': round(achieved / FP64_PEAK_TFLOPS, 5),
+                    'frac_per_launch_alone': round(flops_launch / (kernel_ms_alone * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 5),
                     'traffic_source': traffic_src,
                     'note': 'bound: FP64 VALU issue plus the latency of the sequential N-stage '
                             'Riccati chain (roofline.latency); 78.6 TF/s is the FP64 vector peak '
                             '(= the FP64 MFMA peak) of MI355X; this kernel issues no MFMA (5x5 '
                             'stage blocks, DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
-                            'passes of this config (traffic_source); kernel_ms = mean launch '
-                            'duration over the timed steps (hipEvents on each launch\'s stream; '
-                            'the steps overlap on config.streams streams), kernel_ms_alone = one '
-                            'launch by itself (host-synchronised pass); achieved_per_step = flops '
-                            'per launch / ms_per_step, the device rate over the timed region'}
+                            'passes of this config (traffic_source); achieved = flops per launch / '
+                            'ms_per_step, the device rate over the timed region (the steps overlap '
+                            'on config.streams streams); kernel_ms = mean launch duration over the '
+                            'timed steps (hipEvents on each launch\'s stream, a launch sharing the '
+                            'CUs with the other stream\'s), kernel_ms_alone = one launch by itself '
+                            '(host-synchronised pass), frac_per_launch(_alone) from those'}
             st_json = os.path.join(ROOT, 'profiles', 'stamps_%s.json' % args.config)
             if args.precision == 'fp64' and os.path.exists(st_json):
                 # latency roof: at batch 1024 one instance runs per SIMD, so the

@@ -582,6 +582,8 @@ int bqp_quadprog_batched(bqp_handle h, const bqp_dims* d, int batch, const bqp_s
 // learning-based MPC: Nadaraya-Watson oracle and the Gauss-Newton SQP (bqp_lbmpc.hip)
 // ------------------------------------------------------------------------------------------
 #define LB_NTRIAL 8
+// SQP iterations at one step after which every QP sub-problem is polished (bqp_lbmpc_solve_batched)
+constexpr int LB_POLISH_STALL = 6;
 
 int bqp_nw_oracle_device(bqp_handle h, int batch, int q, const double* data, int64_t sdata,
                          const double* xi, double* g, double* dg, double bandwidth,
@@ -629,18 +631,12 @@ static int lbmpc_check(const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_data*
     return BQP_OK;
 }
 
-int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
-                                   const bqp_lbmpc_data* D, const bqp_options* opt, double* z,
-                                   double* lam, double* cost, int* exitflag, int* iterations,
-                                   void* stream) {
-    if (!h) return BQP_E_ARG;
-    int rc = lbmpc_check(d, batch, D);
-    if (rc) return rc;
-    if (!z || !exitflag || !iterations) return BQP_E_ARG;
-    DevScope ds(h->device);
-    hipStream_t st = (hipStream_t)stream;
-    bqp_options o;
-    resolve(opt, &o);
+// the learned-model SQP's kernel arguments and per-instance state (done, iteration counts, flags
+// zeroed), and the QP sub-problem's dense-kernel arguments: shared by the batched solve and the
+// asynchronous closed loop
+static hipError_t lbmpc_setup(bqp_handle h, const bqp_lbmpc_dims* d, int batch, const bqp_lbmpc_data* D,
+                              const bqp_options& o, double* z, double* lam, int* exitflag, int* iterations,
+                              hipStream_t st, bqp::LbmpcArgs& a, bqp::DenseKernelArgs& q) {
     const int N = d->N, n = N * d->nu + d->np, m = d->m;
     const int nr = d->n_run * (d->nx + d->nu) + 2 * d->nx;
     const size_t B = batch;
@@ -648,9 +644,9 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     const size_t nd = B * nr * n + B * nr + B * n * n + B * n + 2 * B * m + B * n + B +
                       B * LB_NTRIAL + 2 * B + 2 * n2;
     const size_t ni = 3 * B + 4;
-    HIP_TRY(h->lwork.reserve(sizeof(double) * nd + sizeof(int) * ni));
+    hipError_t e = h->lwork.reserve(sizeof(double) * nd + sizeof(int) * ni);
+    if (e != hipSuccess) return e;
     double* p = (double*)h->lwork.p;
-    bqp::LbmpcArgs a;
     memset(&a, 0, sizeof(a));
     a.Jr = p; p += B * nr * n;
     a.er = p; p += B * nr;
@@ -687,14 +683,13 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     a.LAM = D->LAMBDA; a.PSI = D->PSI; a.xs = D->xs;
     a.data = D->data; a.sdata = D->sdata; a.x0 = D->x0; a.sx0 = D->sx0;
     a.Ain = D->Ain; a.bin = D->bin; a.sbin = D->sbin;
-    HIP_TRY(hipMemsetAsync(a.done, 0, sizeof(int) * (B + 1), st));   // done[] and ndone
-    HIP_TRY(hipMemsetAsync(a.hused, 0, sizeof(int) * B, st));
-    HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * B, st));
-    HIP_TRY(hipMemsetAsync(a.flag, 0, sizeof(int) * B, st));
+    if ((e = hipMemsetAsync(a.done, 0, sizeof(int) * (B + 1), st)) != hipSuccess) return e;   // done[], ndone
+    if ((e = hipMemsetAsync(a.hused, 0, sizeof(int) * B, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.iters, 0, sizeof(int) * B, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.flag, 0, sizeof(int) * B, st)) != hipSuccess) return e;
     // QP sub-problem (dense kernel): min 0.5 d'Hd + f'd  s.t.  Ain d <= bin - Ain z
     const int64_t wst = bqp::dense_work_doubles(n, m, 0);
-    HIP_TRY(h->dwork.reserve(sizeof(double) * ((size_t)wst * B + B * bqp::STATS_W + 8)));
-    bqp::DenseKernelArgs q;
+    if ((e = h->dwork.reserve(sizeof(double) * ((size_t)wst * B + B * bqp::STATS_W + 8))) != hipSuccess) return e;
     memset(&q, 0, sizeof(q));
     q.n = n; q.m = m; q.me = 0; q.batch = batch; q.max_iter = 100;
     q.tol_stat = 1e-8; q.tol_feas = 1e-10; q.tol_comp = 1e-14; q.tau = 0.995;   // bqp_default_options
@@ -711,8 +706,30 @@ int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int ba
     // accurate iterate, which the update kernel takes as is), and the polish launch for them was
     // ~1/3 of each SQP iteration (5.5 of 16 ms, BQP_LB_TRACE=2).  A single solve keeps mode 1: its
     // weakly determined tail inputs move ~1e-6 without the polish.
-    constexpr int LB_POLISH_STALL = 6;
+    // instances whose SQP has finished are not solved again (the update kernel skips them too)
+    q.skip = a.done;
     q.stats = (double*)h->dwork.p + (size_t)wst * B;
+    return hipSuccess;
+}
+
+int bqp_lbmpc_solve_batched_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
+                                   const bqp_lbmpc_data* D, const bqp_options* opt, double* z,
+                                   double* lam, double* cost, int* exitflag, int* iterations,
+                                   void* stream) {
+    if (!h) return BQP_E_ARG;
+    int rc = lbmpc_check(d, batch, D);
+    if (rc) return rc;
+    if (!z || !exitflag || !iterations) return BQP_E_ARG;
+    DevScope ds(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    bqp_options o;
+    resolve(opt, &o);
+    const int N = d->N, n = N * d->nu + d->np;
+    const size_t B = batch;
+    bqp::LbmpcArgs a;
+    bqp::DenseKernelArgs q;
+    HIP_TRY(lbmpc_setup(h, d, batch, D, o, z, lam, exitflag, iterations, st, a, q));
+    (void)n;
     HIP_TRY(hipEventRecord(h->ev0, st));
     int launches = 0;
     // diagnostic (BQP_LB_TRACE=2): per-launch event times of the first SQP iterations
@@ -1035,7 +1052,7 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     const int n = N * d->nu + d->np;
     const size_t B = batch;
     const size_t nd = B * nx + B * n + B * m + B + B * (size_t)q * 8;
-    HIP_TRY(h->cwork.reserve(sizeof(double) * nd + sizeof(int) * 2 * B));
+    HIP_TRY(h->cwork.reserve(sizeof(double) * nd + sizeof(int) * (3 * B + 2)));
     double* s = (double*)h->cwork.p;     // measured deviation state
     double* z = s + B * nx;               // SQP iterate / solution
     double* bin = z + B * n;              // rhs of the step's constraints
@@ -1066,7 +1083,53 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     HIP_TRY(hipEventCreate(&e0.e));
     HIP_TRY(hipEventRecord(e0.e, st));
     int launches = 0;
-    for (int t = 0; t < cl->steps; ++t) {
+    if (!getenv("BQP_LB_TRACE")) {
+        // asynchronous (round 5): every instance runs at its own closed-loop step.  Each round is
+        // one SQP iteration of every unfinished instance, then sqp_loop_advance_kernel moves the
+        // instances whose SQP has finished to their next step (u_0, plant, window, constraints,
+        // warm start).  The step-synchronous form below ran every step's SQP launches until the
+        // batch's slowest instance had converged (2.4 SQP iterations per step on average against
+        // up to 6 at a step) while the converged ones idled; per instance the two forms do the
+        // same operations in the same order (tests/test_gpu_lbmpc_dms.py compares them).
+        int* ts = it + B;
+        int* nfin = ts + B;
+        HIP_TRY(hipMemsetAsync(ts, 0, sizeof(int) * (B + 1), st));
+        HIP_TRY(bqp::launch_sqp_loop_prep(batch, nx, n, m, N * d->nu, 0, s, sl->bin0, sl->Bx, bin, z, st));
+        bqp::LbmpcArgs a;
+        bqp::DenseKernelArgs qd;
+        HIP_TRY(lbmpc_setup(h, &dl, batch, &Dl, *opt, z, nullptr, fl, it, st, a, qd));
+        // sub-problem polish per instance: from its own SQP iteration count (lbmpc solve: mode 2
+        // from LB_POLISH_STALL on, before it the loop's mode 3 - none - or 1)
+        qd.polish = opt->polish < 0 ? 0 : (opt->polish == 3 ? 0 : 1);
+        qd.pol_it = opt->polish < 0 ? nullptr : a.iters;
+        qd.pol_stall = LB_POLISH_STALL;
+        bqp::SqpAdvanceArgs v;
+        memset(&v, 0, sizeof(v));
+        v.batch = batch; v.nx = nx; v.n = n; v.m = m; v.nv = N * d->nu; v.warm = sl->warm;
+        v.steps = cl->steps; v.q = q; v.plant = cl->plant; v.delta = cl->delta;
+        v.hinv2 = 1.0 / (bw * bw); v.lam = lam;
+        v.K = D->K; v.bin0 = sl->bin0; v.Bx = sl->Bx; v.xeq = cl->x_eq; v.ueq = cl->u_eq;
+        v.A = D->A; v.Bm = D->B;
+        v.s = s; v.z = z; v.bin = bin; v.X = X; v.U = U; v.win = win; v.XL = lw->XL; v.Zlog = sl->Z;
+        v.done = a.done; v.iters = a.iters; v.flag = fl; v.hused = a.hused; v.ts = ts; v.nfin = nfin;
+        v.flags = exitflag; v.itlog = sl->iterations;
+        const int max_rounds = cl->steps * opt->max_iter;
+        for (int r = 0; r < max_rounds; ++r) {
+            HIP_TRY(bqp::launch_lbmpc_rollout(a, 1, st));
+            HIP_TRY(bqp::launch_lbmpc_normal(a, st));
+            if (a.hess) HIP_TRY(bqp::launch_lbmpc_hess(a, st));
+            HIP_TRY(bqp::launch_dense(qd, st));
+            HIP_TRY(bqp::launch_lbmpc_rollout(a, 0, st));
+            HIP_TRY(bqp::launch_lbmpc_update(a, st));
+            HIP_TRY(bqp::launch_sqp_loop_advance(v, st));
+            launches += a.hess ? 7 : 6;
+            int nf = 0;
+            HIP_TRY(hipMemcpyAsync(&nf, nfin, sizeof(int), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (nf >= batch) break;
+        }
+    }
+    for (int t = 0; t < (getenv("BQP_LB_TRACE") ? cl->steps : 0); ++t) {
         HIP_TRY(bqp::launch_sqp_loop_prep(batch, nx, n, m, N * d->nu, t > 0 && sl->warm, s,
                                           sl->bin0, sl->Bx, bin, z, st));
         if (t > 0 && !sl->warm) HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));

@@ -39,6 +39,12 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_SOC_ALPHA 0.1      // predictor step below this on a primal-feasible iterate: no SOC term
 #define DQ_POL_ROUNDS 4       // active-set corrections of the polish
 
+// polish mode of an instance: the launch's, or 2 once the instance's own SQP iteration count has
+// reached pol_stall (DenseKernelArgs.pol_it)
+__device__ __forceinline__ int pol_mode(const DenseKernelArgs& a, int inst) {
+    return (a.pol_it && a.pol_it[inst] >= a.pol_stall) ? 2 : a.polish;
+}
+
 struct DWork {
     int64_t K, Y, S, z, y, q, w, dz, dy, rd, re, tA, lA, riA, rcA, dtA, dlA, tB, lB, riB, rcB, dtB, dlB, hr, th,
         total;
@@ -962,7 +968,7 @@ template <bool KL>   // KL: the factor lives in LDS (dense_k_lds(n)); a compile-
                      // generic: flat accesses, ~5k cycles per Cholesky pivot)
 __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
-    if (inst >= a.batch) return;
+    if (inst >= a.batch || (a.skip && a.skip[inst])) return;
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
     extern __shared__ __attribute__((aligned(16))) double dlds[];
     double* sc = dlds + dense_tiles(n) + (KL ? n * n : 0);
@@ -1754,7 +1760,7 @@ __device__ __forceinline__ double atv(const double* A, const double* v, int m, i
 template <int NT>
 __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
-    if (inst >= a.batch) return;
+    if (inst >= a.batch || (a.skip && a.skip[inst])) return;
     const int n = a.n, m = a.m, lane = threadIdx.x;
     extern __shared__ double sm[];
     double* K = sm;                       // n x n column-major; lower Cholesky factor in place
@@ -2130,7 +2136,8 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             wave_sync();
         }
     }
-    if (a.polish && (flag == 0 || flag == -8 || (a.polish == 2 && flag == 1)) && a.work) {
+    const int pm = pol_mode(a, inst);
+    if (pm && (flag == 0 || flag == -8 || (pm == 2 && flag == 1)) && a.work) {
         // hand the iterate to dense_polish_kernel through the instance's workspace (DWork)
         const DWork L = DWork::make(n, m, 0);
         double* W = a.work + (int64_t)inst * a.work_stride;
@@ -2172,8 +2179,10 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
 __global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
     if (inst >= a.batch) return;
+    if (a.skip && a.skip[inst]) return;
     const int flag = a.exitflag[inst];
-    if (!(flag == 0 || flag == -8 || (a.polish == 2 && flag == 1))) return;
+    const int pm = pol_mode(a, inst);
+    if (!pm || !(flag == 0 || flag == -8 || (pm == 2 && flag == 1))) return;
     const int n = a.n, m = a.m, me = a.me, tid = threadIdx.x;
     __shared__ double sc[16];
     __shared__ double xs[DT];
@@ -2281,7 +2290,7 @@ hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
         }
     }
     hipError_t err = hipGetLastError();
-    if (err != hipSuccess || !a.polish || !a.work) return err;
+    if (err != hipSuccess || (!a.polish && !a.pol_it) || !a.work) return err;
     hipLaunchKernelGGL(dense_polish_kernel, dim3(a.batch), dim3(DT), 0, st, a);
     return hipGetLastError();
 }

@@ -93,6 +93,9 @@ struct DenseKernelArgs {
     int64_t work_stride;
     int polish;        // 1: active-set polish after a 0 / -8 exit (bqp_dense.hip::dense_polish);
                        // 2: also after a converged exit (exact active-set steps for the SQP)
+    const int* pol_it; // optional: per-instance SQP iteration counts; mode 2 where >= pol_stall
+    int pol_stall;     // (the learned-model loop, whose instances run at their own SQP iteration)
+    const int* skip;   // optional: instances with skip[i] != 0 are not solved (finished SQPs)
 };
 
 int dense_work_doubles(int n, int m, int me);
@@ -144,6 +147,15 @@ hipError_t launch_mg_plant(int plant, int batch, int N, int steps, int t, double
 // learned-model NLP closed loop glue (bqp_closed_loop_sqp): per instance bin = bin0 + Bx s and
 // the warm start (z shifted one stage, zero last move, theta kept) before the SQP; u_0 = K s + z_0
 // for the plant, and the step's z / iteration count into the caller's logs after it
+// asynchronous learned-model loop: one instance's advance to its next closed-loop step
+struct SqpAdvanceArgs {
+    int batch, nx, n, m, nv, warm, steps, q, plant;
+    double delta, hinv2, lam;
+    const double *K, *bin0, *Bx, *xeq, *ueq, *A, *Bm;
+    double *s, *z, *bin, *X, *U, *win, *XL, *Zlog;
+    int *done, *iters, *flag, *hused, *ts, *nfin, *flags, *itlog;
+};
+hipError_t launch_sqp_loop_advance(const SqpAdvanceArgs& a, hipStream_t st);
 hipError_t launch_sqp_loop_prep(int batch, int nx, int n, int m, int nv, int shift, const double* s,
                                 const double* bin0, const double* Bx, double* bin, double* z,
                                 hipStream_t st);

@@ -278,6 +278,118 @@ __global__ void sqp_loop_u0_kernel(int batch, int nx, int n, const double* K, co
         for (int j = 0; j < n; ++j) Zlog[((int64_t)b * steps + t) * n + j] = z[(int64_t)b * n + j];
 }
 
+// ------------------------------------------------------------------------------------------
+// asynchronous learned-model loop (bqp_closed_loop_sqp_device, round 5): every instance runs at
+// its own closed-loop step ts[b].  After each SQP iteration of the batch, an instance whose SQP has
+// finished (done[b] = 1) and still has steps to go advances here, in one workgroup: u_0 = K s +
+// z_0 and the logs (sqp_loop_u0_kernel), the plant step (mg_plant_kernel), the data window
+// (lbmpc_window_kernel: the learned prediction with the window before the sample, then the
+// sample), and unless that was its last step the next step's constraints and warm start
+// (sqp_loop_prep_kernel) with its SQP state reset (done, iterations) - the same operations, in the
+// same order per instance, as the step-synchronous loop, whose SQP launches ran until the
+// slowest instance of the batch had converged while the others idled.  At its last step the
+// instance stays done and nfin counts it.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sqp_loop_advance_kernel(SqpAdvanceArgs a) {
+    const int b = blockIdx.x;
+    if (b >= a.batch || !a.done[b] || a.ts[b] >= a.steps) return;     // uniform per workgroup
+    const int t = a.ts[b], tid = threadIdx.x, lane = tid & 63;
+    const int nx = a.nx, n = a.n, m = a.m, steps = a.steps, q = a.q;
+    __shared__ double sh[8];
+    double* sb = a.s + (int64_t)b * nx;
+    double* zb = a.z + (int64_t)b * n;
+    // u_0 and the logs (sqp_loop_u0_kernel)
+    if (a.Zlog)
+        for (int j = tid; j < n; j += blockDim.x) a.Zlog[((int64_t)b * steps + t) * n + j] = zb[j];
+    if (tid == 0) {
+        double u = zb[0];
+        for (int j = 0; j < nx; ++j) u += a.K[j] * sb[j];
+        if (a.itlog) a.itlog[(int64_t)b * steps + t] = a.iters[b];
+        // plant step (mg_plant_kernel)
+        double x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = sb[i] + a.xeq[i];
+        const double uu = u + a.ueq[0];
+        if (a.plant == BQP_PLANT_MG_ODE23) mg_ode23(a.delta, x, uu);
+        else mg_rk4(a.delta, x, uu);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            sh[i] = x[i] - a.xeq[i];
+            a.X[((int64_t)b * (steps + 1) + t + 1) * 4 + i] = x[i];
+        }
+        a.U[(int64_t)b * steps + t] = uu;
+        if (a.flags) a.flags[(int64_t)b * steps + t] = a.flag[b];
+    }
+    __syncthreads();
+    // data window (lbmpc_window_kernel), wave 0
+    if (tid < 64) {
+        const double* xt = a.X + ((int64_t)b * (steps + 1) + t) * 4;
+        double dx[4], x1[4], nom[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { dx[i] = xt[i] - a.xeq[i]; x1[i] = xt[4 + i]; }
+        const double du = a.U[(int64_t)b * steps + t] - a.ueq[0];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double v = a.Bm[i] * du;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v += a.A[j * 4 + i] * dx[j];   // column-major A
+            nom[i] = v;
+        }
+        const double xi0 = dx[0], xi1 = dx[1], xi2 = du;
+        double* w = a.win + (int64_t)b * q * 8;
+        double sy0 = 0, sy1 = 0, sy2 = 0, sy3 = 0, sk = 0;
+        for (int i = lane; i < q; i += 64) {
+            const double* pt = w + (int64_t)i * 8;
+            const double e0 = pt[0] - xi0, e1 = pt[1] - xi1, e2 = pt[2] - xi2;
+            const double k = exp(-(e0 * e0 + e1 * e1 + e2 * e2) * a.hinv2);
+            sy0 += pt[3] * k; sy1 += pt[4] * k; sy2 += pt[5] * k; sy3 += pt[6] * k;
+            sk += k * pt[7];
+        }
+        sy0 = wave_sum64(sy0); sy1 = wave_sum64(sy1); sy2 = wave_sum64(sy2); sy3 = wave_sum64(sy3);
+        sk = wave_sum64(sk);
+        if (lane == 0) {
+            const double den = a.lam + sk;
+            const double g[4] = {sy0 / den, sy1 / den, sy2 / den, sy3 / den};
+            double* xl = a.XL + ((int64_t)b * (steps + 1) + t + 1) * 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xl[i] = a.xeq[i] + nom[i] + g[i];
+            double* pt = w + (int64_t)((t + 1) % q) * 8;
+            pt[0] = xi0; pt[1] = xi1; pt[2] = xi2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pt[3 + i] = (x1[i] - a.xeq[i]) - nom[i];
+            pt[7] = 1.0;
+        }
+    }
+    if (tid < nx) sb[tid] = sh[tid];      // the new measured deviation state
+    __syncthreads();
+    if (t + 1 < steps) {
+        // the next step's constraints and warm start (sqp_loop_prep_kernel)
+        double* bb = a.bin + (int64_t)b * m;
+        for (int r = tid; r < m; r += blockDim.x) {
+            double v = a.bin0[r];
+            for (int j = 0; j < nx; ++j) v += a.Bx[(int64_t)j * m + r] * sh[j];
+            bb[r] = v;
+        }
+        double v[4];
+        int cnt = 0;
+        for (int j = tid; j < n && cnt < 4; j += blockDim.x, ++cnt)
+            v[cnt] = !a.warm ? 0.0 : (j < a.nv ? ((j + 1 < a.nv) ? zb[j + 1] : 0.0) : zb[j]);
+        __syncthreads();
+        cnt = 0;
+        for (int j = tid; j < n && cnt < 4; j += blockDim.x, ++cnt) zb[j] = v[cnt];
+        if (tid == 0) { a.iters[b] = 0; a.hused[b] = 0; a.ts[b] = t + 1; a.done[b] = 0; }
+    } else if (tid == 0) {
+        a.ts[b] = steps;
+        atomicAdd(a.nfin, 1);
+    }
+}
+
+hipError_t launch_sqp_loop_advance(const SqpAdvanceArgs& a, hipStream_t st) {
+    if (a.n > 4 * 256 || a.nx > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sqp_loop_advance_kernel, dim3(a.batch), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_sqp_loop_prep(int batch, int nx, int n, int m, int nv, int shift, const double* s,
                                 const double* bin0, const double* Bx, double* bin, double* z,
                                 hipStream_t st) {

@@ -141,3 +141,26 @@ def test_indefinite_hessian_instance(mg):
     assert (r.exitflag == 1).all(), r.exitflag
     assert r.iterations.max() <= 20
     assert np.abs(r.U[0, :, 0] - f['U']).max() < 1e-6
+
+
+def test_async_loop_equals_step_synchronous(mg):
+    """bqp_closed_loop_sqp runs every instance at its own closed-loop step (round 5: the instances
+    whose SQP has finished advance while the others iterate).  Per instance it performs the same
+    operations in the same order as the step-synchronous loop (kept behind BQP_LB_TRACE for the
+    per-step diagnostics), so the trajectories, the learned predictions, the windows and the SQP
+    iteration counts are equal bit for bit on 24 perturbed instances over 6 steps"""
+    import os
+    import bqp
+    rng = np.random.default_rng(11)
+    X0 = X_INIT + rng.uniform(-1, 1, (24, 4)) * np.array([0.02, 0.02, 0.0, 0.0])
+    T = 6
+    ra = bqp.closed_loop_sqp(_mpc(mg), X0, T, learning=dict(q=100, mask=1), log_z=True)
+    os.environ['BQP_LB_TRACE'] = '1'
+    try:
+        rs = bqp.closed_loop_sqp(_mpc(mg), X0, T, learning=dict(q=100, mask=1), log_z=True)
+    finally:
+        del os.environ['BQP_LB_TRACE']
+    print('async vs synchronous loop: SQP iterations per step', ra.iterations.sum(axis=0).tolist(),
+          'max per step', ra.iterations.max(axis=0).tolist())
+    for k in ('X', 'U', 'XL', 'window', 'Z', 'iterations', 'exitflag'):
+        assert np.array_equal(ra[k], rs[k]), k

@@ -495,10 +495,25 @@ __device__ __forceinline__ void tile_of(int w, int u, int nbk, int& I, int& J) {
         dacc[id] += _t - dlast;                                            \
         dlast = _t;                                                        \
     } while (0)
+// the same without waiting for vector-memory loads in flight (LDS / scalar only): sections
+// that overlap a copy; chol_solve_w's stamps (optional pointers: only dense_ipm_kernel passes them)
+#define TSTN(acc_, last_, id)                                              \
+    do {                                                                   \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                 \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();        \
+        (acc_)[id] += _t - (last_);                                        \
+        (last_) = _t;                                                      \
+    } while (0)
+#define TSW_ARGS , unsigned long long* dacc = nullptr, unsigned long long* dlastp = nullptr
+#define TSW_PASS , dst_acc, &dst_last
+#define TSW(id) do { if (dacc) TSTN(dacc, *dlastp, id); } while (0)
 #else
 #define TST_ARGS
 #define TST_PASS
 #define TST(id) do { } while (0)
+#define TSW_ARGS
+#define TSW_PASS
+#define TSW(id) do { } while (0)
 #endif
 // the diagonal tile J in registers: symmetric from its lower triangle (the MFMA A'DA forms K(i, j)
 // and K(j, i) with different rounding; chol_2b read the lower triangle only - with both, the
@@ -612,18 +627,26 @@ __device__ void chol_solve_vec(const double* L, int n, double* xs, R& red) {
 }
 
 // one 16-entry block of the substitutions: the block's entries sit in one 16-lane row of a slot
-// (lane jl of the row holds entry e0 + jl); entry j = e0 + JJ is final when step JJ starts, reaches
-// the row by a DPP row broadcast (v_mov_b64_dpp row_newbcast), is scaled by its reciprocal pivot
-// and updates the row's later (forward) or earlier (backward) entries of the block
+// (lane jl of the row holds entry e0 + jl, as its unscaled residual r).  Entry J's value is
+// r_J d_J (d_J its reciprocal pivot); it updates the row's later (forward) or earlier (backward)
+// entries as r_i -= (L_iJ d_J) r_J with the coefficients L_iJ d_J formed before the chain (zero
+// outside the triangle, past n and off the block's row), so each of the 16 dependent steps is one
+// DPP row broadcast (v_mov_b64_dpp row_newbcast) and one FMA (round 4's step - broadcast of x and
+// of d, product, masked update, select - took ~110 cycles); the entries are scaled after it
+template <int JJ>
+__device__ __forceinline__ void tri_coef(double (&lcs)[16], const double (&lc)[16], double dv, int jl,
+                                         bool inrow, int nval, bool fwd) {
+    // the broadcast outside any lane condition (DPP under an exec mask reads 0 from inactive lanes)
+    const double db = rbc<JJ>(dv);
+    const bool ok = inrow && JJ < nval && (fwd ? jl > JJ : jl < JJ);
+    lcs[JJ] = (ok ? -lc[JJ] : 0.0) * db;
+    if constexpr (JJ + 1 < 16) tri_coef<JJ + 1>(lcs, lc, dv, jl, inrow, nval, fwd);
+}
 template <int JJ, bool FWD>
-__device__ __forceinline__ void tri_blk(double& xv, double dv, const double (&lc)[16], int jl, bool inrow,
-                                        int nval) {
+__device__ __forceinline__ void tri_blk(double& rv, const double (&lcs)[16]) {
     constexpr int J = FWD ? JJ : 15 - JJ;
-    const double xj = rbc<J>(xv) * rbc<J>(dv);
-    const bool ok = inrow && J < nval;       // entries past n (partial last block) never broadcast
-    if (ok && (FWD ? jl > J : jl < J)) xv -= lc[J] * xj;
-    if (ok && jl == J) xv = xj;
-    if constexpr (JJ + 1 < 16) tri_blk<JJ + 1, FWD>(xv, dv, lc, jl, inrow, nval);
+    rv = fma(lcs[J], rbc<J>(rv), rv);
+    if constexpr (JJ + 1 < 16) tri_blk<JJ + 1, FWD>(rv, lcs);
 }
 
 // solve L L' x = b in place (xs in LDS, n <= 256) by the first wave alone: lane l keeps entries
@@ -633,7 +656,7 @@ __device__ __forceinline__ void tri_blk(double& xv, double dv, const double (&lc
 // column-at-a-time form spent ~530 cycles per entry on its readlane / load / update chain).  L's
 // column j (forward) and row i (backward, the upper triangle block_cholesky leaves) are both at
 // [j n + e].  No workgroup barrier inside; every thread calls it.
-__device__ void chol_solve_w(const double* L, int n, double* xs) {
+__device__ __forceinline__ void chol_solve_w_body(const double* L, int n, double* xs TSW_ARGS) {
     if (threadIdx.x < 64 && n > 0) {
         const int l = threadIdx.x, jl = l & 15, rw = l >> 4;
         double xr[4], dr[4];
@@ -660,8 +683,13 @@ __device__ void chol_solve_w(const double* L, int n, double* xs) {
                 for (int jj = 0; jj < 16; ++jj) lc[jj] = L[(int64_t)min(e0 + jj, n - 1) * n + ec];
                 // the last block may be partial: steps past n are skipped (backward: they come
                 // first and would reach valid entries)
-                if (fwd) tri_blk<0, true>(xv, dv, lc, jl, inrow, n - e0);
-                else     tri_blk<0, false>(xv, dv, lc, jl, inrow, n - e0);
+                double lcs[16];
+                tri_coef<0>(lcs, lc, dv, jl, inrow, n - e0, fwd);
+                TSW(17);
+                if (fwd) tri_blk<0, true>(xv, lcs);
+                else     tri_blk<0, false>(xv, lcs);
+                if (inrow) xv *= dv;
+                TSW(18);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) if (q == qb) xr[q] = xv;
                 // publish the block, then the 16-column update of the entries after (forward) /
@@ -671,18 +699,20 @@ __device__ void chol_solve_w(const double* L, int n, double* xs) {
                 double xb[16];
 #pragma unroll
                 for (int jj = 0; jj < 16; ++jj) xb[jj] = (e0 + jj < n) ? xs[e0 + jj] : 0.0;
+                TSW(19);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int e = l + 64 * q;
                     const bool upd = e < n && (fwd ? e >= e0 + 16 : e < e0);
                     if (!upd) continue;
-                    double acc = 0.0;
+                    double ac4[4] = {0.0, 0.0, 0.0, 0.0};   // four chains of 4 FMAs, not one of 16
 #pragma unroll
                     for (int jj = 0; jj < 16; ++jj)
-                        acc = fma(L[(int64_t)min(e0 + jj, n - 1) * n + e], xb[jj], acc);
-                    xr[q] -= acc;
+                        ac4[jj & 3] = fma(L[(int64_t)min(e0 + jj, n - 1) * n + e], xb[jj], ac4[jj & 3]);
+                    xr[q] -= (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
                 }
                 wave_sync();
+                TSW(20);
             }
         }
 #pragma unroll
@@ -690,6 +720,10 @@ __device__ void chol_solve_w(const double* L, int n, double* xs) {
     }
     __syncthreads();
 }
+// the called form (factor / vector in global memory or generic pointers); dense_ipm_kernel's
+// factor in LDS inlines the body, so that L and xs are ds_* accesses (the call made them flat
+// loads, ~4 solve-phase round trips slower per block)
+__device__ void chol_solve_w(const double* L, int n, double* xs) { chol_solve_w_body(L, n, xs); }
 
 // sequential per-thread solve of L L' x = b for column vectors stored with stride (one per thread)
 __device__ void chol_solve_col(const double* L, int n, double* x) {
@@ -916,8 +950,8 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
 // diagnostic build only (tools/gpu_r03_dstamps.sh): s_memtime cycles per phase of instance 0,
 // printed by thread 0 at exit; never linked into the product library
 #define DST_DECL                                                           \
-    unsigned long long dst_last = __builtin_amdgcn_s_memtime(), dst_acc[17]; \
-    _Pragma("unroll") for (int i_ = 0; i_ < 17; ++i_) dst_acc[i_] = 0
+    unsigned long long dst_last = __builtin_amdgcn_s_memtime(), dst_acc[25]; \
+    _Pragma("unroll") for (int i_ = 0; i_ < 25; ++i_) dst_acc[i_] = 0
 #define DST(id)                                                            \
     do {                                                                   \
         __builtin_amdgcn_s_waitcnt(0);                                     \
@@ -925,9 +959,11 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         dst_acc[id] += _t - dst_last;                                      \
         dst_last = _t;                                                     \
     } while (0)
+#define DSTN(id) TSTN(dst_acc, dst_last, id)
 #else
 #define DST_DECL do { } while (0)
 #define DST(id) do { } while (0)
+#define DSTN(id) do { } while (0)
 #endif
 
 // dense_ipm_kernel LDS: the A row tiles (TILE rows, stride ts = 32 ceil(n/32) + 1 doubles - odd
@@ -1247,20 +1283,29 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 // two column-major buffers: tile t + 1 is copied by global_load_lds (no VGPR
                 // staging) while the MFMAs consume tile t, one barrier per tile.  One 4-byte
                 // load per lane moves one column's 32 rows (256 B) - rows past m read row m - 1,
-                // whose weight slot is 0 - so each column lands at its own padded offset.
+                // whose weight slot is 0 - so each column lands at its own padded offset.  (The
+                // 16-byte form - four columns per wave-instruction, row pairs rotated per column
+                // against bank conflicts - issued a quarter of the copies and took the same time
+                // per solve: the tile's MFMA chain, not the copy issue, sets the pace.)
                 const int ntile = (m + TILE - 1) / TILE;
                 const int rowl = lane >> 1;
                 // The copy is issued from inline asm (M0 = the column's LDS byte address): with
                 // the builtin, hipcc cannot tell the two buffers apart and waited for the copy of
                 // tile t + 1 before the first LDS read of tile t.  Its completion is waited for
                 // explicitly (vmcnt(0)) before the barrier that hands the buffer over.
+                // The column loop runs on scalar registers (wave index, column count and LDS
+                // address made wave-uniform: a per-lane loop counter put an exec-mask update and
+                // two readfirstlanes on every copy, ~3k cycles per tile)
+                const int wvu = __builtin_amdgcn_readfirstlane(wv);
+                const int64_t cstr = (int64_t)(DT / 64) * m * sizeof(double);
                 auto issue = [&](int t, double* buf) {
-                    const int ncol = min(n, 16 * (((int)tbound(t) + 15) / 16));
-                    const char* src = (const char*)(A + min(t * TILE + rowl, m - 1)) + 4 * (lane & 1);
-                    for (int j = wv; j < ncol; j += DT / 64) {
-                        const char* g = src + (int64_t)j * m * sizeof(double);
-                        const unsigned ldsa = __builtin_amdgcn_readfirstlane(
-                            (unsigned)(uintptr_t)(__attribute__((address_space(3))) double*)(buf + DQ_GB * j));
+                    const int ncol = __builtin_amdgcn_readfirstlane(min(n, 16 * (((int)tbound(t) + 15) / 16)));
+                    const char* g = (const char*)(A + min(t * TILE + rowl, m - 1)) + 4 * (lane & 1) +
+                                    (int64_t)wvu * m * sizeof(double);
+                    unsigned ldsa = __builtin_amdgcn_readfirstlane(
+                        (unsigned)(uintptr_t)(__attribute__((address_space(3))) double*)(buf)) +
+                        (unsigned)(wvu * DQ_GB * sizeof(double));
+                    for (int j = wvu; j < ncol; j += DT / 64, g += cstr, ldsa += (DT / 64) * DQ_GB * sizeof(double)) {
                         unsigned keep;
                         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                                      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -1290,6 +1335,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                         la = lA[rd1]; ta = tA[rd1];
                         issue(t + 1, nxt);
                     }
+                    DSTN(21);
                     const double thi = tbound(t);
                     // k-step s of lane group k4 takes row 8 k4 + s: each lane's 8 rows of a column
                     // are contiguous, read as four ds_read_b128 (rows past the tile hold finite
@@ -1318,9 +1364,12 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                                 acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s4], drv[s4] * aj[s4], acc[u], 0, 0, 0);
                         }
                     }
+                    DSTN(22);
                     if (more && tid < TILE) nxt[DQ_GB * n + tid] = tid < rows1 ? la / ta : 0.0;
                     copy_wait();
+                    DSTN(23);
                     __syncthreads();
+                    DSTN(24);
                 }
             }
             for (int r0 = 0; r0 < (gl ? 0 : m); r0 += TILE) {
@@ -1483,7 +1532,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         __syncthreads();
         for (int j = tid; j < n; j += DT) xs[j] = -q[j];
         __syncthreads();
-        chol_solve_w(K, n, xs);
+        DST(8);
+        if constexpr (KL) chol_solve_w_body(K, n, xs TSW_PASS);
+        else chol_solve_w(K, n, xs);
         DST(8);
         for (int j = tid; j < n; j += DT) w[j] = xs[j];
         __syncthreads();
@@ -1684,10 +1735,12 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     if (inst == 0 && tid == 0)
         printf("DSTAMPS it %d rows %llu atw_res %llu res_rest %llu ada %llu chol %llu solve_pre %llu "
                "atw_sol %llu trsv %llu sol_post %llu step %llu upd %llu other %llu | chol: D %llu Dwait %llu "
-               "P %llu Pwait %llu U %llu\n", it, dst_acc[0],
+               "P %llu Pwait %llu U %llu | trsv: pre+lc %llu chain %llu publish %llu update %llu | ada: "
+               "issue %llu mfma %llu copywait %llu barrier %llu\n", it, dst_acc[0],
                dst_acc[10], dst_acc[11], dst_acc[1], dst_acc[2], dst_acc[3], dst_acc[7], dst_acc[8],
                dst_acc[9], dst_acc[4], dst_acc[5], dst_acc[6], dst_acc[12], dst_acc[13], dst_acc[14],
-               dst_acc[15], dst_acc[16]);
+               dst_acc[15], dst_acc[16], dst_acc[17], dst_acc[18], dst_acc[19], dst_acc[20],
+               dst_acc[21], dst_acc[22], dst_acc[23], dst_acc[24]);
 #endif
     // ---------------------------------------------------------------- outputs
     double fv = 0.0;

@@ -8,6 +8,7 @@
 set -o pipefail
 TAG=${1:-r05_prof}; shift
 CFGS=${@:-C2 C3 C4 C5}
+[ "$CFGS" = "none" ] && CFGS=""   # CLL only
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/$TAG

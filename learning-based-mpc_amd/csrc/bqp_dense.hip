@@ -975,7 +975,8 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
                      // 16-byte aligned columns, 16 lanes' b128 reads on distinct banks)
 __host__ __device__ inline int dense_ts(int n) { return 32 * ((n + 31) / 32) + 1; }
 // one A'DA buffer: column-major 32-row tile, columns 0 .. n-1 of A and column n the row weights
-__host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 1); }
+// (column n: the row weights d_r; column n + 1: the predictor's A' weights, below)
+__host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 2); }
 // the two-buffer A'DA (global_load_lds of tile t + 1 in flight while the MFMAs run on tile t)
 // when both buffers and the factor fit in LDS; otherwise the single row-major tile
 // (every budget below counts the reduction scratch and the tile bounds, DQ_TAIL doubles at the end)
@@ -1302,8 +1303,14 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         DST(11);
     };
 
+    // (A' w)_tid of the predictor's right-hand side, w_r = (lam_r riA_r - t_r lam_r) / t_r, formed
+    // inside the A'DA pipeline from the row tiles it already has in LDS (aq_ok): one pass over A
+    // per iteration less (the predictor's atw, ~0.5M of ~9M cycles per n = 101 solve)
+    double aq_pre = 0.0;
+    bool aq_ok = false;
     // ---------------------------------------------------------------- factorisation
     auto factor = [&]() __attribute__((always_inline)) -> bool {   // inlined: a call spilled (callee budget)
+        aq_ok = false;
         // K = H + sum_r A_r' D_r A_r (+ bound diagonal): lower triangle (n <= 128) or both
         const int ne = n * (n + 1) / 2;
         double dmx = 0.0;                 // largest diagonal entry (pivot floor scale)
@@ -1364,11 +1371,16 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 auto copy_wait = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
                 double* gb0 = dlds;
                 double* gb1 = dlds + dense_gbuf(n);
+                double aw = 0.0;
                 {
                     const int rd0 = min(tid, min(TILE, m) - 1);
-                    const double la = lA[rd0], ta = tA[rd0];
+                    const double la = lA[rd0], ta = tA[rd0], ri = riA[rd0];
                     issue(0, gb0);
-                    if (tid < TILE) gb0[DQ_GB * n + tid] = tid < min(TILE, m) ? la / ta : 0.0;
+                    if (tid < TILE) {
+                        const bool in = tid < min(TILE, m);
+                        gb0[DQ_GB * n + tid] = in ? la / ta : 0.0;
+                        gb0[DQ_GB * (n + 1) + tid] = in ? (la * ri - ta * la) / ta : 0.0;
+                    }
                 }
                 copy_wait();
                 __syncthreads();
@@ -1377,11 +1389,11 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     double* nxt = (t & 1) ? gb0 : gb1;
                     const int r0 = t * TILE;
                     const bool more = t + 1 < ntile;
-                    double la = 1.0, ta = 1.0;
+                    double la = 1.0, ta = 1.0, ri = 0.0;
                     const int rows1 = more ? min(TILE, m - r0 - TILE) : 0;
                     if (more) {
                         const int rd1 = r0 + TILE + min(tid, rows1 - 1);
-                        la = lA[rd1]; ta = tA[rd1];
+                        la = lA[rd1]; ta = tA[rd1]; ri = riA[rd1];
                         issue(t + 1, nxt);
                     }
                     DSTN(21);
@@ -1413,13 +1425,36 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                                 acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[s4], drv[s4] * aj[s4], acc[u], 0, 0, 0);
                         }
                     }
+                    // the predictor's A' w on the columns this tile reaches: thread tid takes
+                    // column tid % 128 over the tile's rows 16 (tid / 128) .. + 15 (all four waves)
+                    if ((tid & 127) < min(n, 16 * (((int)thi + 15) / 16))) {
+                        const double2* pc = reinterpret_cast<const double2*>(cur + DQ_GB * (tid & 127) + 16 * (tid >> 7));
+                        const double2* pw = reinterpret_cast<const double2*>(cur + DQ_GB * (n + 1) + 16 * (tid >> 7));
+                        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                        for (int h = 0; h < TILE / 4; ++h) {
+                            const double2 av = pc[h], wv2 = pw[h];
+                            s0 = fma(av.x, wv2.x, s0);
+                            s1 = fma(av.y, wv2.y, s1);
+                        }
+                        aw += s0 + s1;
+                    }
                     DSTN(22);
-                    if (more && tid < TILE) nxt[DQ_GB * n + tid] = tid < rows1 ? la / ta : 0.0;
+                    if (more && tid < TILE) {
+                        nxt[DQ_GB * n + tid] = tid < rows1 ? la / ta : 0.0;
+                        nxt[DQ_GB * (n + 1) + tid] = tid < rows1 ? (la * ri - ta * la) / ta : 0.0;
+                    }
                     copy_wait();
                     DSTN(23);
                     __syncthreads();
                     DSTN(24);
                 }
+                // the two row halves of each column (the loop's last barrier has retired gb0)
+                if (tid >= 128 && (tid & 127) < n) gb0[tid & 127] = aw;
+                __syncthreads();
+                aq_pre = tid < n ? aw + gb0[tid] : 0.0;
+                aq_ok = true;
+                __syncthreads();
             }
             for (int r0 = 0; r0 < (gl ? 0 : m); r0 += TILE) {
                 const int rows = min(TILE, m - r0);
@@ -1570,7 +1605,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     auto solve = [&]() {
         // q = rd + A'((lam riA - rcA)/tA) + bound terms ; w = -K^{-1} q
         DST(3);
-        const double aq = atw([&](int r) { return (lA[r] * riA[r] - rcA[r]) / tA[r]; });
+        // the first solve after a factorisation (rc = t lam) takes the A' w formed with A'DA
+        const double aq = aq_ok ? aq_pre : atw([&](int r) { return (lA[r] * riA[r] - rcA[r]) / tA[r]; });
+        aq_ok = false;
         DST(7);
         for (int j = tid; j < n; j += DT) {
             double v = rd[j] + aq;
@@ -1961,6 +1998,32 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
         wave_sync();
     };
 
+    // the residuals after a step of length al (as dense_ipm_kernel's scaled_residuals): (1 - al)
+    // times the old ones, the complementarity and max |z| fresh, gscale from the last exact values
+    auto scaled_residuals = [&](double s, double& stat, double& fin, double& csum, double& zmax,
+                                double& cmax) __attribute__((always_inline)) {
+        double fe = 0.0, cs = 0.0, st = 0.0, zm = 0.0, cm = 0.0;
+        for (int r = lane; r < m; r += 64) {
+            const double v = s * riA[r];
+            riA[r] = v;
+            fe = fmax(fe, fabs(v));
+            cs = fma(tA[r], lA[r], cs);
+            cm = fmax(cm, tA[r] * lA[r]);
+        }
+        if (lane < n) {
+            const int j = lane;
+            rd[j] *= s;
+            riB[j] *= s; riB[n + j] *= s;
+            if (upj) { cs += tB[j] * lB[j]; cm = fmax(cm, tB[j] * lB[j]); }
+            if (loj) { cs += tB[n + j] * lB[n + j]; cm = fmax(cm, tB[n + j] * lB[n + j]); }
+            fe = fmax(fe, fmax(fabs(riB[j]), fabs(riB[n + j])));
+            st = fabs(rd[j]);
+            zm = fabs(z[j]);
+        }
+        stat = wmax(st); fin = wmax(fe); csum = wsum(cs); zmax = wmax(zm); cmax = wmax(cm);
+        wave_sync();
+    };
+
     // Cholesky in registers: lane r < n holds row r of the lower factor (Lr[c], c <= r), its
     // reciprocal pivot (dinv) and, after the factorisation, column r of it (Lc[i] = L(i, r),
     // i > r, for the backward substitution).  Right-looking over the columns j: the pivot comes
@@ -2206,12 +2269,22 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     int it = 0;
     double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
+        double al_last = -1.0;            // the last step length (< 0: evaluate the residuals exactly)
         for (it = 0; it <= a.max_iter; ++it) {
-            residuals(stat, fin, csum, gscale, zmax, cmax);
-            const double feas = fin;
+            if (al_last < 0.0) residuals(stat, fin, csum, gscale, zmax, cmax);
+            else scaled_residuals(1.0 - al_last, stat, fin, csum, zmax, cmax);
+            double feas = fin;
             mu = csum * minv;
-            if (stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
-                mu <= a.tol_comp && cmax <= DQ_CMAX_K * a.tol_comp) { flag = 1; break; }
+            auto converged = [&] {
+                return stat <= a.tol_stat * (1.0 + gscale) && feas <= a.tol_feas * (1.0 + bscale) &&
+                       mu <= a.tol_comp && cmax <= DQ_CMAX_K * a.tol_comp;
+            };
+            if (converged() && al_last >= 0.0) {   // confirm on exact residuals
+                residuals(stat, fin, csum, gscale, zmax, cmax);
+                feas = fin;
+                mu = csum * minv;
+            }
+            if (converged()) { flag = 1; break; }
             if (!(isfinite(stat) && isfinite(feas) && isfinite(mu))) { flag = -8; break; }
             if (zmax > zbig) { flag = -3; break; }
             if (mu > DQ_MU_BLOWUP * mu_min && feas > DQ_FEAS_GUARD * (1.0 + bscale)) { flag = -2; break; }
@@ -2247,6 +2320,7 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
             }
             for (int r = lane; r < m; r += 64) { tA[r] += al * dtA[r]; lA[r] += al * dlA[r]; }
             wave_sync();
+            al_last = al;
         }
     }
     const int pm = pol_mode(a, inst);

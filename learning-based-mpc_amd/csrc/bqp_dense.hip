@@ -698,7 +698,10 @@ __device__ __forceinline__ void chol_solve_w_body(const double* L, int n, double
                 wave_sync();
                 double xb[16];
 #pragma unroll
-                for (int jj = 0; jj < 16; ++jj) xb[jj] = (e0 + jj < n) ? xs[e0 + jj] : 0.0;
+                for (int jj = 0; jj < 16; ++jj) {   // unconditional loads (clamped), then the select
+                    const double v = xs[min(e0 + jj, n - 1)];
+                    xb[jj] = (e0 + jj < n) ? v : 0.0;
+                }
                 TSW(19);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {

@@ -499,9 +499,12 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
             const double sq = sqrt(d);
             for (int i = j + 1 + tid; i < n; i += 256) Kx[j * n + i] /= sq;
             __syncthreads();
-            for (int c = j + 1; c < n; ++c) {
+            // trailing update over a 16 x 16 thread grid (ty: columns c, tx: rows i >= c) - each
+            // entry gets the same update as before, in the same order; one thread per column c
+            // ran the c loop serially (~5k cycles per pivot, ~0.5M per test at n = 101)
+            for (int c = j + 1 + ty; c < n; c += 16) {
                 const double lc = Kx[j * n + c];
-                for (int i = c + tid; i < n; i += 256) Kx[c * n + i] -= Kx[j * n + i] * lc;
+                for (int i = c + tx; i < n; i += 16) Kx[c * n + i] -= Kx[j * n + i] * lc;
             }
             __syncthreads();
         }

@@ -742,21 +742,52 @@ def loop_workload(cfg, batch, rank, world):
 
 
 class LoopRunner:
-    """One rank's closed loops on its GPU (bqp.closed_loop / bqp.closed_loop_sqp)."""
+    """One rank's closed loops on its GPU (bqp.closed_loop / bqp.closed_loop_sqp).  With
+    streams > 1 the rank's instances are split into that many contiguous groups, each run by its
+    own host thread on its own handle (HIP stream, workspace): the groups' launches overlap, so the
+    CUs that one group's latency-bound kernels leave idle (the learned rollouts use one wave per
+    instance) run the other group's dense sub-problems.  The instances are independent, so every
+    group's trajectories are the ones the whole batch in one call gives."""
 
-    def __init__(self, cfg, wl, local):
+    def __init__(self, cfg, wl, local, streams=1):
         import bqp
         self.bqp, self.cfg, self.wl = bqp, cfg, wl
-        self.h = bqp.Handle(local)
+        self.streams = max(1, min(int(streams), len(wl['X0'])))
+        self.hs = [bqp.Handle(local) for _ in range(self.streams)]
+        self.h = self.hs[0]
 
-    def run(self, steps):
+    def _one(self, X0, steps, h):
         b = self.bqp
         if self.cfg == 'CL':
-            r = b.closed_loop(self.wl['mpc'], self.wl['X0'], steps, handle=self.h)
-        else:
-            r = b.closed_loop_sqp(self.wl['mpc'], self.wl['X0'], steps,
-                                  learning=dict(q=100, mask=1), handle=self.h)
-        return r
+            return b.closed_loop(self.wl['mpc'], X0, steps, handle=h)
+        return b.closed_loop_sqp(self.wl['mpc'], X0, steps, learning=dict(q=100, mask=1), handle=h)
+
+    def run(self, steps):
+        X0 = self.wl['X0']
+        if self.streams == 1:
+            return self._one(X0, steps, self.h)
+        import threading
+        parts = np.array_split(np.arange(len(X0)), self.streams)
+        res = [None] * self.streams
+        err = []
+
+        def work(i):
+            try:
+                res[i] = self._one(X0[parts[i]], steps, self.hs[i])
+            except Exception as e:               # re-raised on the main thread
+                err.append(e)
+        th = [threading.Thread(target=work, args=(i,)) for i in range(self.streams)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise err[0]
+        out = dict(res[0])
+        for k, v in res[0].items():
+            if isinstance(v, np.ndarray):
+                out[k] = np.concatenate([r[k] for r in res])
+        return out
 
     def kernel_ms(self):
         return self.h.kernel_ms()[0]
@@ -816,7 +847,7 @@ def bench_loop(args):
         dev = torch.device('cuda', local)
     wl = loop_workload(args.config, args.batch, rank, world)
     B = wl['B']
-    runner = StubLoop(args.config, wl) if args.dry_run else LoopRunner(args.config, wl, local)
+    runner = StubLoop(args.config, wl) if args.dry_run else LoopRunner(args.config, wl, local, args.streams)
     if args.warmup > 0:
         runner.run(1)                                   # module load, workspaces
     if not args.dry_run:
@@ -891,7 +922,8 @@ def bench_loop(args):
                     scaling='weak', vs_baseline=None, dtype='f64',
                     data=wl['data'] + (' [CPU dry run: stub loop, gloo]' if args.dry_run else ''),
                     config={'workload': wl['text'] + ', %d steps' % args.steps, 'batch_per_gpu': B,
-                            'horizon': 100, 'parallelism': 'dp%d' % world},
+                            'horizon': 100, 'parallelism': 'dp%d' % world,
+                            'streams': 1 if args.dry_run else runner.streams},
                     roofline=roof, kernel_ms=None if kms is None else round(kms, 4),
                     cpu_baseline=cpu, check=check)
         print(json.dumps(line), flush=True)

@@ -566,17 +566,18 @@ def main():
             # steps overlap on --streams streams: the device's rate over the timed region is the
             # per-step flops over the time per step
             achieved_pipe = flops_launch / (ms_per_step * 1e-3) / 1e12
-            # achieved / frac: the device's rate over the timed region (flops per step over the
-            # time per step: with the steps overlapping on config.streams streams a launch's own
-            # duration counts the time it shares the CUs with the other stream's launch); the
-            # per-launch figure (flops per launch / mean launch duration) beside it
-            roof = {'bound': 'fp64_valu', 'achieved': round(achieved_pipe, 4),
+            # achieved / frac: flops per launch / the mean launch duration over the timed region
+            # (hipEvents on each launch's stream; with the steps overlapping on config.streams
+            # streams a launch's duration includes the time it shares the CUs with the other
+            # stream's launch); beside it the device rate over the timed region (flops per step /
+            # ms per step) and the launch alone
+            roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                    'frac': round(achieved_pipe / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
+                    'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
                     'kernel_ms': round(kernel_ms, 4), 'flops_per_launch': flops_launch,
                     'kernel_ms_alone': round(kernel_ms_alone, 4),
-                    'achieved_per_launch': round(achieved, 4),
-                    'frac_per_launch': round(achieved / FP64_PEAK_TFLOPS, 5),
+                    'achieved_per_step': round(achieved_pipe, 4),
+                    'frac_per_step': round(achieved_pipe / FP64_PEAK_TFLOPS, 5),
                     'frac_per_launch_alone': round(flops_launch / (kernel_ms_alone * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 5),
                     'traffic_source': traffic_src,
                     'note': 'bound: FP64 VALU issue plus the latency of the sequential N-stage '
@@ -585,11 +586,11 @@ def main():
                             'stage blocks, DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
                             'passes of this config (traffic_source); achieved = flops per launch / '
-                            'ms_per_step, the device rate over the timed region (the steps overlap '
-                            'on config.streams streams); kernel_ms = mean launch duration over the '
-                            'timed steps (hipEvents on each launch\'s stream, a launch sharing the '
-                            'CUs with the other stream\'s), kernel_ms_alone = one launch by itself '
-                            '(host-synchronised pass), frac_per_launch(_alone) from those'}
+                            'kernel_ms, the mean launch duration over the timed steps (hipEvents on '
+                            'each launch\'s stream; the steps overlap on config.streams streams, so a '
+                            'launch shares the CUs with the other stream\'s); achieved_per_step = '
+                            'flops per launch / ms_per_step, the device rate over the timed region; '
+                            'kernel_ms_alone = one launch by itself (host-synchronised pass)'}
             st_json = os.path.join(ROOT, 'profiles', 'stamps_%s.json' % args.config)
             if args.precision == 'fp64' and os.path.exists(st_json):
                 # latency roof: at batch 1024 one instance runs per SIMD, so the

@@ -149,6 +149,28 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double h
     }
 }
 
+#ifdef BQP_RSTAMPS
+// diagnostic build only: s_memtime cycles per phase of the learned rollout, printed for instance 0
+#define RST_DECL unsigned long long rst_last = __builtin_amdgcn_s_memtime(), rst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define RST(id)                                                            \
+    do {                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                     \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();        \
+        rst_acc[id] += _t - rst_last;                                      \
+        rst_last = _t;                                                     \
+    } while (0)
+#define RST_PRINT(tag)                                                     \
+    do {                                                                   \
+        if (b == 0 && t == 0 && lane == 0)                                 \
+            printf("RSTAMPS %s gn %d pre %llu nw %llu post %llu term %llu costate %llu pass2 %llu\n", tag, gn, \
+                   rst_acc[0], rst_acc[1], rst_acc[2], rst_acc[3], rst_acc[4], rst_acc[5]); \
+    } while (0)
+#else
+#define RST_DECL do { } while (0)
+#define RST(id) do { } while (0)
+#define RST_PRINT(tag) do { } while (0)
+#endif
+
 __device__ __forceinline__ void load_window(double* D, const double* src, int len, int lane) {
     for (int i = lane; i < len; i += LB_WAVE) D[i] = src[i];
     wave_sync();
@@ -210,12 +232,30 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     auto zv = [&](int j) __attribute__((always_inline)) -> double {
         return gn ? z[j] : z[j] + alpha * dz[j];
     };
-    // column-major small matrices
-    auto Am = [&](int i, int j) __attribute__((always_inline)) { return a.A[j * NX + i]; };
-    auto Bm = [&](int i, int j) __attribute__((always_inline)) { return a.B[j * NX + i]; };
-    auto Km = [&](int i, int j) __attribute__((always_inline)) { return a.K[j * NU + i]; };
-    auto LAM = [&](int i, int j) __attribute__((always_inline)) { return a.LAM[j * NX + i]; };
-    auto PSI = [&](int i, int j) __attribute__((always_inline)) { return a.PSI[j * NU + i]; };
+    // column-major small matrices, copied to LDS once: read from global memory inside the stage
+    // loop they were reloaded after every Jacobian-row store (the compiler cannot rule out
+    // aliasing), a chain of dependent loads per stage (~60 % of the Hessian rollout's cycles in
+    // its stamps)
+    constexpr int OA = 0, OB = OA + NX * NX, OK = OB + NX * NU, OL = OK + NU * NX, OP = OL + NX * NP,
+                  OQ = OP + NU * NP, OR = OQ + NX * NX, OEND = OR + NU * NU;
+    __shared__ double cst[OEND];
+    for (int i = lane; i < OEND; i += LB_WAVE) {
+        double v;
+        if (i < OB) v = a.A[i - OA];
+        else if (i < OK) v = a.B[i - OB];
+        else if (i < OL) v = a.K[i - OK];
+        else if (i < OP) v = a.LAM[i - OL];
+        else if (i < OQ) v = a.PSI[i - OP];
+        else if (i < OR) v = a.Lq[i - OQ];
+        else v = a.Lr[i - OR];
+        cst[i] = v;
+    }
+    wave_sync();
+    auto Am = [&](int i, int j) __attribute__((always_inline)) { return cst[OA + j * NX + i]; };
+    auto Bm = [&](int i, int j) __attribute__((always_inline)) { return cst[OB + j * NX + i]; };
+    auto Km = [&](int i, int j) __attribute__((always_inline)) { return cst[OK + j * NU + i]; };
+    auto LAM = [&](int i, int j) __attribute__((always_inline)) { return cst[OL + j * NX + i]; };
+    auto PSI = [&](int i, int j) __attribute__((always_inline)) { return cst[OP + j * NU + i]; };
     double th[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) th[p] = zv(N * NU + p);
@@ -269,6 +309,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         }
         row += dim;
     };
+    RST_DECL;
     for (int k = 0; k < N; ++k) {
         const double vk = zv(k);
         double u = vk, un = vk;
@@ -289,18 +330,20 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
 #pragma unroll
         for (int i = 0; i < NX; ++i) gx[i] = 0.0;
         if (k < a.n_run) {
-            residual(a.Lq, NX, x, LAM, [&](int c, int i) { return SL[c][i]; }, hess ? gx : nullptr);
+            residual(cst + OQ, NX, x, LAM, [&](int c, int i) { return SL[c][i]; }, hess ? gx : nullptr);
             double gu = 0.0;
-            residual(a.Lr, NU, &u, PSI, [&](int c, int i) { return UL[c]; }, hess ? &gu : nullptr);
+            residual(cst + OR, NU, &u, PSI, [&](int c, int i) { return UL[c]; }, hess ? &gu : nullptr);
 #pragma unroll
             for (int i = 0; i < NX; ++i) gx[i] += Km(0, i) * gu;    // u = K x + v
         }
         // learned step
+        RST(0);
         const double xi[3] = {x[0], x[1], u};
         double g[4], dg[4][3], d2g[4][6];
         if constexpr (HESS) nw_eval<true, true>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane, d2g);
         else if (gn) nw_eval<true>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
         else nw_eval<false>(D, a.q, a.wrows, a.hinv2, a.lam_nw, xi, g, dg, lane);
+        RST(1);
         if (hess && lane == 0) {
             double* st = SS + (int64_t)k * LB_SS;
 #pragma unroll
@@ -340,6 +383,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) { x[i] = x1[i]; xn[i] = xn1[i]; }
+        RST(2);
     }
     // terminal P on x_N (learned or nominal), T on (LAMBDA theta - xs)
 #pragma unroll
@@ -360,7 +404,8 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         if (gn) a.cost0[b] = J;
         else a.costT[(int64_t)b * nt + t] = J;
     }
-    if constexpr (!HESS) return;
+    RST(3);
+    if constexpr (!HESS) { RST_PRINT("rollout"); return; }
     wave_sync();
     // ---- costate pass (uniform on every lane): W_k into the stage store ----
     double pc[NX];
@@ -398,6 +443,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         for (int i = 0; i < NX; ++i) pc[i] = pn[i];
     }
     wave_sync();
+    RST(4);
     // ---- second sensitivity pass: rows Xi_k and W_k Xi_k ----
     double* J2 = a.Jr2 + (int64_t)b * 3 * N * n;
     double* T2 = a.Tr2 + (int64_t)b * 3 * N * n;
@@ -434,6 +480,8 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
             for (int i = 0; i < NX; ++i) SL[c][i] = sl[i];
         }
     }
+    RST(5);
+    RST_PRINT("rollout");
 }
 
 // ------------------------------------------------------------------------------------------

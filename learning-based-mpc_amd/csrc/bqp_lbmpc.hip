@@ -229,9 +229,12 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     const double alpha = gn ? 0.0 : ldexp(1.0, -t);
     const double* z = a.z + (int64_t)b * n;
     const double* dz = a.d + (int64_t)b * n;
-    auto zv = [&](int j) __attribute__((always_inline)) -> double {
-        return gn ? z[j] : z[j] + alpha * dz[j];
-    };
+    // the trial point z + alpha d in LDS (n <= 4 x 64): one global load per stage put a memory
+    // round trip at the head of every stage's chain
+    __shared__ double zsh[LB_WAVE * LB_CPL];
+    for (int j = lane; j < n; j += LB_WAVE) zsh[j] = gn ? z[j] : z[j] + alpha * dz[j];
+    wave_sync();
+    auto zv = [&](int j) __attribute__((always_inline)) -> double { return zsh[j]; };
     // column-major small matrices, copied to LDS once: read from global memory inside the stage
     // loop they were reloaded after every Jacobian-row store (the compiler cannot rule out
     // aliasing), a chain of dependent loads per stage (~60 % of the Hessian rollout's cycles in
@@ -779,7 +782,8 @@ hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st) {
     const int grid = a.batch * (gn ? 1 : a.ntrial);
     const size_t lds = lbmpc_rollout_lds(a, gn);
     auto k = (gn && a.hess) ? lbmpc_rollout_kernel<4, 1, 1, true> : lbmpc_rollout_kernel<4, 1, 1, false>;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    // z columns: LB_CPL per lane (the sensitivities and the LDS trial point); static LDS ~2.4 KB
+    if (a.n > LB_WAVE * LB_CPL || lds > 156 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -307,6 +307,7 @@ class GpuSolver:
         self.lib = bqp.load()
         self.opt = _lib.options(precision={'fp64': 0, 'fp32': 1, 'mixed': 2}[precision], polish=polish)
         self.S = max(1, int(streams))
+        self.active = self.S                 # streams the steps rotate over (<= S)
         self.sets = []
         for i in range(self.S):
             self.sets.append(dict(
@@ -323,11 +324,11 @@ class GpuSolver:
 
     def next_stream(self):
         """the stream the next step() launches on"""
-        return self.sets[self.k % self.S]['stream']
+        return self.sets[self.k % self.active]['stream']
 
     def step(self, with_out=False):
         P = self._lib.dptr
-        i = 0 if with_out else self.k % self.S
+        i = 0 if with_out else self.k % self.active
         self.k += 0 if with_out else 1
         st = self.sets[i]
         rc = self.lib.bqp_solve_ocp_batched_device(
@@ -405,11 +406,17 @@ def main():
                     help='interior-point iterates only (bqp_options.polish = -1)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
-    ap.add_argument('--streams', type=int, default=2,
+    ap.add_argument('--streams', type=int, default=None,
                     help='structured configs: consecutive steps on this many HIP streams in turn '
-                         '(a launch lasts as long as its slowest instance; the next step\'s '
-                         'workgroups start on the CUs it has left)')
+                         '(independent plant groups: a launch lasts as long as its slowest '
+                         'instance, and the other group\'s workgroups start on the CUs it has '
+                         'left).  Default 1: one batch per control step, the BASELINE config; the '
+                         'two-group rate is reported in check.value_two_groups.  CL / CLL: the '
+                         'rank\'s instances in this many concurrent groups (default 2; the same '
+                         'instances, split)')
     args = ap.parse_args()
+    if args.streams is None:
+        args.streams = 2 if args.config in ('CL', 'CLL') else 1
     if args.config in ('C1', 'C2H', 'C2D'):
         return bench_aux(args)
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -435,8 +442,12 @@ def main():
     wl = workload(args.config, args.batch, rank, world)
     prob, B = wl['prob'], wl['X'].shape[0]
     N, nx, nu, npar, mp = prob.N, prob.nx, prob.nu, prob.np, prob.mp
+    # two stream sets at least: the line's value is the --streams rate, check.value_two_groups the
+    # rate of two independent plant groups (consecutive steps on two streams)
     solver = StubSolver(wl) if args.dry_run else GpuSolver(wl, local, args.precision, not args.no_polish,
-                                                           args.streams)
+                                                           max(2, args.streams))
+    if not args.dry_run:
+        solver.active = max(1, args.streams)
 
     for _ in range(args.warmup):
         solver.step()
@@ -466,6 +477,25 @@ def main():
     t1 = time.perf_counter()
     elapsed = bd.max_over_ranks(t1 - t0, dev, world)
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else None
+    # two independent plant groups (reported beside the value, never as it):
+    # the same steps with consecutive steps on two streams
+    two_groups = None
+    if not args.dry_run and solver.active == 1:
+        solver.active = 2
+        for _ in range(2):
+            solver.step()
+        solver.sync()
+        if world > 1:
+            dist.barrier()
+        solver.sync()
+        tg0 = time.perf_counter()
+        for _ in range(args.steps):
+            solver.step()
+        solver.sync()
+        if world > 1:
+            dist.barrier()
+        two_groups = bd.max_over_ranks(time.perf_counter() - tg0, dev, world)
+        solver.active = 1
     # one launch alone (separate pass, host-synchronised per step): the isolated launch time
     kernel_ms_alone = None
     if not args.dry_run:
@@ -538,6 +568,13 @@ def main():
             check['value_all_instances'] = round(value, 1)
             value *= check['converged_frac_all_ranks']
         ms_per_step = 1e3 * elapsed / args.steps
+        if two_groups is not None:
+            v2 = wl['total'] / (two_groups / args.steps) if wl['scaling'] == 'strong' \
+                else world * B * args.steps / two_groups
+            if args.config == 'C4' and 'converged_frac_all_ranks' in check:
+                v2 *= check['converged_frac_all_ranks']
+            check['value_two_groups'] = round(v2, 1)
+            check['ms_per_step_two_groups'] = round(1e3 * two_groups / args.steps, 4)
         roof, cpu = None, None
         if not args.dry_run:
             present = len(os.sched_getaffinity(0))
@@ -563,14 +600,12 @@ def main():
                 except Exception:
                     traffic = None
             check['mean_iterations_ref'] = float(kref.mean())
-            # steps overlap on --streams streams: the device's rate over the timed region is the
-            # per-step flops over the time per step
+            # the device rate over the timed region (flops per step / ms per step)
             achieved_pipe = flops_launch / (ms_per_step * 1e-3) / 1e12
             # achieved / frac: flops per launch / the mean launch duration over the timed region
-            # (hipEvents on each launch's stream; with the steps overlapping on config.streams
-            # streams a launch's duration includes the time it shares the CUs with the other
-            # stream's launch); beside it the device rate over the timed region (flops per step /
-            # ms per step) and the launch alone
+            # (hipEvents around each step on its stream: the solve launch and the repair launch
+            # that follows it; at config.streams = 1, the default, every launch runs alone, so
+            # this is the launch's own duration and rocprofv3's kernel average reproduces it)
             roof = {'bound': 'fp64_valu', 'achieved': round(achieved, 4),
                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                     'frac': round(achieved / FP64_PEAK_TFLOPS, 5), 'traffic': traffic,
@@ -586,11 +621,11 @@ def main():
                             'stage blocks, DESIGN.md 4); algorithmic flops = K_ref x F_iter (SURVEY.md 8(d)); '
                             'traffic = HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE '
                             'passes of this config (traffic_source); achieved = flops per launch / '
-                            'kernel_ms, the mean launch duration over the timed steps (hipEvents on '
-                            'each launch\'s stream; the steps overlap on config.streams streams, so a '
-                            'launch shares the CUs with the other stream\'s); achieved_per_step = '
-                            'flops per launch / ms_per_step, the device rate over the timed region; '
-                            'kernel_ms_alone = one launch by itself (host-synchronised pass)'}
+                            'kernel_ms, the mean duration of a step\'s launches over the timed steps '
+                            '(hipEvents on the launch stream; one stream, so each launch runs alone); '
+                            'achieved_per_step = flops per launch / ms_per_step, the device rate over '
+                            'the timed region; kernel_ms_alone = one launch by itself '
+                            '(host-synchronised pass)'}
             st_json = os.path.join(ROOT, 'profiles', 'stamps_%s.json' % args.config)
             if args.precision == 'fp64' and os.path.exists(st_json):
                 # latency roof: at batch 1024 one instance runs per SIMD, so the
@@ -751,22 +786,30 @@ class LoopRunner:
     group's trajectories are the ones the whole batch in one call gives."""
 
     def __init__(self, cfg, wl, local, streams=1):
+        import torch
         import bqp
-        self.bqp, self.cfg, self.wl = bqp, cfg, wl
+        self.bqp, self.cfg, self.wl, self.torch = bqp, cfg, wl, torch
+        self.local = local
         self.streams = max(1, min(int(streams), len(wl['X0'])))
         self.hs = [bqp.Handle(local) for _ in range(self.streams)]
         self.h = self.hs[0]
+        # each group launches on its own torch stream (the loop's _device entry points run on the
+        # caller's current stream); the trajectories come back as tensors in this GPU's HBM
+        dev = torch.device('cuda', local)
+        self.ss = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(self.streams - 1)]
 
-    def _one(self, X0, steps, h):
+    def _one(self, X0, steps, h, s):
         b = self.bqp
-        if self.cfg == 'CL':
-            return b.closed_loop(self.wl['mpc'], X0, steps, handle=h)
-        return b.closed_loop_sqp(self.wl['mpc'], X0, steps, learning=dict(q=100, mask=1), handle=h)
+        with self.torch.cuda.stream(s):
+            if self.cfg == 'CL':
+                return b.closed_loop(self.wl['mpc'], X0, steps, handle=h, device=self.local)
+            return b.closed_loop_sqp(self.wl['mpc'], X0, steps, learning=dict(q=100, mask=1), handle=h,
+                                     device=self.local)
 
     def run(self, steps):
         X0 = self.wl['X0']
         if self.streams == 1:
-            return self._one(X0, steps, self.h)
+            return self._one(X0, steps, self.h, self.ss[0])
         import threading
         parts = np.array_split(np.arange(len(X0)), self.streams)
         res = [None] * self.streams
@@ -774,7 +817,7 @@ class LoopRunner:
 
         def work(i):
             try:
-                res[i] = self._one(X0[parts[i]], steps, self.hs[i])
+                res[i] = self._one(X0[parts[i]], steps, self.hs[i], self.ss[i])
             except Exception as e:               # re-raised on the main thread
                 err.append(e)
         th = [threading.Thread(target=work, args=(i,)) for i in range(self.streams)]
@@ -788,6 +831,8 @@ class LoopRunner:
         for k, v in res[0].items():
             if isinstance(v, np.ndarray):
                 out[k] = np.concatenate([r[k] for r in res])
+            elif isinstance(v, self.torch.Tensor):
+                out[k] = self.torch.cat([r[k] for r in res])
         return out
 
     def kernel_ms(self):
@@ -869,18 +914,26 @@ def bench_loop(args):
     tg0 = time.perf_counter()
     gathered = {}
     nbytes = 0
+    # (the GPU loop's trajectories are already tensors in this rank's HBM: bqp.closed_loop*(...,
+    # device=...), so the all-gather reads them there - no host round trip before the collective)
+    dev_resident = all(isinstance(r[k], torch.Tensor) for k in names)
     for k in names:
-        t = torch.from_numpy(np.ascontiguousarray(r[k])).to(dev)
-        gathered[k] = bd.gather_rows(t, total, world).cpu().numpy()
-        nbytes += gathered[k].nbytes
+        t = r[k] if isinstance(r[k], torch.Tensor) else torch.from_numpy(np.ascontiguousarray(r[k])).to(dev)
+        gathered[k] = bd.gather_rows(t, total, world)
+    if not args.dry_run:
+        torch.cuda.synchronize()
     t_gather = bd.max_over_ranks(time.perf_counter() - tg0, dev, world)
+    gathered = {k: v.cpu().numpy() for k, v in gathered.items()}
+    nbytes = sum(v.nbytes for v in gathered.values())
     fl = gathered['exitflag']
     check = dict(converged_frac_all_ranks=float((fl == 1).mean()),
                  gathered_instances=int(gathered['X'].shape[0]),
-                 gathered_bytes=int(nbytes), gather_s=round(t_gather, 4))
+                 gathered_bytes=int(nbytes), gather_s=round(t_gather, 4),
+                 gather_from_device=bool(dev_resident))
     if 'iterations' in r and r.get('iterations') is not None:
-        check.update(sqp_iterations_mean=float(np.mean(r['iterations'])),
-                     sqp_iterations_max=int(np.max(r['iterations'])))
+        its = r['iterations']
+        its = its.cpu().numpy() if isinstance(its, torch.Tensor) else its
+        check.update(sqp_iterations_mean=float(np.mean(its)), sqp_iterations_max=int(np.max(its)))
     if args.dry_run and rank == 0:
         full = loop_workload(args.config, B * world, 0, 1)
         # the stub's per-instance result depends only on the instance's own x0, so the unsharded

@@ -51,7 +51,10 @@ typedef struct {
     double tol_stat;   /* stationarity inf-norm / (1 + |cost gradient|_inf), default 1e-8 */
     double tol_feas;   /* primal residual inf-norm / (1 + |bounds, rhs|_inf), default 1e-10 */
     double tol_comp;   /* average complementarity mu (absolute), default 1e-14 */
-    double tau;        /* fraction-to-boundary, default 0.995 */
+    double tau;        /* fraction-to-boundary, default 0.995.  At tau >= 0.995 the structured
+                          solver's step rule lets the corrector step go to 0.99999 of the boundary
+                          on a well-centred iterate; a smaller tau bounds every
+                          step */
     int precision;     /* structured API: 0 = fp64 (default); 1 = fp32 solver arithmetic/LDS state
                           (inputs and outputs stay fp64; tolerances floored at 1e-5 / 1e-6 / 1e-9);
                           2 = mixed: an fp32 launch to those floored tolerances, then an fp64 launch

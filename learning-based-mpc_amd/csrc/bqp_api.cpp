@@ -290,11 +290,14 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
 #else
     const size_t nStamp = 0;
 #endif
-    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + nStamp + nPol)));
+    // + the work-queue counters of the launches (bqp::OCP_QUEUES ints)
+    const size_t nQ = (bqp::OCP_QUEUES + 1) / 2;
+    HIP_TRY(h->work.reserve(sizeof(double) * (nH + nF + nS + 8 + nStamp + nPol + nQ)));
     double* Hd = (double*)h->work.p;
     double* Fd = Hd + nH;
     double* Sd = Fd + nF;
     int* polneed = (int*)(Sd + nS + 8 + nStamp);
+    int* queues = (int*)(Sd + nS + 8 + nStamp + nPol);
     const double* Hinst = nullptr;
     if (hinst) {   // per-instance prepared stage-cost tables
         HIP_TRY(h->wwork.reserve(sizeof(double) * (size_t)batch * nH));
@@ -307,9 +310,11 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         Pg = h->pwork.p;
     }
     HIP_TRY(bqp::launch_ocp_prep(D->W, mp > 0 ? D->Fp : D->W, nx, nu, np, N, mp, d->poly_stage,
-                                 hstride, mpad, Hd, Fd, st));
+                                 hstride, mpad, Hd, Fd, queues, st));
     bqp::OcpKernelArgs a;
     memset(&a, 0, sizeof(a));
+    // the solve launch's work queue (used when the batch exceeds the resident workgroups)
+    a.queue = queues;
     a.N = N; a.mp = mp; a.kp = d->poly_stage; a.batch = batch; a.wpb = wpb;
     const Shared& LS = f32 ? L32 : L64;
     a.hstride = hstride; a.mpad = mpad; a.shared_doubles = LS.doubles;
@@ -351,6 +356,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         a1.exitflag = hflag;
         a1.hand_out = hb; a1.hand_it = hit; a1.hand_stride = (int64_t)hrec;
         a1.pi_out = a1.lamx_out = a1.lamu_out = a1.lamp_out = nullptr;
+        a1.queue = queues + 1;
         HIP_TRY(bqp::launch_ocp_f32(a1, nx, nu, np, st));
         // phase 2: fp64 from the handed-over iterates
         a.hand_in = hb; a.hand_flag = hflag; a.hand_it = hit; a.hand_stride = (int64_t)hrec;
@@ -360,6 +366,7 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         // the mixed mode reports the fp64 solve's status there; the others leave at once
         bqp::OcpKernelArgs a3 = a;
         a3.hand_in = nullptr; a3.hand_it = nullptr; a3.redo_flag = hflag;
+        a3.queue = nullptr;           // sparse: most workgroups leave at once
         HIP_TRY(bqp::launch_ocp(a3, nx, nu, np, st));
     } else if (f32) {
         HIP_TRY(bqp::launch_ocp_f32(a, nx, nu, np, st));
@@ -1083,7 +1090,10 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
     HIP_TRY(hipEventCreate(&e0.e));
     HIP_TRY(hipEventRecord(e0.e, st));
     int launches = 0;
-    if (!getenv("BQP_LB_TRACE")) {
+    // BQP_LB_SYNC selects the step-synchronous loop below (the asynchronous loop's bitwise
+    // reference in tests/test_gpu_lbmpc_dms.py); BQP_LB_TRACE only adds diagnostics to either
+    const bool sync_loop = getenv("BQP_LB_SYNC") != nullptr;
+    if (!sync_loop) {
         // asynchronous (round 5): every instance runs at its own closed-loop step.  Each round is
         // one SQP iteration of every unfinished instance, then sqp_loop_advance_kernel moves the
         // instances whose SQP has finished to their next step (u_0, plant, window, constraints,
@@ -1105,7 +1115,7 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
         qd.pol_stall = LB_POLISH_STALL;
         bqp::SqpAdvanceArgs v;
         memset(&v, 0, sizeof(v));
-        v.batch = batch; v.nx = nx; v.n = n; v.m = m; v.nv = N * d->nu; v.warm = sl->warm;
+        v.batch = batch; v.nx = nx; v.nu = d->nu; v.n = n; v.m = m; v.nv = N * d->nu; v.warm = sl->warm;
         v.steps = cl->steps; v.q = q; v.plant = cl->plant; v.delta = cl->delta;
         v.hinv2 = 1.0 / (bw * bw); v.lam = lam;
         v.K = D->K; v.bin0 = sl->bin0; v.Bx = sl->Bx; v.xeq = cl->x_eq; v.ueq = cl->u_eq;
@@ -1129,7 +1139,7 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
             if (nf >= batch) break;
         }
     }
-    for (int t = 0; t < (getenv("BQP_LB_TRACE") ? cl->steps : 0); ++t) {
+    for (int t = 0; t < (sync_loop ? cl->steps : 0); ++t) {
         HIP_TRY(bqp::launch_sqp_loop_prep(batch, nx, n, m, N * d->nu, t > 0 && sl->warm, s,
                                           sl->bin0, sl->Bx, bin, z, st));
         if (t > 0 && !sl->warm) HIP_TRY(hipMemsetAsync(z, 0, sizeof(double) * B * n, st));

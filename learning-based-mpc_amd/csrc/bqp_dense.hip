@@ -19,6 +19,7 @@
 //      stalled (the structured kernel's rule, bqp_ocp.hip).
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "bqp_internal.h"
 #include "bqp_wave.h"
@@ -37,6 +38,8 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_FEAS_GUARD 1e-8    // -2 needs the primal residual above this (relative)
 #define DQ_CMAX_K 100.0       // convergence also needs every row's t lam <= CMAX_K tol_comp
 #define DQ_SOC_ALPHA 0.1      // predictor step below this on a primal-feasible iterate: no SOC term
+#define DQ_RES_SHORT 0.5      // a step shorter than this: the next residuals evaluated exactly
+#define DQ_RES_EVERY 8        // and at least every 8th iteration (else the (1 - al) recurrence)
 #define DQ_POL_ROUNDS 4       // active-set corrections of the polish
 
 // polish mode of an instance: the launch's, or 2 once the instance's own SQP iteration count has
@@ -1773,9 +1776,19 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
         double al_last = -1.0;            // the last step length (< 0: evaluate the residuals exactly)
+        int since = 0;                    // iterations since the last exact evaluation
+        const int res_every = a.res_every > 0 ? a.res_every : DQ_RES_EVERY;
         for (it = 0; it <= a.max_iter; ++it) {
-            if (al_last < 0.0) residuals(stat, feq, fin, csum, gscale, zmax, cmax);
-            else scaled_residuals(1.0 - al_last, stat, feq, fin, csum, zmax, cmax);
+            // exact residuals at the start, after a short step (the recurrence's (1 - al) hardly
+            // contracts the error an inexact Newton solve leaves - pivot floor, near-singular K)
+            // and every res_every iterations; scaled ones otherwise
+            if (al_last < DQ_RES_SHORT || since + 1 >= res_every) {
+                residuals(stat, feq, fin, csum, gscale, zmax, cmax);
+                since = 0;
+            } else {
+                scaled_residuals(1.0 - al_last, stat, feq, fin, csum, zmax, cmax);
+                ++since;
+            }
             double feas = fmax(feq, fin);
             mu = csum * minv;
             auto converged = [&] {
@@ -2273,9 +2286,19 @@ __global__ void __launch_bounds__(64) dense_wave_kernel(DenseKernelArgs a) {
     double mu = 0.0, mu_min = INFINITY;
     if (flag == 0) {
         double al_last = -1.0;            // the last step length (< 0: evaluate the residuals exactly)
+        int since = 0;                    // iterations since the last exact evaluation
+        const int res_every = a.res_every > 0 ? a.res_every : DQ_RES_EVERY;
         for (it = 0; it <= a.max_iter; ++it) {
-            if (al_last < 0.0) residuals(stat, fin, csum, gscale, zmax, cmax);
-            else scaled_residuals(1.0 - al_last, stat, fin, csum, zmax, cmax);
+            // exact residuals at the start, after a short step (the recurrence's (1 - al) hardly
+            // contracts the error an inexact Newton solve leaves - pivot floor, near-singular K)
+            // and every res_every iterations; scaled ones otherwise
+            if (al_last < DQ_RES_SHORT || since + 1 >= res_every) {
+                residuals(stat, fin, csum, gscale, zmax, cmax);
+                since = 0;
+            } else {
+                scaled_residuals(1.0 - al_last, stat, fin, csum, zmax, cmax);
+                ++since;
+            }
             double feas = fin;
             mu = csum * minv;
             auto converged = [&] {
@@ -2458,7 +2481,13 @@ hipError_t launch_dense_symmetrize(double* H, int n, int count, int64_t stride, 
     return hipGetLastError();
 }
 
-hipError_t launch_dense(const DenseKernelArgs& a, hipStream_t st) {
+hipError_t launch_dense(const DenseKernelArgs& a0, hipStream_t st) {
+    DenseKernelArgs a = a0;
+    // diagnostic: BQP_DENSE_RES_EVERY=k evaluates the residuals exactly every k iterations (1:
+    // never by the recurrence; tests/test_gpu_quadprog_status.py compares the two)
+    if (a.res_every <= 0) {
+        if (const char* e = getenv("BQP_DENSE_RES_EVERY")) a.res_every = atoi(e);
+    }
     if (a.n > 256 || a.me > 256) return hipErrorInvalidValue;
     if (a.me == 0 && a.n <= SW_NMAX && small_lds_doubles(a.n, a.m) <= SW_LDS_MAX) {
         const size_t lds = sizeof(double) * small_lds_doubles(a.n, a.m);

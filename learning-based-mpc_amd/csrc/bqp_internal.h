@@ -15,8 +15,14 @@ constexpr int STATS_W = 7;
 //   H  : (N+1) stages x hstride doubles, stage cost in internal order [x; theta; u], row-major
 //   Fp : column-major [NV][mpad] polytope matrix in internal order
 // All other arrays are in the public (external) layout with per-instance element strides.
+constexpr int OCP_QUEUES = 4;   // work-queue counters per structured solve (one per launch)
 struct OcpKernelArgs {
     int N, mp, kp, batch, wpb, hstride, mpad, shared_doubles, max_iter;
+    // persistent work queue: when the batch needs more workgroups than the
+    // device holds at once, the launch is sized to the resident workgroups and every instance
+    // slot (stage / row wave pair) takes its next instance from this counter (zeroed by the prep
+    // kernel) as soon as its current one is done; nullptr: one instance per slot, grid = batch
+    int* queue;
     double tol_stat, tol_feas, tol_comp, tau;
     const double* H;
     const double* Fp;
@@ -75,7 +81,7 @@ int ocp_wave_lds_doubles_f32(int N, int nx, int nu, int np, int mpad, bool fpi, 
 hipError_t launch_ocp_f32(const OcpKernelArgs& a, int nx, int nu, int np, hipStream_t st, bool pol = false);
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,
-                           hipStream_t st);
+                           int* qzero, hipStream_t st);
 hipError_t launch_ocp_prep_h(const double* W, int64_t sW, int batch, int nx, int nu, int np,
                              int N, int hstride, double* Hout, hipStream_t st);
 hipError_t launch_ocp_finalize(const double* stats, int batch, void* out, hipStream_t st);
@@ -96,6 +102,8 @@ struct DenseKernelArgs {
     const int* pol_it; // optional: per-instance SQP iteration counts; mode 2 where >= pol_stall
     int pol_stall;     // (the learned-model loop, whose instances run at their own SQP iteration)
     const int* skip;   // optional: instances with skip[i] != 0 are not solved (finished SQPs)
+    int res_every;     // exact residual evaluation at least every res_every iterations (0: 8;
+                       // 1: every iteration, the diagnostic BQP_DENSE_RES_EVERY)
 };
 
 int dense_work_doubles(int n, int m, int me);
@@ -149,7 +157,7 @@ hipError_t launch_mg_plant(int plant, int batch, int N, int steps, int t, double
 // for the plant, and the step's z / iteration count into the caller's logs after it
 // asynchronous learned-model loop: one instance's advance to its next closed-loop step
 struct SqpAdvanceArgs {
-    int batch, nx, n, m, nv, warm, steps, q, plant;
+    int batch, nx, nu, n, m, nv, warm, steps, q, plant;
     double delta, hinv2, lam;
     const double *K, *bin0, *Bx, *xeq, *ueq, *A, *Bm;
     double *s, *z, *bin, *X, *U, *win, *XL, *Zlog;

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "bqp_internal.h"
 #include "bqp_wave.h"
@@ -89,6 +90,7 @@ namespace dp {
 #define TAU_FAST_MU 1e-6
 #define TAU_FAST 0.99999
 #define TAU_FAST_END 0.99999
+#define TAU_FAST_MIN 0.995   // the fast rule applies at tau >= the default only
 #define CMAX_K 100.0
 #define SOC_ALPHA 0.1
 #define DEG_POLISH 1e-10
@@ -120,6 +122,11 @@ __device__ __forceinline__ float frcp(float t) {
 // iteration loop in registers (dozens of them: the stage wave's scratch spills)
 __device__ __forceinline__ int opq(int v) {
     asm volatile("" : "+v"(v));
+    return v;
+}
+// the same for a wave-uniform value (kept in a scalar register)
+__device__ __forceinline__ int opq_s(int v) {
+    asm volatile("" : "+s"(v));
     return v;
 }
 
@@ -194,6 +201,7 @@ enum : int {
     X_PCHG,      //         rows an active-set correction would move
     X_PDEC,      //         decision (stage wave): 0 pass, 1 accept, 2 correct the set, 3 give up
     X_CGD,       //         inner step (row wave): 0 CG step, 1 multiplier (AL) step, 2 pass done
+    X_NEXT,      // persistent launch: the slot's next instance (stage wave, int bits)
     X_NXCH = 20
 };
 
@@ -2179,8 +2187,10 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
         const real rm = row_pass(0, true, smu, 0.0, L.dsc, L.duc);
         // step rule (oracle/cpu_ipm.c TAU_FAST): a predictor step above 0.99 on an iterate with
         // mu > 1e-6, or any predictor step of at least 0.99999 (the Newton end phase), lets the
-        // corrector go to 0.99999 of the boundary, else tau
-        const bool fast = (al_aff > real(TAU_FAST_AFF) && mu > real(TAU_FAST_MU)) || al_aff >= real(TAU_FAST_END);
+        // corrector go to 0.99999 of the boundary, else tau.  Only at the default tau or above: a
+        // caller's smaller tau (bqp_options.tau, chosen for robustness) bounds every step
+        const bool fast = a.tau >= TAU_FAST_MIN &&
+                          ((al_aff > real(TAU_FAST_AFF) && mu > real(TAU_FAST_MU)) || al_aff >= real(TAU_FAST_END));
         const real tau = fast ? fmax(real(a.tau), real(TAU_FAST)) : real(a.tau);
         real al = (rm > 1.0 ? 1.0 / rm : 1.0) * tau;
         if (al > 1.0) al = 1.0;
@@ -2601,15 +2611,15 @@ __device__ __forceinline__ void row_wave(const OcpKernelArgs& a, real* W, const 
 // ==========================================================================================
 // kernel: QPB instances per workgroup, waves [0, QPB) stage waves, [QPB, 2 QPB) row waves
 // ==========================================================================================
-template <int NX, int NU, int NP, int SPL, int RPL, int BPL, bool POL>
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL, bool POL, bool QUEUE>
 __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
     constexpr int NS = NX + NP;
     constexpr int NV = NS + NU;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     real* lds = reinterpret_cast<real*>(lds_raw);
     const int N = a.N;
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    const int lane_k = threadIdx.x & 63;
+    const int wid = QUEUE ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6);
     const int qpb = a.wpb;
     if constexpr (POL) {
         // repair launch: a workgroup none of whose instances the solve launch marked leaves
@@ -2619,7 +2629,7 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
         if (!__syncthreads_or(need)) return;
     }
     // ---------------- shared tables: H (N+1 stages) and Fp (column-major, mpad rows) -------
-    if constexpr (SPL == 2) {
+    if constexpr (SPL == 2 && !QUEUE) {
         // mixed mode, cold retry launch: a workgroup none of whose instances needs the retry
         // leaves before staging the shared tables
         if (a.redo_flag) {
@@ -2658,53 +2668,116 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
     }
     __syncthreads();
     const bool rowwave = wid >= qpb;
-    const int slot = rowwave ? wid - qpb : wid;
-    const int inst = blockIdx.x * qpb + slot;
-    if (inst >= a.batch) return;       // both waves of an empty slot leave together
-    if (POL && a.pol_need[inst] == 0) return;   // repair launch: nothing to polish here
-    if (!POL && SPL == 2 && a.redo_flag &&
-        !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
-        return;                        // mixed mode, cold retry launch: nothing to redo here
-    const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, a.sh_hp >= 0,
-                                LNG && a.sh_bnd >= 0, a.H_inst != nullptr);
-    real* W = lds + a.shared_doubles + slot * L.total;
-    if (fpi && rowwave) {
-        // the instance's polytope, external column-major [x; u; theta] (n_poly rows) -> internal
-        // [x; theta; u] columns of mpad rows (the layout of the shared table, ocp_prep_kernel)
-        Fs = W + L.Fi;
-        const double* Fg = a.Fp_inst + (int64_t)inst * a.sFp;
-        constexpr int NS = NX + NP;
-        for (int r = lane; r < a.mpad; r += WAVE) {
+    const int slot0 = rowwave ? wid - qpb : wid;
+    // one instance on this slot (both waves of the pair)
+    auto instance = [&](int inst, int slot, int lane) __attribute__((always_inline)) {
+        const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, a.sh_hp >= 0,
+                                    LNG && a.sh_bnd >= 0, a.H_inst != nullptr);
+        real* W = lds + a.shared_doubles + slot * L.total;
+        real* Fsi = Fs;
+        if (fpi && rowwave) {
+            // the instance's polytope, external column-major [x; u; theta] (n_poly rows) -> internal
+            // [x; theta; u] columns of mpad rows (the layout of the shared table, ocp_prep_kernel)
+            Fsi = W + L.Fi;
+            const double* Fg = a.Fp_inst + (int64_t)inst * a.sFp;
+            for (int r = lane; r < a.mpad; r += WAVE) {
 #pragma unroll
-            for (int c = 0; c < NV; ++c) {
-                const int e = c < NX ? c : (c < NS ? NX + NU + (c - NX) : NX + (c - NS));
-                real v = (r < a.mp) ? (real)Fg[(int64_t)e * a.mp + r] : real(0);
-                if (a.kp == N && c >= NS) v = 0;
-                Fs[c * a.mpad + r] = v;
+                for (int c = 0; c < NV; ++c) {
+                    const int e = c < NX ? c : (c < NS ? NX + NU + (c - NX) : NX + (c - NS));
+                    real v = (r < a.mp) ? (real)Fg[(int64_t)e * a.mp + r] : real(0);
+                    if (a.kp == N && c >= NS) v = 0;
+                    Fsi[c * a.mpad + r] = v;
+                }
             }
+            wave_sync();
         }
-        wave_sync();
-    }
 #if defined(BQP_EXP_ONLY)   // register-budget diagnostic: one wave's code alone (never run)
-    if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
-    else row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+        if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+        else row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fsi, lds, lane, inst);
 #else
-    if (!rowwave)
-        stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
-    else
-        row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+        if (!rowwave)
+            stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+        else
+            row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fsi, lds, lane, inst);
 #endif
+        return W + L.xch;
+    };
+    if constexpr (!QUEUE) {
+        const int inst = blockIdx.x * qpb + slot0;
+        if (inst >= a.batch) return;       // both waves of an empty slot leave together
+        if (POL && a.pol_need[inst] == 0) return;   // repair launch: nothing to polish here
+        if (!POL && SPL == 2 && a.redo_flag &&
+            !(a.exitflag[inst] != 1 && (a.redo_flag[inst] == 1 || a.redo_flag[inst] == 0)))
+            return;                        // mixed mode, cold retry launch: nothing to redo here
+        const int slot = slot0;
+        const int lane = lane_k;
+        const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, a.sh_hp >= 0,
+                                    LNG && a.sh_bnd >= 0, a.H_inst != nullptr);
+        real* W = lds + a.shared_doubles + slot * L.total;
+        if (fpi && rowwave) {
+            // the instance's polytope, external column-major [x; u; theta] (n_poly rows) -> internal
+            // [x; theta; u] columns of mpad rows (the layout of the shared table, ocp_prep_kernel)
+            Fs = W + L.Fi;
+            const double* Fg = a.Fp_inst + (int64_t)inst * a.sFp;
+            for (int r = lane; r < a.mpad; r += WAVE) {
+#pragma unroll
+                for (int c = 0; c < NV; ++c) {
+                    const int e = c < NX ? c : (c < NS ? NX + NU + (c - NX) : NX + (c - NS));
+                    real v = (r < a.mp) ? (real)Fg[(int64_t)e * a.mp + r] : real(0);
+                    if (a.kp == N && c >= NS) v = 0;
+                    Fs[c * a.mpad + r] = v;
+                }
+            }
+            wave_sync();
+        }
+#if defined(BQP_EXP_ONLY)   // register-budget diagnostic: one wave's code alone (never run)
+        if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+        else row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+#else
+        if (!rowwave)
+            stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+        else
+            row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
+#endif
+    } else {
+        // persistent work queue (ocp_queue_kernel; launch_t sizes the grid to the resident
+        // workgroups when the batch needs more): the slot's first instance is the static one,
+        // every later one comes from the counter a.queue, so a slot starts its next instance as
+        // soon as its current one is done instead of idling until the workgroup's slowest instance
+        // ends, and the shared tables are staged once per workgroup lifetime (SURVEY 7 "per-wave
+        // early exit with a persistent-kernel work queue"; the C4 iteration counts run from 3 to
+        // 42 around a mean of 8.5)
+        int inst = blockIdx.x * qpb + slot0;
+        while (inst < a.batch) {
+            // the lane and slot made opaque per instance: nothing lane- or slot-dependent is
+            // hoisted out of the instance loop into registers carried across instances (the
+            // solve phases are at the 256-VGPR budget; opq)
+            real* X = instance(inst, opq_s(slot0), opq(lane_k));
+            // next instance: the stage wave takes a ticket and hands it to its row wave through
+            // the slot's exchange block; one workgroup barrier on each wave of the pair (the other
+            // slots' waves pass it inside their own iterations, as every barrier of this kernel)
+            int* xn = reinterpret_cast<int*>(X + X_NEXT);
+            if (!rowwave && lane_k == 0) *xn = atomicAdd(a.queue, 1) + (int)gridDim.x * qpb;
+            BARRIER();
+            inst = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(xn));
+        }
+    }
 }
 
-// the solve kernel (no polish code: the main loop keeps its register budget) and the repair
-// kernel (same IPM, then the active-set polish) over the instances the solve kernel marked
+// the solve kernel (no polish code: the main loop keeps its register budget), the repair kernel
+// (same IPM, then the active-set polish) over the instances the solve kernel marked, and the
+// persistent solve kernel (work queue) for batches beyond the resident workgroups
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_ipm_kernel(OcpKernelArgs a) {
-    ocp_body<NX, NU, NP, SPL, RPL, BPL, false>(a);
+    ocp_body<NX, NU, NP, SPL, RPL, BPL, false, false>(a);
 }
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_polish_kernel(OcpKernelArgs a) {
-    ocp_body<NX, NU, NP, SPL, RPL, BPL, true>(a);
+    ocp_body<NX, NU, NP, SPL, RPL, BPL, true, false>(a);
+}
+template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
+__global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_queue_kernel(OcpKernelArgs a) {
+    ocp_body<NX, NU, NP, SPL, RPL, BPL, false, true>(a);
 }
 
 }  // namespace dp / sp
@@ -2727,13 +2800,36 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_polish_kernel(OcpKer
 #endif
 
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
-static hipError_t launch_t(const OcpKernelArgs& a, int blocks, size_t lds, hipStream_t st, bool pol) {
+static hipError_t launch_t(const OcpKernelArgs& a0, int blocks, size_t lds, hipStream_t st, bool pol) {
 #ifdef BQP_F32
     (void)pol;
     auto k = sp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
+    auto kq = sp::ocp_queue_kernel<NX, NU, NP, SPL, RPL, BPL>;
 #else
     auto k = pol ? dp::ocp_polish_kernel<NX, NU, NP, SPL, RPL, BPL> : dp::ocp_ipm_kernel<NX, NU, NP, SPL, RPL, BPL>;
+    auto kq = dp::ocp_queue_kernel<NX, NU, NP, SPL, RPL, BPL>;
 #endif
+    OcpKernelArgs a = a0;
+    // persistent launch (ocp_queue_kernel) when the batch needs more workgroups than fit on the
+    // device at once: the grid is the resident workgroups and the slots pull the remaining
+    // instances from a.queue; otherwise one instance per slot (BQP_NO_QUEUE: always, for A/B)
+    const bool no_queue = getenv("BQP_NO_QUEUE") != nullptr;
+    if (!pol && !a.redo_flag && a.queue && !no_queue) {
+        int dev = 0, cus = 0, per_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (lds > 64 * 1024 && e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)kq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kq, 128 * a.wpb, lds);
+        if (e != hipSuccess) return e;
+        const int resident = cus * (per_cu > 0 ? per_cu : 1);
+        if (blocks > resident) {
+            hipLaunchKernelGGL(kq, dim3(resident), dim3(128 * a.wpb), lds, st, a);
+            return hipGetLastError();
+        }
+    }
+    a.queue = nullptr;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

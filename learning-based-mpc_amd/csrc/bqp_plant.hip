@@ -385,7 +385,9 @@ __global__ void __launch_bounds__(256) sqp_loop_advance_kernel(SqpAdvanceArgs a)
 }
 
 hipError_t launch_sqp_loop_advance(const SqpAdvanceArgs& a, hipStream_t st) {
-    if (a.n > 4 * 256 || a.nx > 8) return hipErrorInvalidValue;
+    // the kernel is written for the MG plant shape (x[4], one input: RK4 / ode23 of
+    // models/trueModel.m, K x + c with K 1 x 4)
+    if (a.n > 4 * 256 || a.nx != 4 || a.nu != 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(sqp_loop_advance_kernel, dim3(a.batch), dim3(256), 0, st, a);
     return hipGetLastError();
 }

@@ -21,8 +21,11 @@ __device__ __forceinline__ int ext_index(int i, int nx, int nu, int np) {
 
 __global__ void ocp_prep_kernel(const double* __restrict__ W, const double* __restrict__ Fp,
                                 int nx, int nu, int np, int N, int mp, int kp, int hstride,
-                                int mpad, double* __restrict__ Hout, double* __restrict__ Fout) {
+                                int mpad, double* __restrict__ Hout, double* __restrict__ Fout,
+                                int* __restrict__ qzero) {
     const int nv = nx + nu + np, ns = nx + np;
+    // the structured launches' work-queue counters (OcpKernelArgs::queue), one per launch
+    if (qzero && blockIdx.x == 0 && threadIdx.x < OCP_QUEUES) qzero[threadIdx.x] = 0;
     const int nH = (N + 1) * hstride;
     const int nF = nv * mpad;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nH + nF; t += gridDim.x * blockDim.x) {
@@ -51,11 +54,11 @@ __global__ void ocp_prep_kernel(const double* __restrict__ W, const double* __re
 
 hipError_t launch_ocp_prep(const double* W, const double* Fp, int nx, int nu, int np, int N,
                            int mp, int kp, int hstride, int mpad, double* Hout, double* Fout,
-                           hipStream_t st) {
+                           int* qzero, hipStream_t st) {
     const int total = (N + 1) * hstride + (nx + nu + np) * mpad;
     const int blocks = (total + 255) / 256;
     hipLaunchKernelGGL(ocp_prep_kernel, dim3(blocks), dim3(256), 0, st, W, Fp, nx, nu, np, N,
-                       mp, kp, hstride, mpad, Hout, Fout);
+                       mp, kp, hstride, mpad, Hout, Fout, qzero);
     return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@
 #define TAU_FAST_MU 1e-6     /* ... and mu above this: the corrector step goes to TAU_FAST */
 #define TAU_FAST 0.99999
 #define TAU_FAST_END 0.99999 /* predictor step at least this: the fast step at any mu */
+#define TAU_FAST_MIN 0.995   /* the fast rule applies only at tau >= the default (a caller's smaller tau bounds every step) */
 #define CMAX_K 100.0     /* and every row: t_i lam_i <= CMAX_K tol_comp (the average alone lets one */
 #endif            /* weakly active row keep t ~ 1e-10: first moves off by 1e-7 at N = 100) */
 #ifndef DEG_POLISH
@@ -981,7 +982,8 @@ static int solve_one(const prob_t* P, work_t* W, const opts_t* op, int* iters, d
              * fast corrector step too.  Iterations on the C port: C2 9.13 -> 7.20 (stored states;
              * max 16 -> 15), C3 12.60 -> 11.49, C5 9.54 -> 7.87, C4 10.29 -> 8.53 (the exact
              * classification unchanged). */
-            const double tau = ((a_pred_keep > TAU_FAST_AFF && mu > TAU_FAST_MU) || a_pred_keep >= TAU_FAST_END)
+            const double tau = op->tau >= TAU_FAST_MIN &&
+                                       ((a_pred_keep > TAU_FAST_AFF && mu > TAU_FAST_MU) || a_pred_keep >= TAU_FAST_END)
                                    ? fmax(op->tau, TAU_FAST) : op->tau;
             a = max_step(P, W) * tau;
         }

@@ -355,7 +355,7 @@ def solve(d, x0, w=None, opts=None, trace=None):
         # step rule (oracle/cpu_ipm.c TAU_FAST): a nearly full predictor step on an iterate with
         # mu > 1e-6, or any predictor step of at least 0.99999, lets the corrector go to 0.99999 of
         # the boundary
-        fast = (a > TAU_FAST_AFF and mu > TAU_FAST_MU) or a >= TAU_FAST_END
+        fast = op['tau'] >= 0.995 and ((a > TAU_FAST_AFF and mu > TAU_FAST_MU) or a >= TAU_FAST_END)
         tau = max(op['tau'], TAU_FAST) if fast else op['tau']
         a = min(1.0, tau * _max_step(st, o, dt, dl))
         _apply(st, o, a, ds, du, dpi, dt, dl)

@@ -83,3 +83,31 @@ def test_fmincon_lmpc_loop_ode23(mg, term_set):
           'states %.2e, all states k>=200 %.2e' % (ep, e[:, :2].max(), e[200:].max()))
     assert ep < 1e-13
     assert e[:, :2].max() < 5e-3
+
+
+def test_device_resident_loops_equal_host(mg, term_set):
+    """bqp.closed_loop / closed_loop_sqp with device=0 run the _device entry
+    points on device memory and return torch tensors in HBM (what bench.py's trajectory
+    all-gather reads); they equal the host-pointer calls bit for bit"""
+    import torch
+    import bqp
+    g = golden('dms_DSS_tLMPC.npz')
+    tl = bqp.TrackingLMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'],
+                          mg['LAMBDA'], mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'],
+                          term_set[0], term_set[1], mg['x_wp'], mg['u_wp'], N=100)
+    X0 = g['x'][[0, 50, 100, 150]]
+    rh = bqp.closed_loop(tl, X0, 5, delta=0.01)
+    rd = bqp.closed_loop(tl, X0, 5, delta=0.01, device=0)
+    assert isinstance(rd.X, torch.Tensor) and rd.X.is_cuda
+    for k in ('X', 'U', 'exitflag'):
+        assert np.array_equal(rd[k].cpu().numpy(), rh[k]), k
+    lg = golden('lbmpc_instance.npz')
+    dl = bqp.DMSLBMPC(mg['A'], mg['B'], mg['Q'], mg['R'], mg['P'], mg['Tscalar'], mg['LAMBDA'],
+                      mg['PSI'], mg['F_x'], mg['h_x'], mg['F_u'], mg['h_u'], lg['F_w_N'],
+                      lg['h_w_N'], lg['F_x_d'], lg['h_x_d'], mg['x_wp'], mg['u_wp'], N=100)
+    x0 = np.array([0.15, 1.2875, 1.1547, 0.0]) + np.array([[0.0, 0, 0, 0], [0.003, -0.002, 0, 0]])
+    sh = bqp.closed_loop_sqp(dl, x0, 3, learning=dict(q=100, mask=1))
+    sd = bqp.closed_loop_sqp(dl, x0, 3, learning=dict(q=100, mask=1), device=0)
+    assert sd.X.is_cuda
+    for k in ('X', 'U', 'XL', 'window', 'exitflag', 'iterations'):
+        assert np.array_equal(sd[k].cpu().numpy(), sh[k]), k

@@ -90,3 +90,37 @@ def test_lbmpc_infeasible_subproblem(mg, handle):
     r = lb.solve(X0, td, handle=handle)
     assert r.exitflag[0] == -2 and r.exitflag[2] == -2, r.exitflag
     assert r.exitflag[1] == 1
+
+
+@pytest.mark.parametrize('n', [20, 40])
+def test_residual_recurrence_vs_exact_residuals(n, handle):
+    """the dense kernels step the residuals by the (1 - alpha) recurrence and evaluate
+    them exactly only at the start, after a short step (alpha < 0.5), every 8th iteration and to
+    confirm convergence.  On a nearly singular H (eigenvalues 1 ... 1e-15: the factor of K runs
+    into the pivot floor once the barrier terms dominate) the exit flag, iteration count and
+    solution must match the path that evaluates them exactly every iteration
+    (BQP_DENSE_RES_EVERY=1), and the algorithm statement oracle/dense_ipm.py.  n = 20: the one-wave
+    kernel, n = 40: the workgroup kernel."""
+    import os
+    from oracle import dense_ipm
+    rng = np.random.default_rng(17)
+    M, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    H = (M * np.logspace(0, -15, n)) @ M.T
+    H = 0.5 * (H + H.T)
+    qp = dict(H=H, f=rng.standard_normal(n), A=rng.standard_normal((3 * n, n)),
+              b=rng.uniform(0.5, 2.0, 3 * n), lb=-3 * np.ones(n), ub=3 * np.ones(n))
+    x, fval, ef, out, lam = _solve(qp, handle)
+    os.environ['BQP_DENSE_RES_EVERY'] = '1'
+    try:
+        xe, fe, efe, oute, lame = _solve(qp, handle)
+    finally:
+        del os.environ['BQP_DENSE_RES_EVERY']
+    r = dense_ipm.solve(**qp)
+    print('n %d: flags %d / %d (statement %d), iterations %d / %d (statement %d), |x - x_exact| %.2e'
+          % (n, ef[0], efe[0], r['exitflag'], out['iterations'][0], oute['iterations'][0],
+             r['iterations'], np.abs(x - xe).max()))
+    assert ef[0] == efe[0] == r['exitflag'] == 1
+    assert abs(int(out['iterations'][0]) - int(oute['iterations'][0])) <= 1
+    assert abs(int(out['iterations'][0]) - r['iterations']) <= 1
+    assert abs(fval[0] - fe[0]) <= 1e-10 * max(1.0, abs(fe[0]))
+    assert np.abs(x - xe).max() < 1e-6

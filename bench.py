@@ -404,6 +404,9 @@ def main():
                     help='structured solver arithmetic (C5 compares both)')
     ap.add_argument('--no-polish', action='store_true',
                     help='interior-point iterates only (bqp_options.polish = -1)')
+    ap.add_argument('--no-two-groups', action='store_true',
+                    help='skip the two-group pass of check.value_two_groups (profiling runs: every '
+                         'launch of the command then runs alone)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU/gloo rehearsal of the multi-rank path with a stub solver (tests)')
     ap.add_argument('--streams', type=int, default=None,
@@ -480,7 +483,7 @@ def main():
     # two independent plant groups (reported beside the value, never as it):
     # the same steps with consecutive steps on two streams
     two_groups = None
-    if not args.dry_run and solver.active == 1:
+    if not args.dry_run and solver.active == 1 and not args.no_two_groups:
         solver.active = 2
         for _ in range(2):
             solver.step()

@@ -380,6 +380,13 @@ int bqp_closed_loop_sqp_device(bqp_handle h, const bqp_lbmpc_dims* d, int batch,
  * launch stream (ms), and the number of kernel launches it covered. */
 int bqp_last_kernel_ms(bqp_handle h, double* ms, int* launches);
 
+/* Diagnostic: per instance of the most recent mixed-precision structured solve on this handle
+ * (bqp_options.precision = 2, N + 1 > 64), the fp32 phase's exit flag (1 / 0: continued in fp64
+ * from its iterate; -2 / -8: solved from the fp64 initial point), or 2 where the continuation did
+ * not converge and the retry launch solved the instance again from the fp64 initial point
+ * (tests/test_gpu_mixed.py).  batch must equal that solve's. */
+int bqp_debug_mixed_flags(bqp_handle h, int batch, int* flags);
+
 #ifdef __cplusplus
 }
 #endif

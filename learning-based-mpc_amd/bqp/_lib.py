@@ -74,7 +74,8 @@ EXPORTS = ['bqp_create', 'bqp_destroy', 'bqp_default_options', 'bqp_version', 'b
            'bqp_quadprog_batched_device', 'bqp_last_kernel_ms', 'bqp_nw_oracle',
            'bqp_nw_oracle_device', 'bqp_lbmpc_solve_batched', 'bqp_lbmpc_solve_batched_device',
            'bqp_closed_loop_ocp', 'bqp_closed_loop_ocp_device', 'bqp_closed_loop_lbmpc',
-           'bqp_closed_loop_lbmpc_device', 'bqp_closed_loop_sqp', 'bqp_closed_loop_sqp_device']
+           'bqp_closed_loop_lbmpc_device', 'bqp_closed_loop_sqp', 'bqp_closed_loop_sqp_device',
+           'bqp_debug_mixed_flags']
 
 _lib = None
 
@@ -110,6 +111,7 @@ def load():
     lib.bqp_quadprog_batched_device.argtypes = [C.c_void_p, C.POINTER(Dims), C.c_int, C.POINTER(Strides)] + \
         [_PD] * 8 + [C.POINTER(Options), _PD, _PD, _PI, _PD, _PD, _PD, _PD, C.c_void_p, C.c_void_p]
     lib.bqp_last_kernel_ms.argtypes = [C.c_void_p, _PD, _PI]
+    lib.bqp_debug_mixed_flags.argtypes = [C.c_void_p, C.c_int, _PI]
     lib.bqp_nw_oracle.argtypes = [C.c_void_p, C.c_int, C.c_int, _PD, C.c_int64, _PD, _PD, _PD,
                                   C.c_double, C.c_double]
     lib.bqp_nw_oracle_device.argtypes = [C.c_void_p, C.c_int, C.c_int, _PD, C.c_int64, _PD, _PD,
@@ -193,6 +195,15 @@ class Handle:
         n = C.c_int(0)
         check(self._lib.bqp_last_kernel_ms(self._h, C.byref(ms), C.byref(n)), 'bqp_last_kernel_ms')
         return ms.value, n.value
+
+    def mixed_flags(self, batch):
+        """per instance of the last mixed-precision solve on this handle: the fp32 phase's exit
+        flag, 2 where the retry launch solved it again from the fp64 start (bqp_debug_mixed_flags)"""
+        import numpy as np
+        out = np.zeros(batch, np.int32)
+        check(self._lib.bqp_debug_mixed_flags(self._h, int(batch), out.ctypes.data_as(_PI)),
+              'bqp_debug_mixed_flags')
+        return out
 
     def close(self):
         if self._h:

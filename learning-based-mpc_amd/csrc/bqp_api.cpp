@@ -50,6 +50,8 @@ struct bqp_handle_s {
     DevBuf pwork;  // long-horizon layout: global Riccati tables
     DevBuf wwork;  // per-instance stage-cost tables
     int last_batch = 0;
+    int* mixed_flags = nullptr;   // the last mixed-mode solve's fp32-phase flags (2: redone cold)
+    int mixed_batch = 0;
 };
 
 namespace {
@@ -166,6 +168,15 @@ int bqp_destroy(bqp_handle h) {
         if (h->stream) hipStreamDestroy(h->stream);
     }
     delete h;
+    return BQP_OK;
+}
+
+int bqp_debug_mixed_flags(bqp_handle h, int batch, int* flags) {
+    if (!h || !flags || batch <= 0) return BQP_E_ARG;
+    if (!h->mixed_flags || batch != h->mixed_batch) return BQP_E_ARG;
+    DevScope ds(h->device);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(flags, h->mixed_flags, sizeof(int) * batch, hipMemcpyDeviceToHost));
     return BQP_OK;
 }
 
@@ -348,6 +359,8 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         float* hb = (float*)h->hwork.p;
         int* hflag = (int*)(hb + hrec * batch);
         int* hit = hflag + batch;
+        h->mixed_flags = hflag;
+        h->mixed_batch = batch;
         bqp::OcpKernelArgs a1 = a;
         a1.wpb = wpb32;
         a1.shared_doubles = L32.doubles; a1.sh_F = L32.sh_F; a1.sh_hp = L32.sh_hp; a1.sh_bnd = L32.sh_bnd;

@@ -201,8 +201,9 @@ enum : int {
     X_PCHG,      //         rows an active-set correction would move
     X_PDEC,      //         decision (stage wave): 0 pass, 1 accept, 2 correct the set, 3 give up
     X_CGD,       //         inner step (row wave): 0 CG step, 1 multiplier (AL) step, 2 pass done
-    X_NEXT,      // persistent launch: the slot's next instance (stage wave, int bits)
-    X_NXCH = 20
+    X_NEXT,      // persistent launch: the slot's next instance (row wave, int bits; two slots
+    X_NEXT1,     //   used alternately by successive instances of the slot)
+    X_NXCH = 22
 };
 
 // Per-instance LDS layout (in doubles), sized from N at run time.
@@ -340,7 +341,7 @@ __device__ __forceinline__ bool hand_warm(const OcpKernelArgs& a, int inst) {
 // ==========================================================================================
 template <int NX, int NU, int NP, int SPL, bool POL>
 __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, const QpLds& L,
-                                           const real* Hs, int lane_w, int inst) {
+                                           const real* Hs, int lane_w, int inst, int pslot) {
     const int lane = lane_w;
     // POL: the repair kernel (ocp_polish_kernel) - the same IPM, then the active-set polish
     constexpr bool PC = POL && BQP_POLISH && !BQP_EXP_NOSTAGE;
@@ -357,7 +358,11 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
 #define BQP_HK(k) const real* Hk = Hs + (k) * hstride; \
     const double* Hkg = (a.H_inst ? a.H_inst + (int64_t)inst * (N + 1) * hstride : a.H) + (int64_t)(k) * hstride
 #define BQP_HV(idx) (LNG ? (real)Hkg[idx] : Hk[idx])
-    real* Pgl = LNG ? (real*)a.Pg + (int64_t)inst * (N + 1) * pk_stride(NS) : nullptr;
+    // the long-horizon Riccati tables in global scratch, per instance slot: a persistent launch
+    // reuses its slots' tables for every instance they take, so the tables stay in the XCD's L2
+    // (512 resident slots x 12.9 KB at N = 100) instead of every instance writing its own
+    // region back to HBM
+    real* Pgl = LNG ? (real*)a.Pg + (int64_t)pslot * (N + 1) * pk_stride(NS) : nullptr;
     // per-instance stage costs: the instance's prepared table (global), copied into the LDS slot
     // on short horizons
     if (!LNG && a.H_inst) {
@@ -1461,6 +1466,12 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     if (lane == 0) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
+        // mixed mode, cold retry launch: mark the instance as solved again from the fp64 start
+        // (its fp32-phase flag 0 / 1 becomes 2), so that the repair launch starts it cold too
+        // (hand_warm) and bqp_debug_mixed_flags can tell which instances phase 3 redid.  Written
+        // after the instance's last barrier: its row wave read the flag when the instance began.
+        if constexpr (!POL && SPL == 2)
+            if (a.redo_flag) a.redo_flag[inst] = 2;
         if (a.stats) {
             double* so = a.stats + (int64_t)inst * STATS_W;
             so[0] = (double)(it + it0); so[1] = stat; so[2] = feas; so[3] = mu; so[4] = feq; so[5] = fin;
@@ -2669,8 +2680,9 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
     __syncthreads();
     const bool rowwave = wid >= qpb;
     const int slot0 = rowwave ? wid - qpb : wid;
-    // one instance on this slot (both waves of the pair)
-    auto instance = [&](int inst, int slot, int lane) __attribute__((always_inline)) {
+    // one instance on this slot (both waves of the pair); a persistent launch's row wave takes the
+    // ticket of the slot's next instance into the exchange word xnext first
+    auto instance = [&](int inst, int slot, int lane, int xnext) __attribute__((always_inline)) {
         const QpLds L = QpLds::make(N, NX, NU, NP, a.mpad, fpi, LNG, a.sh_hp >= 0,
                                     LNG && a.sh_bnd >= 0, a.H_inst != nullptr);
         real* W = lds + a.shared_doubles + slot * L.total;
@@ -2691,12 +2703,14 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
             }
             wave_sync();
         }
+        if (rowwave && lane == 0)
+            *reinterpret_cast<int*>(W + L.xch + X_NEXT + xnext) = atomicAdd(a.queue, 1) + (int)gridDim.x * qpb;
 #if defined(BQP_EXP_ONLY)   // register-budget diagnostic: one wave's code alone (never run)
-        if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+        if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst, blockIdx.x * qpb + slot0);
         else row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fsi, lds, lane, inst);
 #else
         if (!rowwave)
-            stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+            stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst, blockIdx.x * qpb + slot0);
         else
             row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fsi, lds, lane, inst);
 #endif
@@ -2731,11 +2745,11 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
             wave_sync();
         }
 #if defined(BQP_EXP_ONLY)   // register-budget diagnostic: one wave's code alone (never run)
-        if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+        if (BQP_EXP_ONLY == 1) stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst, inst);
         else row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
 #else
         if (!rowwave)
-            stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst);
+            stage_wave<NX, NU, NP, SPL, POL>(a, W, L, Hs, lane, inst, inst);
         else
             row_wave<NX, NU, NP, BPL, RPL, POL>(a, W, L, Fs, lds, lane, inst);
 #endif
@@ -2747,19 +2761,28 @@ __device__ __forceinline__ void ocp_body(const OcpKernelArgs& a) {
         // ends, and the shared tables are staged once per workgroup lifetime (SURVEY 7 "per-wave
         // early exit with a persistent-kernel work queue"; the C4 iteration counts run from 3 to
         // 42 around a mean of 8.5)
+        //
+        // Barrier alignment: every barrier is workgroup-wide, so the slots of a workgroup advance
+        // barrier by barrier together, and a barrier interval lasts as long as the longest phase
+        // any slot runs in it.  A cold-started instance passes 4 + 6 K + 2 barriers (I0..I3, K
+        // full iterations B0, B2..B6, the last pass B0, B2), a multiple of 6, so an instance that
+        // starts right after its predecessor's last barrier runs its iterations' phases in step
+        // with the other slots' (factor beside factor, solve beside solve).  The hand-over
+        // therefore takes no barrier of its own: the row wave takes the ticket of the slot's next
+        // instance at the start of the current one (before I0, into one of two exchange words
+        // used alternately), and both waves read it after the last barrier.  (A hand-over barrier
+        // shifted every later instance of the slot by one phase: C3 2.83 -> 3.43 ms per launch,
+        // gpurun_out/r06_a.)  Instances continued from the mixed mode's handoff (one barrier
+        // before the loop) are not queued (launch_t).
         int inst = blockIdx.x * qpb + slot0;
+        int par = 0;
         while (inst < a.batch) {
             // the lane and slot made opaque per instance: nothing lane- or slot-dependent is
             // hoisted out of the instance loop into registers carried across instances (the
             // solve phases are at the 256-VGPR budget; opq)
-            real* X = instance(inst, opq_s(slot0), opq(lane_k));
-            // next instance: the stage wave takes a ticket and hands it to its row wave through
-            // the slot's exchange block; one workgroup barrier on each wave of the pair (the other
-            // slots' waves pass it inside their own iterations, as every barrier of this kernel)
-            int* xn = reinterpret_cast<int*>(X + X_NEXT);
-            if (!rowwave && lane_k == 0) *xn = atomicAdd(a.queue, 1) + (int)gridDim.x * qpb;
-            BARRIER();
-            inst = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(xn));
+            real* X = instance(inst, opq_s(slot0), opq(lane_k), par);
+            inst = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(X + X_NEXT + par));
+            par ^= 1;
         }
     }
 }
@@ -2814,7 +2837,7 @@ static hipError_t launch_t(const OcpKernelArgs& a0, int blocks, size_t lds, hipS
     // device at once: the grid is the resident workgroups and the slots pull the remaining
     // instances from a.queue; otherwise one instance per slot (BQP_NO_QUEUE: always, for A/B)
     const bool no_queue = getenv("BQP_NO_QUEUE") != nullptr;
-    if (!pol && !a.redo_flag && a.queue && !no_queue) {
+    if (!pol && !a.redo_flag && !a.hand_in && a.queue && !no_queue) {
         int dev = 0, cus = 0, per_cu = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

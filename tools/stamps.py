@@ -23,19 +23,23 @@ _lib.LIB_PATH = os.environ.get('BQP_STAMPS_LIB') or os.path.join(ROOT, 'learning
 lib = _lib.load()
 lib.bqp_debug_stamps.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, _lib._PD]
 import bench
-g = np.load(os.path.join(ROOT, 'tests', 'golden', 'lmpc_N20.npz'))
 pos = [a for a in sys.argv[1:] if not a.startswith('--')]
 jout = sys.argv[sys.argv.index('--json') + 1] if '--json' in sys.argv else None
-if jout in pos:
-    pos.remove(jout)
-B = int(pos[0]) if pos else 1024
-lm = bench.workload('C2', B, 0, 1)['prob']
-X = g['dx'][np.arange(B) % 1000]
+cfg = sys.argv[sys.argv.index('--config') + 1] if '--config' in sys.argv else 'C2'
+for o in (jout, cfg):
+    if o in pos:
+        pos.remove(o)
+B = int(pos[0]) if pos else {'C2': 1024, 'C3': 4096}[cfg]
+# the config's bench workload (C2: MG N = 20, 616-row terminal set; C3: DI N = 30, 22 rows,
+# per-instance linear terms)
+wl = bench.workload(cfg, B, 0, 1)
+lm, X = wl['prob'], wl['X']
 h = bqp.Handle(0)
-r = bqp.solve_ocp(lm, X, handle=h)
-r = bqp.solve_ocp(lm, X, handle=h)
+kw = {} if wl['w'] is None else dict(w=wl['w'])
+r = bqp.solve_ocp(lm, X, handle=h, **kw)
+r = bqp.solve_ocp(lm, X, handle=h, **kw)
 st = np.zeros((B, 32))
-_lib.check(lib.bqp_debug_stamps(h.value, 20, 6, 616, _lib.ptr(st)), 'stamps')
+_lib.check(lib.bqp_debug_stamps(h.value, lm.N, lm.nx + lm.nu + lm.np, lm.mp, _lib.ptr(st)), 'stamps')
 # STAMP(id) closes phase id; the phase names follow the barrier schedule of bqp_ocp.hip
 stage = ['wait B0 + residual combine', 'combine', 'wait B1', 'decide + factor', 'wait B2',
          'solve pred (post-fwd)', 'wait B3,B4', 'solve corr (post-fwd)', 'wait B5,B6', 'update + partials',
@@ -58,7 +62,7 @@ if jout:
     waits = [i for i, n in enumerate(stage) if n.startswith('wait')]
     sw = st[:, 0:16].sum(axis=1).mean()
     busy = sw - sum(st[:, i].mean() for i in waits)
-    res = {'batch': B, 'kernel_ms_stamp_build': ms, 'iterations_mean': float(it),
+    res = {'config': cfg, 'batch': B, 'kernel_ms_stamp_build': ms, 'iterations_mean': float(it),
            'stage_wave_cycles_per_instance': float(sw),
            'stage_wave_busy_frac': float(busy / sw),
            'stage_wave_cycles_per_iter': float(busy / it),

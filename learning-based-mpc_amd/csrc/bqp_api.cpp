@@ -282,10 +282,18 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         const int shared_doubles = S.doubles;
         const int per_wave = single ? bqp::ocp_wave_lds_doubles_f32(N, nx, nu, np, mpad, fpi, false, S.hpsh, false, hinst)
                                     : bqp::ocp_wave_lds_doubles(N, nx, nu, np, mpad, fpi, S.lng, S.hpsh, S.bndsh, hinst);
-        const size_t lds_budget = 160 * 1024 / (single ? sizeof(float) : sizeof(double));
+        // 160 KB per workgroup less the repair kernel's 256 B of static LDS (its
+        // __syncthreads_or scratch): N = 50 at two instances per workgroup sits exactly there
+        const size_t lds_budget = (160 * 1024 - 256) / (single ? sizeof(float) : sizeof(double));
         // long horizons (N + 1 > 64, two stages per lane) are compiled for <= 256 threads per
         // workgroup: one wave per SIMD, whose 512 registers hold the doubled stage state
         wpb = (N + 1 > 64) ? 2 : 4;
+        // diagnostic (the A/B variants of tools/gpu_r06_*.sh): BQP_OCP_WPB sets the instances per
+        // workgroup the LDS budget then caps
+        if (const char* e = getenv("BQP_OCP_WPB")) {
+            const int v = atoi(e);
+            if (v >= 1 && v <= 8) wpb = v;
+        }
         while (wpb > 1 && (size_t)shared_doubles + (size_t)wpb * per_wave > lds_budget) --wpb;
         return (size_t)shared_doubles + (size_t)per_wave <= lds_budget;
     };

@@ -201,10 +201,13 @@ enum : int {
     X_PCHG,      //         rows an active-set correction would move
     X_PDEC,      //         decision (stage wave): 0 pass, 1 accept, 2 correct the set, 3 give up
     X_CGD,       //         inner step (row wave): 0 CG step, 1 multiplier (AL) step, 2 pass done
-    X_NEXT,      // persistent launch: the slot's next instance (row wave, int bits; two slots
-    X_NEXT1,     //   used alternately by successive instances of the slot)
-    X_NXCH = 22
+    X_NXCH = 20
 };
+// persistent launch (ocp_queue_kernel, never the repair kernel): the slot's next instance, taken
+// by the row wave (int bits; two words used alternately by successive instances of the slot) in
+// two polish-only slots
+constexpr int X_NEXT = X_PVA;
+static_assert(X_PVIOL == X_PVA + 1, "X_NEXT + 1 must be a polish-only slot");
 
 // Per-instance LDS layout (in doubles), sized from N at run time.
 struct QpLds {
@@ -2798,8 +2801,15 @@ template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_polish_kernel(OcpKernelArgs a) {
     ocp_body<NX, NU, NP, SPL, RPL, BPL, true, false>(a);
 }
+#ifndef BQP_DI_OCC3
+#define BQP_DI_OCC3 0
+#endif
+// A/B variant (make ab VFLAGS=-DBQP_DI_OCC3=1; host: BQP_OCP_WPB=5): the DI queue kernel with five
+// instances per workgroup (145 KB of LDS) and three waves per SIMD (168 VGPRs) - VERDICT r5 item 4
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
-__global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_queue_kernel(OcpKernelArgs a) {
+__global__ void __launch_bounds__(SPL == 2 ? 256 : ((BQP_DI_OCC3 && NX == 2) ? 640 : 512),
+                                  (BQP_DI_OCC3 && NX == 2 && SPL == 1) ? 3 : 1)
+ocp_queue_kernel(OcpKernelArgs a) {
     ocp_body<NX, NU, NP, SPL, RPL, BPL, false, true>(a);
 }
 
@@ -2822,6 +2832,18 @@ __global__ void __launch_bounds__(SPL == 2 ? 256 : 512) ocp_queue_kernel(OcpKern
 #define BQP_FAM_DI 1
 #endif
 
+// dynamic LDS of a launch: the kernel's static LDS must fit beside it (a launch past 160 KB is
+// refused up front, and a failed attribute call does not leave a stale error for the next launch)
+static hipError_t lds_attr(const void* k, size_t lds) {
+    hipFuncAttributes fa;
+    hipError_t e = hipFuncGetAttributes(&fa, k);
+    if (e == hipSuccess && lds + fa.sharedSizeBytes > 160 * 1024) e = hipErrorInvalidValue;
+    if (e == hipSuccess && lds > 64 * 1024)
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
+}
+
 template <int NX, int NU, int NP, int SPL, int RPL, int BPL>
 static hipError_t launch_t(const OcpKernelArgs& a0, int blocks, size_t lds, hipStream_t st, bool pol) {
 #ifdef BQP_F32
@@ -2841,8 +2863,7 @@ static hipError_t launch_t(const OcpKernelArgs& a0, int blocks, size_t lds, hipS
         int dev = 0, cus = 0, per_cu = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (lds > 64 * 1024 && e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)kq, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e == hipSuccess) e = lds_attr((const void*)kq, lds);
         if (e == hipSuccess)
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kq, 128 * a.wpb, lds);
         if (e != hipSuccess) return e;
@@ -2853,10 +2874,7 @@ static hipError_t launch_t(const OcpKernelArgs& a0, int blocks, size_t lds, hipS
         }
     }
     a.queue = nullptr;
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
+    if (hipError_t e = lds_attr((const void*)k, lds)) return e;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(128 * a.wpb), lds, st, a);
     return hipGetLastError();
 }

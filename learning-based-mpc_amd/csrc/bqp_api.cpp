@@ -50,7 +50,8 @@ struct bqp_handle_s {
     DevBuf pwork;  // long-horizon layout: global Riccati tables
     DevBuf wwork;  // per-instance stage-cost tables
     int last_batch = 0;
-    int* mixed_flags = nullptr;   // the last mixed-mode solve's fp32-phase flags (2: redone cold)
+    int* mixed_flags = nullptr;   // the last mixed-mode solve's fp32-phase flags
+    int* mixed_cont = nullptr;    // and its continuation's exit flags (bqp_debug_mixed_flags)
     int mixed_batch = 0;
 };
 
@@ -176,7 +177,15 @@ int bqp_debug_mixed_flags(bqp_handle h, int batch, int* flags) {
     if (!h->mixed_flags || batch != h->mixed_batch) return BQP_E_ARG;
     DevScope ds(h->device);
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(flags, h->mixed_flags, sizeof(int) * batch, hipMemcpyDeviceToHost));
+    std::vector<int> f2((size_t)2 * batch);
+    HIP_TRY(hipMemcpy(f2.data(), h->mixed_flags, sizeof(int) * batch, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(f2.data() + batch, h->mixed_cont, sizeof(int) * batch, hipMemcpyDeviceToHost));
+    // the retry launch solved again the instances whose continuation ended != 1 after a warm
+    // start (fp32-phase flag 0 / 1): reported as 2
+    for (int i = 0; i < batch; ++i) {
+        const int hf = f2[i], c2 = f2[(size_t)batch + i];
+        flags[i] = ((hf == 0 || hf == 1) && c2 != 1) ? 2 : hf;
+    }
     return BQP_OK;
 }
 
@@ -363,11 +372,13 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         const int hf = bqp::ocp_hand_floats(N, nx, nu, np, mp);
         if (hf <= 0) return BQP_E_UNSUPPORTED;
         const size_t hrec = ((size_t)hf + 63) & ~(size_t)63;
-        HIP_TRY(h->hwork.reserve(sizeof(float) * hrec * batch + 2 * sizeof(int) * (size_t)batch));
+        HIP_TRY(h->hwork.reserve(sizeof(float) * hrec * batch + 3 * sizeof(int) * (size_t)batch));
         float* hb = (float*)h->hwork.p;
         int* hflag = (int*)(hb + hrec * batch);
         int* hit = hflag + batch;
+        int* c2flag = hit + batch;    // the continuation's exit flags (diagnostic)
         h->mixed_flags = hflag;
+        h->mixed_cont = c2flag;
         h->mixed_batch = batch;
         bqp::OcpKernelArgs a1 = a;
         a1.wpb = wpb32;
@@ -382,6 +393,8 @@ int bqp_solve_ocp_batched_device(bqp_handle h, const bqp_ocp_dims* d, int batch,
         // phase 2: fp64 from the handed-over iterates
         a.hand_in = hb; a.hand_flag = hflag; a.hand_it = hit; a.hand_stride = (int64_t)hrec;
         HIP_TRY(bqp::launch_ocp(a, nx, nu, np, st));
+        // (diagnostic record of the continuation's exit flags, for bqp_debug_mixed_flags)
+        HIP_TRY(hipMemcpyAsync(c2flag, exitflag, sizeof(int) * batch, hipMemcpyDeviceToDevice, st));
         // phase 3: a continuation that did not converge (-8 / -2 / 0: marginal instances, e.g.
         // nearly infeasible perturbed models) is solved again from the fp64 initial point, so
         // the mixed mode reports the fp64 solve's status there; the others leave at once

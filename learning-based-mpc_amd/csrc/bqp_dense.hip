@@ -552,14 +552,16 @@ __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int c16 = lane & 15, k4 = lane >> 4;
     const int nbk = (n + 15) >> 4;
+    // D: the diagonal tile J by its owner (wave J % 4, slot J / 4): the 16 pivots, L_JJ to LDS, the
+    // reciprocal pivots and the fail flag to rv
+    auto dfac = [&](int J) __attribute__((always_inline)) {
+        bool ok = true;
+        if (J < 4) ok = dtile(acc[0], J, K, n, fl, rv, lane, k4, c16);
+        else       ok = dtile(acc[1], J, K, n, fl, rv, lane, k4, c16);
+        if (lane == 0) rv[16] = ok ? 0.0 : 1.0;
+    };
+    if (wv == 0) dfac(0);
     for (int J = 0; J < nbk; ++J) {
-        // ---- D: the diagonal tile, by its owner (wave J % 4, slot J / 4) ----
-        if ((J & 3) == wv) {
-            bool ok = true;
-            if (J < 4) ok = dtile(acc[0], J, K, n, fl, rv, lane, k4, c16);
-            else       ok = dtile(acc[1], J, K, n, fl, rv, lane, k4, c16);
-            if (lane == 0) rv[16] = ok ? 0.0 : 1.0;
-        }
         TST(12);
         __syncthreads();
         TST(13);
@@ -587,9 +589,14 @@ __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW]
         __syncthreads();
         TST(15);
         // ---- U: every tile (I, K), K > J: K_IK -= L_IJ L_KJ' on the matrix cores ----
-#pragma unroll
-        for (int u = 0; u < TPW; ++u) {
-            if (tI[u] < 0 || tJ[u] <= J) continue;
+        // Lookahead (round 6): the diagonal tiles (slots 0, 1) first; the owner of tile J + 1 then
+        // factors it (D of the next block column) while the other waves are still updating their
+        // off-diagonal tiles, instead of all waves waiting at the next barrier for the diagonal
+        // pivot chain.  Each tile takes the same operations in the same order as before (the
+        // factor is bitwise the same); D writes block (J + 1, J + 1) of K and rv, which the
+        // remaining updates of column J do not read.
+        auto upd = [&](int u) __attribute__((always_inline)) {
+            if (tI[u] < 0 || tJ[u] <= J) return;
             const int rA = 16 * tI[u] + c16, rB = 16 * tJ[u] + c16;
             double av[4], bv[4];
 #pragma unroll
@@ -601,7 +608,12 @@ __device__ __forceinline__ bool tile_chol(dbl4 (&acc)[TPW], const int (&tI)[TPW]
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4)
                 acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc[u], 0, 0, 0);
-        }
+        };
+        upd(0);
+        if constexpr (TPW > 1) upd(1);
+        if (((J + 1) & 3) == wv) dfac(J + 1);
+#pragma unroll
+        for (int u = 2; u < TPW; ++u) upd(u);
         TST(16);
     }
     __syncthreads();
@@ -726,6 +738,62 @@ __device__ __forceinline__ void chol_solve_w_body(const double* L, int n, double
     }
     __syncthreads();
 }
+// The same substitutions on all four waves of the workgroup (round 6; dense_ipm_kernel with the
+// factor in LDS, n <= 256): wave w keeps entry l + 64 w of lane l in a register.  Block b's
+// 16-step chain runs in its owner wave (w = b / 4, the 16-lane row b % 4), which publishes the
+// solved block through LDS; after one workgroup barrier every wave applies the block to its own
+// entries.  One chain per block on the critical path and the 16-column updates spread over 256
+// lanes instead of four entries per lane on wave 0 while three waves idled; each entry receives
+// the same updates in the same order as in chol_solve_w_body (bitwise the same solution).
+__device__ __forceinline__ void chol_solve_wg(const double* L, int n, double* xs) {
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, jl = l & 15, rw = l >> 4;
+    const int e = l + 64 * w;
+    double xr = (e < n) ? xs[e] : 0.0;
+    const int ek = min(e, n - 1);
+    const double dr = 1.0 / L[(int64_t)ek * n + ek];       // the pivots' reciprocals
+    const int nb = (n + 15) >> 4;
+    for (int pass = 0; pass < 2; ++pass) {
+        const bool fwd = pass == 0;
+        for (int bi = 0; bi < nb; ++bi) {
+            const int b = fwd ? bi : nb - 1 - bi;
+            const int e0 = 16 * b;
+            if (w == (b >> 2)) {                               // wave-uniform: the block's owner
+                const bool inrow = rw == (b & 3);
+                double xv = xr;
+                double lc[16];
+                const int ec = min(e0 + jl, n - 1);
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj) lc[jj] = L[(int64_t)min(e0 + jj, n - 1) * n + ec];
+                double lcs[16];
+                tri_coef<0>(lcs, lc, dr, jl, inrow, n - e0, fwd);
+                if (fwd) tri_blk<0, true>(xv, lcs);
+                else     tri_blk<0, false>(xv, lcs);
+                if (inrow) xv *= dr;
+                xr = xv;
+                if (inrow) xs[e0 + jl] = xv;                    // publish the block
+            }
+            __syncthreads();
+            double xb[16];
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {                   // unconditional loads (clamped), then the select
+                const double v = xs[min(e0 + jj, n - 1)];
+                xb[jj] = (e0 + jj < n) ? v : 0.0;
+            }
+            const bool upd = e < n && (fwd ? e >= e0 + 16 : e < e0);
+            if (upd) {
+                double ac4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int jj = 0; jj < 16; ++jj)
+                    ac4[jj & 3] = fma(L[(int64_t)min(e0 + jj, n - 1) * n + e], xb[jj], ac4[jj & 3]);
+                xr -= (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
+            }
+        }
+        __syncthreads();                                        // the passes publish the same slots
+    }
+    if (e < n) xs[e] = xr;
+    __syncthreads();
+}
+
 // the called form (factor / vector in global memory or generic pointers); dense_ipm_kernel's
 // factor in LDS inlines the body, so that L and xs are ds_* accesses (the call made them flat
 // loads, ~4 solve-phase round trips slower per block)
@@ -1625,7 +1693,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         for (int j = tid; j < n; j += DT) xs[j] = -q[j];
         __syncthreads();
         DST(8);
-        if constexpr (KL) chol_solve_w_body(K, n, xs TSW_PASS);
+        if constexpr (KL) chol_solve_wg(K, n, xs);
         else chol_solve_w(K, n, xs);
         DST(8);
         for (int j = tid; j < n; j += DT) w[j] = xs[j];

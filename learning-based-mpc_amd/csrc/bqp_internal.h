@@ -45,7 +45,7 @@ struct OcpKernelArgs {
     // third launch of the mixed mode (cold fp64): only the instances whose warm continuation
     // did not converge (exitflag != 1 with a warm hand_flag) are solved again from the fp64
     // initial point; every other instance leaves at once
-    int* redo_flag;         // (phase 3 sets 2 for the instances it solved again; bqp_debug_mixed_flags)
+    const int* redo_flag;
     // per-instance polytope (bqp_ocp_data.sFp != 0): the caller's column-major n_poly x nv
     // blocks, stride sFp; the shared Fp table is then unused
     const double* Fp_inst;

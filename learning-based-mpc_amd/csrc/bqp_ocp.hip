@@ -1469,12 +1469,6 @@ __device__ __forceinline__ void stage_wave(const OcpKernelArgs& a, real* W, cons
     if (lane == 0) {
         if (a.fval) a.fval[inst] = fv;
         a.exitflag[inst] = flag;
-        // mixed mode, cold retry launch: mark the instance as solved again from the fp64 start
-        // (its fp32-phase flag 0 / 1 becomes 2), so that the repair launch starts it cold too
-        // (hand_warm) and bqp_debug_mixed_flags can tell which instances phase 3 redid.  Written
-        // after the instance's last barrier: its row wave read the flag when the instance began.
-        if constexpr (!POL && SPL == 2)
-            if (a.redo_flag) a.redo_flag[inst] = 2;
         if (a.stats) {
             double* so = a.stats + (int64_t)inst * STATS_W;
             so[0] = (double)(it + it0); so[1] = stat; so[2] = feas; so[3] = mu; so[4] = feq; so[5] = fin;

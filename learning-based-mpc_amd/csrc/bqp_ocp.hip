@@ -134,32 +134,43 @@ __device__ __forceinline__ int opq_s(int v) {
 __device__ __forceinline__ double fmar(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float fmar(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
+// Factor of a small SPD block for chol_solve_small (R^_k = M_uu per stage in the Riccati
+// recursion, P_0[theta, theta] once per factorisation).  n = 2 (the DI model family): LDL' with
+// the reciprocal pivots stored, L row-major = [1/d0, 0, l10, 1/d1] (round 6): no square root and
+// two divisions on the recursion's per-stage chain instead of two square roots and five divisions
+// (the DI factor was 40 % of the stage wave's cycles, profiles/stamps_C3.json); still a
+// factorisation applied by substitution (oracle/cpu_ipm.c spd_fac / spd_solve, same operations),
+// with the same static pivot floor on the same pivots d0 = M00, d1 = M11 - M10^2 / M00.
 template <int N>
 __device__ __forceinline__ bool chol_small(const real (&M)[N][N], real (&L)[N][N]) {
     bool ok = true;
     real d0 = M[0][0];
     if (!(d0 > PIV_FLOOR * M[0][0])) d0 = PIV_FLOOR * M[0][0];
     ok = ok && (d0 > 0.0);
-    L[0][0] = sqrt(d0);
     if constexpr (N == 2) {
-        L[0][1] = 0.0;
-        L[1][0] = M[1][0] / L[0][0];
-        real d1 = M[1][1] - L[1][0] * L[1][0];
+        const real r0 = real(1) / d0;
+        const real l10 = M[1][0] * r0;
+        real d1 = M[1][1] - l10 * M[1][0];
         if (!(d1 > PIV_FLOOR * M[1][1])) d1 = PIV_FLOOR * M[1][1];
         ok = ok && (d1 > 0.0);
-        L[1][1] = sqrt(d1);
+        L[0][0] = r0;
+        L[0][1] = 0.0;
+        L[1][0] = l10;
+        L[1][1] = real(1) / d1;
+    } else {
+        L[0][0] = sqrt(d0);
     }
     return ok;
 }
-// b <- M^{-1} b with M = L L' (substitution, same order as oracle/cpu_ipm.c spd_solve); L row-major.
-// For n = 1 the factor slot holds 1/M instead (one reciprocal, no square root).
+// b <- M^{-1} b from chol_small's factor (n = 2: L z = b, D w = z, L' x = w; same order as
+// oracle/cpu_ipm.c spd_solve); L row-major.  For n = 1 the factor slot holds 1/M instead (one
+// reciprocal, no square root).
 template <int N>
 __device__ __forceinline__ void chol_solve_small(const real* L, real (&b)[N]) {
     if constexpr (N == 2) {
-        b[0] = b[0] / L[0];
-        b[1] = (b[1] - L[2] * b[0]) / L[3];
-        b[1] = b[1] / L[3];
-        b[0] = (b[0] - L[2] * b[1]) / L[0];
+        const real w1 = (b[1] - L[2] * b[0]) * L[3];
+        b[0] = b[0] * L[0] - L[2] * w1;
+        b[1] = w1;
     } else {
         b[0] = b[0] * L[0];
     }

@@ -112,6 +112,20 @@ static int spd_fac(int n, const double* M, double* L) {
         L[0] = 1.0 / M[0];
         return 0;
     }
+    if (n == 2) {
+        /* LDL' with the reciprocal pivots stored, L = [1/d0, 0, l10, 1/d1] (the kernel's
+         * chol_small, round 6: no square roots on the Riccati recursion's per-stage chain) */
+        double d0 = M[0];
+        if (!(d0 > PIV_FLOOR * M[0])) d0 = PIV_FLOOR * M[0];
+        if (!(d0 > 0)) return -1;
+        const double r0 = 1.0 / d0;
+        const double l10 = M[2] * r0;
+        double d1 = M[3] - l10 * M[2];
+        if (!(d1 > PIV_FLOOR * M[3])) d1 = PIV_FLOOR * M[3];
+        if (!(d1 > 0)) return -1;
+        L[0] = r0; L[1] = 0.0; L[2] = l10; L[3] = 1.0 / d1;
+        return 0;
+    }
     for (int i = 0; i < n * n; ++i) L[i] = 0.0;
     for (int j = 0; j < n; ++j) {
         double d = M[j * n + j];
@@ -134,6 +148,12 @@ static void spd_solve(int n, const double* L, double* b) {
     /* b <- M^{-1} b from spd_fac's factor */
     if (n == 1) {
         b[0] = b[0] * L[0];
+        return;
+    }
+    if (n == 2) {
+        const double w1 = (b[1] - L[2] * b[0]) * L[3];
+        b[0] = b[0] * L[0] - L[2] * w1;
+        b[1] = w1;
         return;
     }
     for (int i = 0; i < n; ++i) {

@@ -29,6 +29,7 @@ namespace bqp {
 #define DT 256
 #define TILE 32
 #define DQ_THL 256   // A row-tile bounds kept in LDS (m <= 8192 rows)
+#define DQ_RPT 4     // rows per thread of the register-resident row state (m <= DQ_RPT * DT)
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_PIV_FLOOR 1e-14    // static pivot floor of K, relative to its largest diagonal entry
 #define DQ_CONVEX_EPS 1e-10   // shift of the convexity test (relative)
@@ -1055,6 +1056,7 @@ __host__ __device__ inline int dense_gbuf(int n) { return DQ_GB * (n + 2); }
 // when both buffers and the factor fit in LDS; otherwise the single row-major tile
 // (every budget below counts the reduction scratch and the tile bounds, DQ_TAIL doubles at the end)
 #define DQ_TAIL (48 + DQ_THL)
+#define DQ_NVEC 17   // n-vectors of dense_ipm_kernel RG in LDS (5 of n, 6 of 2n)
 __host__ __device__ inline bool dense_glds(int n) {
     const int a = TILE * dense_ts(n), b = 2 * dense_gbuf(n);
     return n <= 128 && (size_t)((a > b ? a : b) + n * n + DQ_TAIL) * sizeof(double) <= DENSE_LDS_MAX;
@@ -1074,9 +1076,10 @@ __host__ __device__ inline size_t dense_lds_bytes(int n) {
     return sizeof(double) * (size_t)(dense_tiles(n) + (dense_k_lds(n) ? n * n : 0) + DQ_TAIL);
 }
 
-template <bool KL>   // KL: the factor lives in LDS (dense_k_lds(n)); a compile-time choice so that
+template <bool KL,    // KL: the factor lives in LDS (dense_k_lds(n)); a compile-time choice so that
                      // every access to it is a ds_* instruction (a run-time select made the pointer
                      // generic: flat accesses, ~5k cycles per Cholesky pivot)
+          bool RG>   // RG: the row state in registers, the n-vectors in LDS (dense_rows_in_regs)
 __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const int inst = blockIdx.x;
     if (inst >= a.batch || (a.skip && a.skip[inst])) return;
@@ -1099,10 +1102,34 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     const double* e = a.beq ? a.beq + (int64_t)inst * a.sbeq : nullptr;
     const double* lb = a.lb ? a.lb + (int64_t)inst * a.slb : nullptr;
     const double* ub = a.ub ? a.ub + (int64_t)inst * a.sub : nullptr;
-    double *z = W + L.z, *y = W + L.y, *q = W + L.q, *w = W + L.w, *dz = W + L.dz, *dy = W + L.dy;
-    double *rd = W + L.rd, *re = W + L.re;
+    // RG: the n-vectors of the iteration and the bound rows in LDS as well, after the tail (DQ_NVEC
+    // n doubles: z, q, w, dz, rd, then tB, lB, riB, rcB, dtB, dlB of 2n each); the repair launch's
+    // start (z, tB, lB) is copied to the workspace at the end
+    double* vb = dlds + dense_tiles(n) + (KL ? n * n : 0) + DQ_TAIL;
+    double *z = RG ? vb : W + L.z, *y = W + L.y, *q = RG ? vb + n : W + L.q, *w = RG ? vb + 2 * n : W + L.w;
+    double *dz = RG ? vb + 3 * n : W + L.dz, *dy = W + L.dy;
+    double *rd = RG ? vb + 4 * n : W + L.rd, *re = W + L.re;
     double *tA = W + L.tA, *lA = W + L.lA, *riA = W + L.riA, *rcA = W + L.rcA, *dtA = W + L.dtA, *dlA = W + L.dlA;
-    double *tB = W + L.tB, *lB = W + L.lB, *riB = W + L.riB, *rcB = W + L.rcB, *dtB = W + L.dtB, *dlB = W + L.dlB;
+    double *tB = RG ? vb + 5 * n : W + L.tB, *lB = RG ? vb + 7 * n : W + L.lB, *riB = RG ? vb + 9 * n : W + L.riB;
+    double *rcB = RG ? vb + 11 * n : W + L.rcB, *dtB = RG ? vb + 13 * n : W + L.dtB, *dlB = RG ? vb + 15 * n : W + L.dlB;
+    // the row state of the m rows of A - slack t, multiplier lam, residual ri, complementarity rc,
+    // the direction dt, dlam - in registers when RG (round 6): row r = tid + DT i in slot i, the
+    // mapping of every row pass below; otherwise in the instance's workspace.  In the workspace
+    // it was rewritten every iteration and left L2 for HBM (135 MB of writes per 128-instance
+    // launch of the learned loop's sub-problem, profiles/pmc_CLL.json of round 5).  The row
+    // weights of the A'DA tiles (another mapping) are formed by the threads that hold the rows.
+    constexpr int RPT = RG ? DQ_RPT : 1;
+    double tAr[RPT], lAr[RPT], riAr[RPT], rcAr[RPT], dtAr[RPT], dlAr[RPT];
+#define TA(i, r) (RG ? tAr[RG ? (i) : 0] : tA[r])
+#define LA(i, r) (RG ? lAr[RG ? (i) : 0] : lA[r])
+#define RIA(i, r) (RG ? riAr[RG ? (i) : 0] : riA[r])
+#define RCA(i, r) (RG ? rcAr[RG ? (i) : 0] : rcA[r])
+#define DTA(i, r) (RG ? dtAr[RG ? (i) : 0] : dtA[r])
+#define DLA(i, r) (RG ? dlAr[RG ? (i) : 0] : dlA[r])
+    // the rows of this thread: slot i, row r (unrolled over the DQ_RPT slots when RG)
+#define DQ_ROWS(i, r) \
+    _Pragma("unroll") for (int i = 0; RG ? (i < RPT) : (tid + i * DT < m); ++i) \
+        if (const int r = tid + i * DT; !RG || r < m)
     double* K = KL ? dlds + dense_tiles(n) : W + L.K;   // the factor (LDS when it fits)
     double* Y = W + L.Y;
     double* S = W + L.S;
@@ -1178,8 +1205,8 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     // (coalesced along the rows of column-major A, as the factorisation does), thread j < n
     // accumulating column j from LDS; the column loops over all m rows that one thread per
     // column ran before touched 64 cache lines per wave load (m = 1024: ~0.5 ms per product)
-    auto atw = [&](auto&& wfun) -> double {
-        if (m + n <= TILE * ts) {
+    auto atw = [&](auto&& wfun) __attribute__((always_inline)) -> double {
+        if (RG || m + n <= TILE * ts) {   // (RG: the host checked that it fits)
             // the row weights into LDS once; wave wv takes column groups 16 g (g = wv, wv + 4,
             // ..): lanes over rows, 16 independent loads per row step, one transposed wave sum
             // (wsum_t) per group; no tile barriers (the tile version waited on a load round
@@ -1187,7 +1214,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             double* wl = tileA;
             double* out = tileA + m;
             __syncthreads();
-            for (int r = tid; r < m; r += DT) wl[r] = wfun(r);
+            DQ_ROWS(i, r) wl[r] = wfun(i, r);
             __syncthreads();
             const int lane = tid & 63, wv = tid >> 6;
             for (int g = wv; 16 * g < n; g += DT / 64) {
@@ -1228,7 +1255,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             const int rows = min(TILE, m - r0);
             __syncthreads();
             load_tile(r0, rows, n);
-            if (tid < rows) tileA[tid * ts + tw] = wfun(r0 + tid);
+            if (tid < rows) tileA[tid * ts + tw] = wfun(0, r0 + tid);
             __syncthreads();
             if (tid < n)
                 for (int rr = 0; rr < rows; ++rr) acc += tileA[rr * ts + tid] * tileA[rr * ts + tw];
@@ -1262,15 +1289,15 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 
     // ---------------------------------------------------------------- residuals
     auto residuals = [&](double& stat, double& feq, double& fin, double& csum, double& gscale, double& zmax,
-                         double& cmax) {
+                         double& cmax) __attribute__((always_inline)) {
         double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, gs = 0.0, zm = 0.0, cm = 0.0;
         stage_v(z);
-        for (int r = tid; r < m; r += DT) {
-            const double v = tA[r] - b[r] + arow(r);
-            riA[r] = v;
+        DQ_ROWS(i, r) {
+            const double v = TA(i, r) - b[r] + arow(r);
+            RIA(i, r) = v;
             fe = fmax(fe, fabs(v));
-            cs += tA[r] * lA[r];
-            cm = fmax(cm, tA[r] * lA[r]);
+            cs += TA(i, r) * LA(i, r);
+            cm = fmax(cm, TA(i, r) * LA(i, r));
         }
         // f + H z (z from vlds; row j of H read across the lanes - coalesced, H symmetric as
         // the factorisation assumes; 16 loads in flight) into rd, completed below
@@ -1293,7 +1320,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             re[r] = v;
             fq = fmax(fq, fabs(v));
         }
-        const double alam = atw([&](int r) { return lA[r]; });   // (A' lam)_tid
+        const double alam = atw([&](int i, int r) { return LA(i, r); });   // (A' lam)_tid
         DST(10);
         for (int j = tid; j < n; j += DT) {
             double v = rd[j];
@@ -1338,13 +1365,13 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
     // if they do not pass).  gscale (max |f + H z|, the stationarity tolerance's scale) keeps its
     // last exact value.
     auto scaled_residuals = [&](double s, double& stat, double& feq, double& fin, double& csum, double& zmax,
-                                double& cmax) {
+                                double& cmax) __attribute__((always_inline)) {
         double fe = 0.0, fq = 0.0, cs = 0.0, st = 0.0, zm = 0.0, cm = 0.0;
-        for (int r = tid; r < m; r += DT) {
-            const double v = s * riA[r];
-            riA[r] = v;
+        DQ_ROWS(i, r) {
+            const double v = s * RIA(i, r);
+            RIA(i, r) = v;
             fe = fmax(fe, fabs(v));
-            const double c = tA[r] * lA[r];
+            const double c = TA(i, r) * LA(i, r);
             cs += c;
             cm = fmax(cm, c);
         }
@@ -1447,8 +1474,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 double* gb1 = dlds + dense_gbuf(n);
                 double aw = 0.0;
                 {
+                    // rows 0 .. TILE - 1: threads 0 .. TILE - 1, slot 0 (RG)
                     const int rd0 = min(tid, min(TILE, m) - 1);
-                    const double la = lA[rd0], ta = tA[rd0], ri = riA[rd0];
+                    const double la = RG ? lAr[0] : lA[rd0], ta = RG ? tAr[0] : tA[rd0], ri = RG ? riAr[0] : riA[rd0];
                     issue(0, gb0);
                     if (tid < TILE) {
                         const bool in = tid < min(TILE, m);
@@ -1465,9 +1493,17 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                     const bool more = t + 1 < ntile;
                     double la = 1.0, ta = 1.0, ri = 0.0;
                     const int rows1 = more ? min(TILE, m - r0 - TILE) : 0;
+                    // RG: the rows of tile t + 1 are held by threads wb .. wb + TILE - 1 (slot s1)
+                    const int wb = (r0 + TILE) % DT, s1 = (r0 + TILE) / DT, tl = RG ? tid - wb : tid;
                     if (more) {
-                        const int rd1 = r0 + TILE + min(tid, rows1 - 1);
-                        la = lA[rd1]; ta = tA[rd1]; ri = riA[rd1];
+                        if constexpr (RG) {
+#pragma unroll
+                            for (int i = 0; i < RPT; ++i)
+                                if (i == s1) { la = lAr[i]; ta = tAr[i]; ri = riAr[i]; }
+                        } else {
+                            const int rd1 = r0 + TILE + min(tid, rows1 - 1);
+                            la = lA[rd1]; ta = tA[rd1]; ri = riA[rd1];
+                        }
                         issue(t + 1, nxt);
                     }
                     DSTN(21);
@@ -1514,9 +1550,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                         aw += s0 + s1;
                     }
                     DSTN(22);
-                    if (more && tid < TILE) {
-                        nxt[DQ_GB * n + tid] = tid < rows1 ? la / ta : 0.0;
-                        nxt[DQ_GB * (n + 1) + tid] = tid < rows1 ? (la * ri - ta * la) / ta : 0.0;
+                    if (more && tl >= 0 && tl < TILE) {
+                        nxt[DQ_GB * n + tl] = tl < rows1 ? la / ta : 0.0;
+                        nxt[DQ_GB * (n + 1) + tl] = tl < rows1 ? (la * ri - ta * la) / ta : 0.0;
                     }
                     copy_wait();
                     DSTN(23);
@@ -1530,7 +1566,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 aq_ok = true;
                 __syncthreads();
             }
-            for (int r0 = 0; r0 < (gl ? 0 : m); r0 += TILE) {
+            for (int r0 = 0; r0 < ((RG || gl) ? 0 : m); r0 += TILE) {
                 const int rows = min(TILE, m - r0);
                 __syncthreads();
                 // only the columns the tile's rows reach, to the 16-column block (the MFMA operands
@@ -1601,7 +1637,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             }
             DST(2);
         }
-        for (int base = 0; base < (n <= 128 ? 0 : ne); base += DT * 8) {
+        for (int base = 0; base < ((RG || n <= 128) ? 0 : ne); base += DT * 8) {
             double acc[8];
             int ii[8], jj[8];
 #pragma unroll
@@ -1676,11 +1712,11 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 
     // ---------------------------------------------------------------- solve (rc given)
     double* xs = tileA;  // LDS vector workspace (n <= 256 and me <= 256)
-    auto solve = [&]() {
+    auto solve = [&]() __attribute__((always_inline)) {
         // q = rd + A'((lam riA - rcA)/tA) + bound terms ; w = -K^{-1} q
         DST(3);
         // the first solve after a factorisation (rc = t lam) takes the A' w formed with A'DA
-        const double aq = aq_ok ? aq_pre : atw([&](int r) { return (lA[r] * riA[r] - rcA[r]) / tA[r]; });
+        const double aq = aq_ok ? aq_pre : atw([&](int i, int r) { return (LA(i, r) * RIA(i, r) - RCA(i, r)) / TA(i, r); });
         aq_ok = false;
         DST(7);
         for (int j = tid; j < n; j += DT) {
@@ -1716,10 +1752,10 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             dz[j] = v;
         }
         stage_v(dz);
-        for (int r = tid; r < m; r += DT) {
+        DQ_ROWS(i, r) {
             const double v = arow(r);
-            dtA[r] = -riA[r] - v;
-            dlA[r] = (-rcA[r] - lA[r] * dtA[r]) / tA[r];
+            DTA(i, r) = -RIA(i, r) - v;
+            DLA(i, r) = (-RCA(i, r) - LA(i, r) * DTA(i, r)) / TA(i, r);
         }
         for (int j = tid; j < n; j += DT) {
             dtB[j] = dlB[j] = dtB[n + j] = dlB[n + j] = 0.0;
@@ -1730,10 +1766,10 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         DST(9);
     };
 
-    auto max_step = [&]() -> double {
+    auto max_step = [&]() __attribute__((always_inline)) -> double {
         double al = 1.0;
 #define DQ_RATIO(v, dv) if ((dv) < 0.0) al = fmin(al, -(v) / (dv));
-        for (int r = tid; r < m; r += DT) { DQ_RATIO(tA[r], dtA[r]); DQ_RATIO(lA[r], dlA[r]); }
+        DQ_ROWS(i, r) { DQ_RATIO(TA(i, r), DTA(i, r)); DQ_RATIO(LA(i, r), DLA(i, r)); }
         for (int j = tid; j < n; j += DT) {
             if (up_present(j)) { DQ_RATIO(tB[j], dtB[j]); DQ_RATIO(lB[j], dlB[j]); }
             if (lo_present(j)) { DQ_RATIO(tB[n + j], dtB[n + j]); DQ_RATIO(lB[n + j], dlB[n + j]); }
@@ -1741,9 +1777,9 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
 #undef DQ_RATIO
         return red.min(al);
     };
-    auto comp_after = [&](double al) -> double {
+    auto comp_after = [&](double al) __attribute__((always_inline)) -> double {
         double c = 0.0;
-        for (int r = tid; r < m; r += DT) c += (tA[r] + al * dtA[r]) * (lA[r] + al * dlA[r]);
+        DQ_ROWS(i, r) c += (TA(i, r) + al * DTA(i, r)) * (LA(i, r) + al * DLA(i, r));
         for (int j = tid; j < n; j += DT) {
             if (up_present(j)) c += (tB[j] + al * dtB[j]) * (lB[j] + al * dlB[j]);
             if (lo_present(j)) c += (tB[n + j] + al * dtB[n + j]) * (lB[n + j] + al * dlB[n + j]);
@@ -1762,7 +1798,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         if (!lo_present(j)) rcB[n + j] = 0.0;
     }
     for (int r = tid; r < me; r += DT) y[r] = 0.0;
-    for (int r = tid; r < m; r += DT) { tA[r] = 1.0; lA[r] = 1.0; rcA[r] = 1.0; }
+    DQ_ROWS(i, r) { TA(i, r) = 1.0; LA(i, r) = 1.0; RCA(i, r) = 1.0; RIA(i, r) = 0.0; DTA(i, r) = 0.0; DLA(i, r) = 0.0; }
     // bound rows take part in the unit-scaled start like the structured kernel (lam = 1)
     for (int j = tid; j < n; j += DT) {
         if (up_present(j)) lB[j] = 1.0;
@@ -1822,7 +1858,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         double tmin = INFINITY, tmax = -INFINITY;
         for (int j = tid; j < n; j += DT) z[j] += dz[j];
         for (int r = tid; r < me; r += DT) y[r] += dy[r];
-        for (int r = tid; r < m; r += DT) { const double t = 1.0 + dtA[r]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
+        DQ_ROWS(i, r) { const double t = 1.0 + DTA(i, r); tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
         for (int j = tid; j < n; j += DT) {
             if (up_present(j)) { const double t = 1.0 + dtB[j]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
             if (lo_present(j)) { const double t = 1.0 + dtB[n + j]; tmin = fmin(tmin, t); tmax = fmax(tmax, t); }
@@ -1831,7 +1867,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         tmax = red.max(tmax);
         const double shp = (tmin <= 0.0) ? 1.0 - tmin : 0.0;
         const double shd = (tmax >= 0.0) ? 1.0 + tmax : 0.0;
-        for (int r = tid; r < m; r += DT) { const double t = 1.0 + dtA[r]; tA[r] = t + shp; lA[r] = -t + shd; }
+        DQ_ROWS(i, r) { const double t = 1.0 + DTA(i, r); TA(i, r) = t + shp; LA(i, r) = -t + shd; }
         for (int j = tid; j < n; j += DT) {
             const double tu = 1.0 + dtB[j], tl = 1.0 + dtB[n + j];
             tB[j] = up_present(j) ? tu + shp : 1.0; lB[j] = up_present(j) ? -tu + shd : 0.0;
@@ -1875,7 +1911,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             mu_min = fmin(mu_min, mu);
             if (it == a.max_iter) break;
             if (!factor()) { flag = -8; break; }
-            for (int r = tid; r < m; r += DT) rcA[r] = tA[r] * lA[r];
+            DQ_ROWS(i, r) RCA(i, r) = TA(i, r) * LA(i, r);
             for (int j = tid; j < 2 * n; j += DT) rcB[j] = tB[j] * lB[j];
             __syncthreads();
             solve();
@@ -1886,7 +1922,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
             sg = sg * sg * sg;
             const double smu = sg * mu;
             const double soc = (al < DQ_SOC_ALPHA && feas <= DQ_FEAS_GUARD * (1.0 + bscale)) ? 0.0 : 1.0;
-            for (int r = tid; r < m; r += DT) rcA[r] = tA[r] * lA[r] + soc * dtA[r] * dlA[r] - smu;
+            DQ_ROWS(i, r) RCA(i, r) = TA(i, r) * LA(i, r) + soc * DTA(i, r) * DLA(i, r) - smu;
             for (int j = tid; j < n; j += DT) {
                 rcB[j] = up_present(j) ? tB[j] * lB[j] + soc * dtB[j] * dlB[j] - smu : 0.0;
                 rcB[n + j] = lo_present(j) ? tB[n + j] * lB[n + j] + soc * dtB[n + j] * dlB[n + j] - smu : 0.0;
@@ -1906,7 +1942,7 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
                 if (lo_present(j)) { tB[n + j] += al * dtB[n + j]; lB[n + j] += al * dlB[n + j]; }
             }
             for (int r = tid; r < me; r += DT) y[r] += al * dy[r];
-            for (int r = tid; r < m; r += DT) { tA[r] += al * dtA[r]; lA[r] += al * dlA[r]; }
+            DQ_ROWS(i, r) { TA(i, r) += al * DTA(i, r); LA(i, r) += al * DLA(i, r); }
             __syncthreads();
             al_last = al;
             DST(5);
@@ -1933,8 +1969,21 @@ __global__ void __launch_bounds__(DT) dense_ipm_kernel(DenseKernelArgs a) {
         if (a.lam_lower) a.lam_lower[(int64_t)inst * n + j] = (lo_present(j) && flag != -6) ? lB[n + j] : 0.0;
         if (a.lam_upper) a.lam_upper[(int64_t)inst * n + j] = (up_present(j) && flag != -6) ? lB[j] : 0.0;
     }
-    for (int r = tid; r < m; r += DT)
-        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = flag != -6 ? lA[r] : 0.0;
+    DQ_ROWS(i, r) {
+        if (a.lam_ineqlin) a.lam_ineqlin[(int64_t)inst * m + r] = flag != -6 ? LA(i, r) : 0.0;
+        if constexpr (RG) { tA[r] = TA(i, r); lA[r] = LA(i, r); }   // the repair launch's start
+    }
+    if constexpr (RG) {
+        for (int j = tid; j < n; j += DT) W[L.z + j] = z[j];
+        for (int j = tid; j < 2 * n; j += DT) { W[L.tB + j] = tB[j]; W[L.lB + j] = lB[j]; }
+    }
+#undef TA
+#undef LA
+#undef RIA
+#undef RCA
+#undef DTA
+#undef DLA
+#undef DQ_ROWS
     for (int r = tid; r < me; r += DT)
         if (a.lam_eqlin) a.lam_eqlin[(int64_t)inst * me + r] = flag != -6 ? y[r] : 0.0;
     fv = red.sum(fv);
@@ -2519,11 +2568,20 @@ __global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
 // dynamic LDS above 64 KB needs the kernel attribute on the current device; set on every launch
 // (a host call of about a microsecond) so that no process-wide state is kept (include/bqp.h: handles
 // on several host threads and devices share nothing)
-template <bool KL>
+template <bool KL, bool RG>
 static hipError_t dense_lds_attr(size_t lds) {
     if (lds <= 64 * 1024) return hipSuccess;
-    return hipFuncSetAttribute((const void*)dense_ipm_kernel<KL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    return hipFuncSetAttribute((const void*)dense_ipm_kernel<KL, RG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                DENSE_LDS_MAX);
+}
+
+// the row state in registers (dense_ipm_kernel RG): at most DQ_RPT rows per thread, the A'DA on
+// the two global_load_lds buffers (the only path that forms the tile row weights from registers)
+// and A'w with the row weights staged in LDS whole.  BQP_DENSE_NO_RG=1: the workspace form (A/B).
+static bool dense_rows_in_regs(int n, int m) {
+    if (const char* e = getenv("BQP_DENSE_NO_RG")) if (atoi(e) != 0) return false;
+    return m > 0 && m <= DQ_RPT * DT && dense_k_lds(n) && dense_glds(n) && m + n <= TILE * dense_ts(n) &&
+           dense_lds_bytes(n) + sizeof(double) * DQ_NVEC * n <= DENSE_LDS_MAX;
 }
 
 // H <- (H + H')/2 in place for `count` n x n matrices `stride` doubles apart (the host entry's
@@ -2566,14 +2624,19 @@ hipError_t launch_dense(const DenseKernelArgs& a0, hipStream_t st) {
     } else {
         const size_t lds = dense_lds_bytes(a.n);
         if (lds > DENSE_LDS_MAX) return hipErrorInvalidValue;
-        if (dense_k_lds(a.n)) {
-            hipError_t e = dense_lds_attr<true>(lds);
+        if (dense_rows_in_regs(a.n, a.m)) {
+            const size_t ldsr = lds + sizeof(double) * DQ_NVEC * a.n;
+            hipError_t e = dense_lds_attr<true, true>(ldsr);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(dense_ipm_kernel<true>, dim3(a.batch), dim3(DT), lds, st, a);
+            hipLaunchKernelGGL((dense_ipm_kernel<true, true>), dim3(a.batch), dim3(DT), ldsr, st, a);
+        } else if (dense_k_lds(a.n)) {
+            hipError_t e = dense_lds_attr<true, false>(lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((dense_ipm_kernel<true, false>), dim3(a.batch), dim3(DT), lds, st, a);
         } else {
-            hipError_t e = dense_lds_attr<false>(lds);
+            hipError_t e = dense_lds_attr<false, false>(lds);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(dense_ipm_kernel<false>, dim3(a.batch), dim3(DT), lds, st, a);
+            hipLaunchKernelGGL((dense_ipm_kernel<false, false>), dim3(a.batch), dim3(DT), lds, st, a);
         }
     }
     hipError_t err = hipGetLastError();

@@ -148,7 +148,9 @@ __device__ __forceinline__ bool chol_small(const real (&M)[N][N], real (&L)[N][N
     if (!(d0 > PIV_FLOOR * M[0][0])) d0 = PIV_FLOOR * M[0][0];
     ok = ok && (d0 > 0.0);
     if constexpr (N == 2) {
-        const real r0 = real(1) / d0;
+        // reciprocals by frcp (estimate + two Newton steps, as the n = 1 path): the IEEE division's
+        // scale / fixup sequence was twice as long on the chain
+        const real r0 = frcp(d0);
         const real l10 = M[1][0] * r0;
         real d1 = M[1][1] - l10 * M[1][0];
         if (!(d1 > PIV_FLOOR * M[1][1])) d1 = PIV_FLOOR * M[1][1];
@@ -156,7 +158,7 @@ __device__ __forceinline__ bool chol_small(const real (&M)[N][N], real (&L)[N][N
         L[0][0] = r0;
         L[0][1] = 0.0;
         L[1][0] = l10;
-        L[1][1] = real(1) / d1;
+        L[1][1] = frcp(d1);
     } else {
         L[0][0] = sqrt(d0);
     }

@@ -14,10 +14,11 @@
 //                         weighted residuals of the quadratic cost and - GN mode - the forward
 //                         sensitivities dx/dz (lanes over the columns of z) written as the rows
 //                         of the residual Jacobian Jr (row-major, coalesced along z)
-//   lbmpc_normal_kernel   one workgroup per instance: H = 2 Jr'Jr, f = 2 Jr'er through LDS row
-//                         tiles, and the QP right-hand side b_in - A_in z
+//   lbmpc_normal_kernel   one workgroup per instance: H = 2 Jr'Jr on the fp64 matrix cores and
+//                         f = 2 Jr'er through LDS row tiles, and the QP right-hand side b_in - A_in z
 //   lbmpc_hess_kernel     (exact Hessian) one workgroup per instance: H_GN + the second-order
-//                         term of the learned dynamics, kept if its LDS Cholesky succeeds
+//                         term of the learned dynamics (its row products on the matrix cores),
+//                         kept if its LDS Cholesky succeeds
 //   lbmpc_update_kernel   one wave per instance: convergence test (step, NLP stationarity
 //                         |f + A_in' lam|), Armijo choice among the trial step lengths, z += a d
 #include <hip/hip_runtime.h>
@@ -488,6 +489,73 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
 }
 
 // ------------------------------------------------------------------------------------------
+// row-product sums on the fp64 matrix cores (round 6): sum_r X(r, :)' Y(r, :) over the rows of
+// LDS row tiles (row-major, stride ld, columns zero-padded to 16 ceil(n / 16), rows past the
+// data zero) into the lower block triangle of 16 x 16 tiles.  Wave w holds the tiles of lb_tile
+// (diagonal tiles w, w + 4, then every fourth strictly lower tile; at most LB_TPW); per k-step of
+// 4 rows lane l supplies X(4 s + l/16, 16 I + l%16) and Y(4 s + l/16, 16 J + l%16) to one
+// v_mfma_f64_16x16x4f64, and tile (I, J), lane l, register e ends with entry
+// (16 I + l/16 + 4 e, 16 J + l%16).  (The VALU 8 x 8 register tiles they replace ran at a few
+// percent of the FP64 rate, one LDS operand pair per FMA pair.)
+// ------------------------------------------------------------------------------------------
+typedef double lbd4 __attribute__((ext_vector_type(4)));
+#define LB_TPW 9
+__device__ __forceinline__ void lb_tile(int w, int u, int nbk, int& I, int& J) {
+    I = -1; J = 0;
+    if (u < 2) {
+        const int d = w + 4 * u;
+        if (d < nbk) { I = d; J = d; }
+        return;
+    }
+    const int o = 4 * (u - 2) + w;
+    if (o >= nbk * (nbk - 1) / 2) return;
+    int i = 1;
+    while ((i + 1) * i / 2 <= o) ++i;
+    I = i;
+    J = o - i * (i - 1) / 2;
+}
+// rows r0 .. r0 + rc - 1 of the row-major nrows x n matrix G into the tile T (rows 0 .. R - 1,
+// stride ld, ncp = 16 ceil(n / 16) columns, zeros past rc and n): 8 loads in flight per thread
+template <int R>
+__device__ __forceinline__ void lb_load_rows(double* T, const double* G, int r0, int rc, int n, int ncp, int ld,
+                                             int tid) {
+    const int tot = R * ncp;
+    for (int b0 = 0; b0 < tot; b0 += 8 * 256) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = b0 + tid + 256 * u;
+            const int r = i / ncp, c = i - r * ncp;
+            v[u] = (i < tot && r < rc && c < n) ? G[(int64_t)(r0 + r) * n + c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = b0 + tid + 256 * u;
+            const int r = i / ncp, c = i - r * ncp;
+            if (i < tot) T[r * ld + c] = v[u];
+        }
+    }
+}
+// the k-steps of one tile: acc += X'Y (and, SYM, += Y'X as well)
+template <int R, bool SYM>
+__device__ __forceinline__ void lb_mfma_rows(lbd4 (&acc)[LB_TPW], const int (&tI)[LB_TPW], const int (&tJ)[LB_TPW],
+                                             const double* X, const double* Y, int ld, int lane) {
+    const int c16 = lane & 15, k4 = lane >> 4;
+#pragma unroll
+    for (int s = 0; s < R / 4; ++s) {
+        const double* xr = X + (4 * s + k4) * ld + c16;
+        const double* yr = Y + (4 * s + k4) * ld + c16;
+#pragma unroll
+        for (int u = 0; u < LB_TPW; ++u) {
+            if (tI[u] < 0) continue;
+            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[16 * tI[u]], yr[16 * tJ[u]], acc[u], 0, 0, 0);
+            if constexpr (SYM)
+                acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(yr[16 * tI[u]], xr[16 * tJ[u]], acc[u], 0, 0, 0);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // exact Hessian (a.hess): Hx = H_GN + sym(Jr2' Tr2) through LDS row tiles (8 x 8 accumulators
 // per thread, as the normal kernel), then a right-looking Cholesky of Hx in LDS; if every pivot
 // is above 1e-10 max|Hx_ii| (oracle/lbmpc.py pd_cholesky) Hx replaces the Gauss-Newton H,
@@ -498,62 +566,45 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
     const int b = blockIdx.x;
     if (b >= a.batch || a.done[b]) return;
     const int n = a.n, nr2 = 3 * a.N, tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;
+    const int lane = tid & 63, wv = tid >> 6, c16 = lane & 15, k4 = lane >> 4;
+    const int tx = tid & 15, ty = tid >> 4;      // the Cholesky test's 16 x 16 thread grid
+    const int nbk = (n + 15) >> 4, ncp = 16 * nbk;
     double* TA = lh;
-    double* TB = lh + 16 * n;
-    double* Kx = lh + 32 * n;
+    double* TB = lh + 16 * ncp;
+    double* Kx = lh + 32 * ncp;
     __shared__ double red[4];
     if (n > 128) return;
     const double* J2 = a.Jr2 + (int64_t)b * nr2 * n;
     const double* T2 = a.Tr2 + (int64_t)b * nr2 * n;
-    double acc[8][8];
+    // S = Jr2'Tr2 + Tr2'Jr2 on the lower block triangle (lb_mfma_rows, two MFMAs per k-step)
+    int tI[LB_TPW], tJ[LB_TPW];
+    lbd4 acc[LB_TPW];
 #pragma unroll
-    for (int p = 0; p < 8; ++p)
-#pragma unroll
-        for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] = 0.0;
+    for (int u = 0; u < LB_TPW; ++u) { lb_tile(wv, u, nbk, tI[u], tJ[u]); acc[u] = lbd4{0.0, 0.0, 0.0, 0.0}; }
     for (int r0 = 0; r0 < nr2; r0 += 16) {
         const int rc = min(16, nr2 - r0);
         __syncthreads();
-        for (int i = tid; i < rc * n; i += 256) { TA[i] = J2[(int64_t)r0 * n + i]; TB[i] = T2[(int64_t)r0 * n + i]; }
+        lb_load_rows<16>(TA, J2, r0, rc, n, ncp, ncp, tid);
+        lb_load_rows<16>(TB, T2, r0, rc, n, ncp, ncp, tid);
         __syncthreads();
-        for (int r = 0; r < rc; ++r) {
-            const double* Ar = TA + r * n;
-            const double* Br = TB + r * n;
-            double cj[8];
-#pragma unroll
-            for (int q2 = 0; q2 < 8; ++q2) cj[q2] = (tx + 16 * q2 < n) ? Br[tx + 16 * q2] : 0.0;
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const int i = ty + 16 * p;
-                const double ci = (i < n) ? Ar[i] : 0.0;
-#pragma unroll
-                for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] += ci * cj[q2];
-            }
-        }
+        lb_mfma_rows<16, true>(acc, tI, tJ, TA, TB, ncp, lane);
     }
-    __syncthreads();
-    // Kx(i, j) = Jr2(:, i)' Tr2(:, j) (column-major in LDS), then H_GN + its symmetric part: each
-    // pair (i > j) and each diagonal entry belongs to one thread
-#pragma unroll
-    for (int p = 0; p < 8; ++p)
-#pragma unroll
-        for (int q2 = 0; q2 < 8; ++q2) {
-            const int i = ty + 16 * p, j = tx + 16 * q2;
-            if (i < n && j < n) Kx[j * n + i] = acc[p][q2];
-        }
-    __syncthreads();
+    // H_GN + the symmetric part S / 2 of Jr2'Tr2, both triangles, in LDS (column-major): each
+    // entry (i >= j) belongs to one lane
     const double* H = a.H + (int64_t)b * n * n;
     double dmx = 0.0;
-    for (int e = tid; e < n * n; e += 256) {
-        const int i = e % n, j = e / n;
-        if (i > j) {
-            const double v = H[e] + 0.5 * (Kx[j * n + i] + Kx[i * n + j]);
-            Kx[j * n + i] = v;
-            Kx[i * n + j] = v;
-        } else if (i == j) {
-            const double v = H[e] + Kx[e];
-            Kx[e] = v;
-            dmx = fmax(dmx, fabs(v));
+#pragma unroll
+    for (int u = 0; u < LB_TPW; ++u) {
+        if (tI[u] < 0) continue;
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+            const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
+            if (i < n && j < n && i >= j) {
+                const double v = H[(int64_t)j * n + i] + 0.5 * acc[u][e2];
+                Kx[j * n + i] = v;
+                Kx[i * n + j] = v;
+                if (i == j) dmx = fmax(dmx, fabs(v));
+            }
         }
     }
     dmx = wmax(dmx);
@@ -619,59 +670,75 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
 // ------------------------------------------------------------------------------------------
 // normal equations H = 2 Jr'Jr, f = 2 Jr'er (column-major H), QP rhs b_in - A_in z
 // ------------------------------------------------------------------------------------------
-#define LB_RC 16         // Jr rows per LDS tile
-#define LB_MAXN 128      // n <= 128 for the normal kernel (8 x 8 accumulators per thread)
+#define LB_RC 32         // Jr rows per LDS tile (8 k-steps of the matrix cores)
+#define LB_MAXN 128      // n <= 128 for the normal kernel (16 x 16 tiles of 8 x 8 blocks)
+#define LB_TS 130        // LDS row stride of the tile (the 16 ceil(n / 16) <= 128 columns + 2)
 __global__ void __launch_bounds__(256) lbmpc_normal_kernel(LbmpcArgs a) {
-    __shared__ double T[LB_RC * LB_MAXN];
+    __shared__ double T[LB_RC * LB_TS];
     __shared__ double E[LB_RC];
     const int b = blockIdx.x;
     if (b >= a.batch || a.done[b]) return;
     const int n = a.n, nr = a.nr, tid = threadIdx.x;
-    const int tx = tid & 15, ty = tid >> 4;
+    const int lane = tid & 63, wv = tid >> 6, c16 = lane & 15, k4 = lane >> 4;
+    const int nbk = (n + 15) >> 4, ncp = 16 * nbk;
     const double* Jr = a.Jr + (int64_t)b * nr * n;
     const double* er = a.er + (int64_t)b * nr;
-    double acc[8][8], fa = 0.0;
+    // Jr'Jr on the lower block triangle (lb_mfma_rows); Jr'er by thread tid < n
+    int tI[LB_TPW], tJ[LB_TPW];
+    lbd4 acc[LB_TPW];
 #pragma unroll
-    for (int p = 0; p < 8; ++p)
-#pragma unroll
-        for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] = 0.0;
+    for (int u = 0; u < LB_TPW; ++u) { lb_tile(wv, u, nbk, tI[u], tJ[u]); acc[u] = lbd4{0.0, 0.0, 0.0, 0.0}; }
+    double fa = 0.0;
     for (int r0 = 0; r0 < nr; r0 += LB_RC) {
         const int rc = min(LB_RC, nr - r0);
         __syncthreads();
-        for (int i = tid; i < rc * n; i += 256) T[(i / n) * LB_MAXN + (i % n)] = Jr[(int64_t)r0 * n + i];
-        if (tid < rc) E[tid] = er[r0 + tid];
+        lb_load_rows<LB_RC>(T, Jr, r0, rc, n, ncp, LB_TS, tid);
+        if (tid < LB_RC) E[tid] = tid < rc ? er[r0 + tid] : 0.0;
         __syncthreads();
-        for (int r = 0; r < rc; ++r) {
-            const double* Tr = T + r * LB_MAXN;
-            double cj[8];
-#pragma unroll
-            for (int q2 = 0; q2 < 8; ++q2) cj[q2] = (tx + 16 * q2 < n) ? Tr[tx + 16 * q2] : 0.0;
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const int i = ty + 16 * p;
-                const double ci = (i < n) ? Tr[i] : 0.0;
-#pragma unroll
-                for (int q2 = 0; q2 < 8; ++q2) acc[p][q2] += ci * cj[q2];
-            }
-            if (tid < n) fa += Tr[tid] * E[r];
-        }
+        lb_mfma_rows<LB_RC, false>(acc, tI, tJ, T, T, LB_TS, lane);
+        if (tid < n)
+            for (int r = 0; r < rc; ++r) fa += T[r * LB_TS + tid] * E[r];
     }
+    // H = 2 Jr'Jr (column-major, both triangles from the lower one: exactly symmetric)
     double* H = a.H + (int64_t)b * n * n;
 #pragma unroll
-    for (int p = 0; p < 8; ++p)
+    for (int u = 0; u < LB_TPW; ++u) {
+        if (tI[u] < 0) continue;
 #pragma unroll
-        for (int q2 = 0; q2 < 8; ++q2) {
-            const int i = ty + 16 * p, j = tx + 16 * q2;
-            if (i < n && j < n) H[(int64_t)j * n + i] = 2.0 * acc[p][q2];
+        for (int e2 = 0; e2 < 4; ++e2) {
+            const int i = 16 * tI[u] + k4 + 4 * e2, j = 16 * tJ[u] + c16;
+            if (i < n && j < n && i >= j) {
+                const double v = 2.0 * acc[u][e2];
+                H[(int64_t)j * n + i] = v;
+                H[(int64_t)i * n + j] = v;
+            }
         }
+    }
     if (tid < n) a.f[(int64_t)b * n + tid] = 2.0 * fa;
-    // b_in - A_in z (A_in column-major m x n, shared)
+    // b_in - A_in z (A_in column-major m x n, shared): z staged in LDS, 8 columns' loads in
+    // flight and four partial sums per row (the serial column loop waited on every load)
     const double* z = a.z + (int64_t)b * n;
     const double* bin = a.bin + (int64_t)b * a.sbin;
-    for (int r = tid; r < a.m; r += 256) {
-        double v = bin[r];
-        for (int j = 0; j < n; ++j) v -= a.Ain[(int64_t)j * a.m + r] * z[j];
-        a.bsh[(int64_t)b * a.m + r] = v;
+    __syncthreads();
+    double* zs = T;
+    for (int j = tid; j < n; j += 256) zs[j] = z[j];
+    __syncthreads();
+    const int m = a.m;
+    for (int r = tid; r < m; r += 256) {
+        const double* ar = a.Ain + r;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int j = 0;
+        for (; j + 8 <= n; j += 8) {
+            double av[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) av[u] = ar[(int64_t)(j + u) * m];
+            s0 = fma(av[0], zs[j], s0); s1 = fma(av[1], zs[j + 1], s1);
+            s2 = fma(av[2], zs[j + 2], s2); s3 = fma(av[3], zs[j + 3], s3);
+            s0 = fma(av[4], zs[j + 4], s0); s1 = fma(av[5], zs[j + 5], s1);
+            s2 = fma(av[6], zs[j + 6], s2); s3 = fma(av[7], zs[j + 7], s3);
+        }
+        for (; j < n; ++j) s0 = fma(ar[(int64_t)j * m], zs[j], s0);
+        a.bsh[(int64_t)b * m + r] = bin[r] - ((s0 + s1) + (s2 + s3));
     }
 }
 
@@ -792,8 +859,9 @@ hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st) {
     return hipGetLastError();
 }
 
-// the exact-Hessian kernel holds 32 rows of Jr2 tiles and the n x n sum in LDS
-static size_t lbmpc_hess_lds(int n) { return sizeof(double) * ((size_t)32 * n + (size_t)n * n); }
+// the exact-Hessian kernel holds 16-row tiles of Jr2 and Tr2 (16 ceil(n / 16) columns) and the
+// n x n sum in LDS
+static size_t lbmpc_hess_lds(int n) { return sizeof(double) * ((size_t)32 * 16 * ((n + 15) / 16) + (size_t)n * n); }
 bool lbmpc_hess_fits(int n) { return n <= 128 && lbmpc_hess_lds(n) <= 160 * 1024 - 64; }
 
 hipError_t launch_lbmpc_hess(const LbmpcArgs& a, hipStream_t st) {

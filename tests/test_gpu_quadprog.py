@@ -120,6 +120,50 @@ def test_dense_lds_layout_sizes(n, handle):
         assert np.abs(x[i] - z).max() / max(1, np.abs(z).max()) < 5e-8
 
 
+@pytest.mark.parametrize('m', [300, 1024])
+def test_dense_rows_in_registers_equals_workspace_form(m, handle):
+    """round 6: dense_ipm_kernel keeps the row state of A's rows in registers and the n-vectors in
+    LDS when they fit (m <= 1024, n <= 106: the learned loop's sub-problem is n = 101, m = 1024);
+    BQP_DENSE_NO_RG=1 selects the workspace form of the same iteration.  The two are compiled
+    separately and are not bit-identical (a product with two uses, e.g. t lam in the residual
+    pass, is fused into an FMA where the workspace form re-loads its operands and kept where the
+    register form shares it), and on these degenerate random QPs (about a third of 1024 rows
+    active) round-off moves the iteration count (tools/diag_dense_rg.py: 18 / 16 and 18 / 35
+    iterations, each form deterministic run to run): both converge, to the same optimum (x within
+    1e-8, f within 1e-9 relative), each run of the register form repeats bit for bit, KKT
+    stationarity holds, and for m = 300 the result is the exact optimum (oracle/exact_qp.py)."""
+    import os
+    import bqp
+    from oracle import exact_qp
+    n, B = 101, 4
+    rng = np.random.default_rng(7 + m)
+    M = rng.standard_normal((n, n))
+    H = M @ M.T / n + np.eye(n)
+    A = rng.standard_normal((m, n))
+    f = rng.standard_normal((B, n))
+    b = rng.uniform(0.2, 1.0, (B, m))
+    lb, ub = -2.0 * np.ones(n), 2.0 * np.ones(n)
+    x, fval, flag, out, lam = bqp.quadprog(H, f, A, b, lb=lb, ub=ub, handle=handle)
+    x2, fval2, flag2, out2, lam2 = bqp.quadprog(H, f, A, b, lb=lb, ub=ub, handle=handle)
+    os.environ['BQP_DENSE_NO_RG'] = '1'
+    try:
+        xw, fw, flw, outw, lamw = bqp.quadprog(H, f, A, b, lb=lb, ub=ub, handle=handle)
+    finally:
+        del os.environ['BQP_DENSE_NO_RG']
+    print('m %d: iterations %s / %s, max |dx| %.2e' % (m, out['iterations'], outw['iterations'], np.abs(x - xw).max()))
+    assert np.array_equal(x, x2) and np.array_equal(out['iterations'], out2['iterations'])
+    assert (flag == 1).all() and (flw == 1).all()
+    assert np.abs(x - xw).max() < 1e-8 * max(1.0, np.abs(x).max())
+    assert np.abs(fval - fw).max() < 1e-9 * max(1.0, np.abs(fw).max())
+    for i in range(B):
+        r = H @ x[i] + f[i] + A.T @ lam['ineqlin'][i] + lam['upper'][i] - lam['lower'][i]
+        assert np.abs(r).max() < 1e-6 * (1 + np.abs(f[i]).max())
+    if m == 300:
+        A2 = np.vstack([A, np.eye(n), -np.eye(n)])
+        z = exact_qp.solve(H, f[0], A2, np.concatenate([b[0], ub, -lb]))["z"]
+        assert np.abs(x[0] - z).max() / max(1, np.abs(z).max()) < 5e-8
+
+
 def test_nonsymmetric_h_uses_symmetric_part(handle):
     """MATLAB quadprog solves with (H + H')/2 when H is not symmetric; the host entry
     symmetrises its staging copy, so the result equals the solve with the symmetric part (to the

@@ -34,6 +34,21 @@ namespace bqp {
 #define LB_MAXQ 512      // NW window capacity (data points) held in LDS
 #define LB_CPL 4         // z columns per lane in the sensitivity recursion (n <= 256)
 
+// a readlane broadcast kept in vector registers (round 6): as scalar registers the 50 totals of
+// the Hessian rollout's NW sums outgrew the SGPR file and were spilled to and reloaded from VGPR
+// lanes (~780 readlanes per stage in the stage-cost phase of the ISA)
+__device__ __forceinline__ double rlv(double v, int src) {
+    double r = rl(v, src);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+// the lane index made opaque inside a loop: the masks derived from it (column j < n, j == k, ...)
+// are formed where they are used instead of hoisted out of the stage loop and kept in scalar
+// registers for its whole length
+__device__ __forceinline__ int lb_opq(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 // NW sums at xi over the window in LDS: point i at D[wr i .. wr i + wr - 1], wr = 7 rows
 // [X; Y] (every point counts in the normaliser, oracleL2NW.m / hybrid_LBMPC_casadi.m:331-358) or
 // wr = 8 rows [X; Y; v] (casadiL2NW.m:14-28: the normaliser is lambda + sum_j v_j k_j, the
@@ -95,15 +110,15 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double h
             }
         }
         const double ta = wsum_t(va, lane);
-        s = rl(ta, 0);
+        s = rlv(ta, 0);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sy[r] = rl(ta, 1 + r);
+        for (int r = 0; r < 4; ++r) sy[r] = rlv(ta, 1 + r);
         if constexpr (JAC) {
 #pragma unroll
             for (int c3 = 0; c3 < 3; ++c3) {
-                ds[c3] = rl(ta, 5 + c3);
+                ds[c3] = rlv(ta, 5 + c3);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) dsy[r][c3] = rl(ta, 8 + 3 * r + c3);
+                for (int r = 0; r < 4; ++r) dsy[r][c3] = rlv(ta, 8 + 3 * r + c3);
             }
         }
         if constexpr (HESS) {
@@ -117,9 +132,9 @@ __device__ __forceinline__ void nw_eval(const double* D, int q, int wr, double h
             const double tb = wsum_t(vb, lane);
 #pragma unroll
             for (int e = 0; e < 6; ++e) {
-                s2[e] = rl(tb, e);
+                s2[e] = rlv(tb, e);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) sy2[r][e] = rl(tb, 6 + 6 * r + e);
+                for (int r = 0; r < 4; ++r) sy2[r][e] = rlv(tb, 6 + 6 * r + e);
             }
         }
     }
@@ -219,7 +234,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     static_assert(NX == 4 && NU == 1, "NW input xi = [x_1; x_2; u] with the 4-state model, nu = 1");
     extern __shared__ double lbd[];
     double* D = lbd;
-    const int lane = threadIdx.x;
+    int lane = threadIdx.x;              // re-made opaque at each stage (lb_opq)
     const int nt = gn ? 1 : a.ntrial;
     const int b = blockIdx.x / nt, t = blockIdx.x % nt;
     if (b >= a.batch || a.done[b]) return;
@@ -315,6 +330,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     };
     RST_DECL;
     for (int k = 0; k < N; ++k) {
+        lane = lb_opq(lane);
         const double vk = zv(k);
         double u = vk, un = vk;
 #pragma unroll
@@ -456,6 +472,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
 #pragma unroll
         for (int i = 0; i < NX; ++i) SL[c][i] = 0.0;
     for (int k = 0; k < N; ++k) {
+        lane = lb_opq(lane);
         const double* st = SS + (int64_t)k * LB_SS;
         const double w00 = st[12], w01 = st[13], w02 = st[14], w11 = st[15], w12 = st[16], w22 = st[17];
 #pragma unroll

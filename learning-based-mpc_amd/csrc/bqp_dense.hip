@@ -832,9 +832,40 @@ struct DPolish {
     double bscale, tol_stat;
 };
 
+#ifdef BQP_DSTAMPS
+// diagnostic build only: s_memtime cycles per phase of the polish of instance 0 (printed at exit)
+#define PST_DECL                                                           \
+    unsigned long long pst_last = __builtin_amdgcn_s_memtime(), pst_acc[9]; \
+    int pst_rounds = 0;                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < 9; ++i_) pst_acc[i_] = 0
+#define PST(id)                                                            \
+    do {                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                     \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();        \
+        pst_acc[id] += _t - pst_last;                                      \
+        pst_last = _t;                                                     \
+    } while (0)
+#define PST_RET(v)                                                         \
+    do {                                                                   \
+        if (blockIdx.x == 0 && threadIdx.x == 0)                           \
+            printf("PSTAMPS n %d m %d rounds %d ret %d actlist %llu K %llu cholK %llu Y %llu S %llu "    \
+                   "cholS %llu mult %llu checks %llu corr %llu\n", n, m, pst_rounds, (int)(v), pst_acc[0], \
+                   pst_acc[1], pst_acc[2], pst_acc[3], pst_acc[4], pst_acc[5], pst_acc[6], pst_acc[7],    \
+                   pst_acc[8]);                                            \
+        return (v);                                                        \
+    } while (0)
+#define PST_ROUND() (++pst_rounds)
+#else
+#define PST_DECL do { } while (0)
+#define PST(id) do { } while (0)
+#define PST_RET(v) return (v)
+#define PST_ROUND() do { } while (0)
+#endif
+
 template <int NTH, class R>
 __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
     R red{sc};
+    PST_DECL;
     const int n = p.n, m = p.m, me = p.me, tid = threadIdx.x;
     const DWork L = DWork::make(n, m, me);
     double *K = p.W + L.K, *Y = p.W + L.Y, *S = p.W + L.S;
@@ -868,6 +899,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
     const double rho = fmax(1.0, red.max(hd));
     const double tf = 1e-12 * (1.0 + p.bscale);
     for (int round = 0; round < DQ_POL_ROUNDS; ++round) {
+        PST_ROUND();
         __syncthreads();
         if (tid == 0) {             // active row list (serial: a handful of rounds per instance)
             int c = 0;
@@ -882,7 +914,8 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
             sc[9] = (over || me + c > n) ? -1.0 : (double)c;
         }
         __syncthreads();
-        if (sc[9] < 0.0) return false;       // more active rows than variables: degenerate
+        PST(0);
+        if (sc[9] < 0.0) PST_RET(false);     // more active rows than variables: degenerate
         const int na = (int)sc[9], ne = me + na;
         // K = H + rho G_a'G_a
         double dmx = 0.0;
@@ -899,7 +932,9 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         }
         const double kfl = DQ_PIV_FLOOR * fmax(red.max(dmx), 1e-300);
         __syncthreads();
+        PST(1);
         block_cholesky<NTH>(K, n, sc, kfl);
+        PST(2);
         // Y = K^{-1} Ex', S = Ex Y (one thread per row of Ex)
         for (int k = tid; k < ne; k += NTH) {
             double* yc = Y + (int64_t)k * n;
@@ -910,6 +945,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         // ra = G_a z - h_a
         for (int k = tid; k < na; k += NTH) { const int r = (int)idx[k]; ra[k] = gdot(r, p.z) - hr(r); }
         __syncthreads();
+        PST(3);
         double smx = 0.0;
         for (int t2 = tid; t2 < ne * ne; t2 += NTH) {
             const int r1 = t2 % ne, r2 = t2 / ne;
@@ -929,6 +965,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         }
         const double sfl = DQ_PIV_FLOOR * fmax(red.max(smx), 1e-300);
         __syncthreads();
+        PST(4);
         if (ne > 0) block_cholesky<NTH>(S, ne, sc, sfl);
         chol_solve_w(K, n, xs);
         for (int j = tid; j < n; j += NTH) w[j] = xs[j];
@@ -949,6 +986,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         if (ne > 0) chol_solve_w(S, ne, xs);
         for (int k = tid; k < ne; k += NTH) mult[k] = xs[k];
         __syncthreads();
+        PST(5);
         for (int j = tid; j < n; j += NTH) {
             double v = p.z[j] + w[j];
             for (int k = 0; k < ne; ++k) v -= Y[(int64_t)k * n + j] * mult[k];
@@ -962,6 +1000,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
             if (r < m) nuA[r] = mult[me + k]; else nuB[r - m] = mult[me + k];
         }
         __syncthreads();
+        PST(6);
         // checks at zn
         double viol = 0.0, va = 0.0, lmx = 0.0, lneg = 0.0, fe = 0.0, st = 0.0, gs = 0.0;
         for (int r = tid; r < m; r += NTH) {
@@ -994,6 +1033,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         const double stat = red.max(st), gsc = red.max(gs), vio = red.max(viol), vac = red.max(va);
         const double lx = red.max(lmx), ln = red.min(lneg), fq = red.max(fe);
         const double td = 1e-9 * (1.0 + lx);
+        PST(7);
         if (isfinite(stat) && stat <= p.tol_stat * (1.0 + gsc) && vio <= tf && vac <= tf && ln >= -td && fq <= tf) {
             for (int j = tid; j < n; j += NTH) {
                 p.z[j] = zn[j];
@@ -1004,7 +1044,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
             for (int k = tid; k < me; k += NTH) p.y[k] = mult[k];
             if (tid == 0) { sc[10] = stat; sc[11] = fmax(fmax(vio, 0.0), fq); }
             __syncthreads();
-            return true;
+            PST_RET(true);
         }
         // set corrections
         double chg = 0.0;
@@ -1016,9 +1056,11 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
             if (actB[q2] != 0.0 && nuB[q2] < -td) { actB[q2] = 0.0; chg = 1.0; }
             else if (actB[q2] == 0.0 && riB[q2] > tf) { actB[q2] = 1.0; chg = 1.0; }
         }
-        if (red.max(chg) == 0.0) return false;
+        const bool nochg = red.max(chg) == 0.0;
+        PST(8);
+        if (nochg) PST_RET(false);
     }
-    return false;
+    PST_RET(false);
 }
 
 #ifdef BQP_DSTAMPS

@@ -847,7 +847,7 @@ struct DPolish {
     } while (0)
 #define PST_RET(v)                                                         \
     do {                                                                   \
-        if (blockIdx.x == 0 && threadIdx.x == 0)                           \
+        if ((blockIdx.x & 15) == 0 && threadIdx.x == 0)                    \
             printf("PSTAMPS n %d m %d rounds %d ret %d actlist %llu K %llu cholK %llu Y %llu S %llu "    \
                    "cholS %llu mult %llu checks %llu corr %llu\n", n, m, pst_rounds, (int)(v), pst_acc[0], \
                    pst_acc[1], pst_acc[2], pst_acc[3], pst_acc[4], pst_acc[5], pst_acc[6], pst_acc[7],    \

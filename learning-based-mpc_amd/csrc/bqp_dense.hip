@@ -42,6 +42,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 #define DQ_RES_SHORT 0.5      // a step shorter than this: the next residuals evaluated exactly
 #define DQ_RES_EVERY 8        // and at least every 8th iteration (else the (1 - al) recurrence)
 #define DQ_POL_ROUNDS 4       // active-set corrections of the polish
+#define DQ_POL_KLDS (16 * 1024) // doubles of K the polish kernel keeps in LDS (n <= 128)
 
 // polish mode of an instance: the launch's, or 2 once the instance's own SQP iteration count has
 // reached pol_stall (DenseKernelArgs.pol_it)
@@ -830,6 +831,9 @@ struct DPolish {
     double *z, *y, *tA, *lA, *tB, *lB;
     double* W;             // the instance's DWork
     double bscale, tol_stat;
+    double* Kl;            // the n x n matrix K in LDS (dense_polish_kernel when it fits), else null:
+                           // the workspace's (round 6: the Cholesky and the n-long substitutions of the
+                           // Schur columns were L2 round trips, ~65 % of a polish in its stamps)
 };
 
 #ifdef BQP_DSTAMPS
@@ -868,7 +872,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
     PST_DECL;
     const int n = p.n, m = p.m, me = p.me, tid = threadIdx.x;
     const DWork L = DWork::make(n, m, me);
-    double *K = p.W + L.K, *Y = p.W + L.Y, *S = p.W + L.S;
+    double *K = p.Kl ? p.Kl : p.W + L.K, *Y = p.W + L.Y, *S = p.W + L.S;
     double *actA = p.W + L.rcA, *actB = p.W + L.rcB, *nuA = p.W + L.dlA, *nuB = p.W + L.dlB;
     double *riA = p.W + L.riA, *riB = p.W + L.riB, *idx = p.W + L.dtB, *zn = p.W + L.dz;
     double *w = p.W + L.w, *mult = p.W + L.rd, *ra = p.W + L.q;
@@ -1001,7 +1005,28 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
         }
         __syncthreads();
         PST(6);
-        // checks at zn
+        // checks at zn.  A' nuA by groups of 16 columns, lanes over the rows (coalesced, 16 loads in
+        // flight) and one transposed wave sum per group, into xs (free here); one thread per column
+        // running down the m rows waited on every load (round 6)
+        if (m > 0) {
+            const int lane = tid & 63, wv = tid >> 6;
+            for (int g0 = 16 * wv; g0 < n; g0 += 16 * (NTH / 64)) {
+                double ac[16];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) ac[c] = 0.0;
+                for (int r = lane; r < m; r += 64) {
+                    const double nr = nuA[r];
+                    double av[16];
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) av[c] = p.A[(int64_t)min(g0 + c, n - 1) * m + r];
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) ac[c] = fma(av[c], nr, ac[c]);
+                }
+                const double tot = wsum_t(ac, lane);
+                if (lane < 16 && g0 + lane < n) xs[g0 + lane] = tot;
+            }
+            __syncthreads();
+        }
         double viol = 0.0, va = 0.0, lmx = 0.0, lneg = 0.0, fe = 0.0, st = 0.0, gs = 0.0;
         for (int r = tid; r < m; r += NTH) {
             const double v = gdot(r, zn) - p.b[r];
@@ -1021,7 +1046,7 @@ __device__ bool dense_polish(const DPolish p, double* sc, double* xs) {
             for (int i = 0; i < n; ++i) v += p.H[(int64_t)i * n + j] * zn[i];
             gs = fmax(gs, fabs(v));
             for (int k = 0; k < me; ++k) v += p.E[(int64_t)j * me + k] * mult[k];
-            for (int r = 0; r < m; ++r) v += p.A[(int64_t)j * m + r] * nuA[r];
+            if (m > 0) v += xs[j];
             v += nuB[j] - nuB[n + j];
             st = fmax(st, fabs(v));
         }
@@ -2582,7 +2607,9 @@ __global__ void __launch_bounds__(DT) dense_polish_kernel(DenseKernelArgs a) {
     const double rows = red.sum(cnt) + (double)m;
     const double bscale = red.max(bsl);
     if (rows == 0.0 || red.max(zf) != 0.0) return;
-    const DPolish pp{n, m, me, H, f, A, b, E, e, lb, ub, z, y, tA, lA, tB, lB, W, bscale, a.tol_stat};
+    extern __shared__ double plds[];
+    double* Kl = (size_t)n * n <= DQ_POL_KLDS ? plds : nullptr;
+    const DPolish pp{n, m, me, H, f, A, b, E, e, lb, ub, z, y, tA, lA, tB, lB, W, bscale, a.tol_stat, Kl};
     if (!dense_polish<DT, Red>(pp, sc, xs)) return;
     const double stat = sc[10], feas = sc[11];
     double fv = 0.0;
@@ -2683,7 +2710,14 @@ hipError_t launch_dense(const DenseKernelArgs& a0, hipStream_t st) {
     }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess || (!a.polish && !a.pol_it) || !a.work) return err;
-    hipLaunchKernelGGL(dense_polish_kernel, dim3(a.batch), dim3(DT), 0, st, a);
+    // K of the polish in LDS when it fits (dense_polish: DPolish::Kl)
+    const size_t plds = (size_t)a.n * a.n <= DQ_POL_KLDS ? sizeof(double) * a.n * a.n : 0;
+    if (plds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)dense_polish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(sizeof(double) * DQ_POL_KLDS));
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(dense_polish_kernel, dim3(a.batch), dim3(DT), plds, st, a);
     return hipGetLastError();
 }
 

@@ -837,7 +837,8 @@ struct DPolish {
 };
 
 #ifdef BQP_DSTAMPS
-// diagnostic build only: s_memtime cycles per phase of the polish of instance 0 (printed at exit)
+// diagnostic build only: s_memtime cycles per phase of the polish (every 16th instance of a launch
+// prints its phases at exit)
 #define PST_DECL                                                           \
     unsigned long long pst_last = __builtin_amdgcn_s_memtime(), pst_acc[9]; \
     int pst_rounds = 0;                                                    \

@@ -532,25 +532,30 @@ __device__ __forceinline__ void lb_tile(int w, int u, int nbk, int& I, int& J) {
     J = o - i * (i - 1) / 2;
 }
 // rows r0 .. r0 + rc - 1 of the row-major nrows x n matrix G into the tile T (rows 0 .. R - 1,
-// stride ld, ncp = 16 ceil(n / 16) columns, zeros past rc and n): 8 loads in flight per thread
+// stride ld, ncp = 16 ceil(n / 16) columns, zeros past rc and n) in two halves (round 6):
+// lb_fetch_rows issues the loads of the next row tile into registers before the matrix cores
+// consume the current one, lb_put_rows stores them after the next barrier - one memory round trip
+// per tile, hidden behind the MFMAs, instead of two to four exposed ones (250k of the exact-Hessian kernel's cycles were its row-tile loads: stamps of the
+// diagnostic build, gpurun_out/r06_q)
 template <int R>
-__device__ __forceinline__ void lb_load_rows(double* T, const double* G, int r0, int rc, int n, int ncp, int ld,
-                                             int tid) {
+__device__ __forceinline__ void lb_fetch_rows(double (&v)[R / 2], const double* G, int r0, int rc, int n, int ncp,
+                                              int tid) {
+    const int tot = R * ncp;               // <= R * 128 = 256 * R / 2
+#pragma unroll
+    for (int u = 0; u < R / 2; ++u) {
+        const int i = tid + 256 * u;
+        const int r = i / ncp, c = i - r * ncp;
+        v[u] = (i < tot && r < rc && c < n) ? G[(int64_t)(r0 + r) * n + c] : 0.0;
+    }
+}
+template <int R>
+__device__ __forceinline__ void lb_put_rows(double* T, const double (&v)[R / 2], int ncp, int ld, int tid) {
     const int tot = R * ncp;
-    for (int b0 = 0; b0 < tot; b0 += 8 * 256) {
-        double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = b0 + tid + 256 * u;
-            const int r = i / ncp, c = i - r * ncp;
-            v[u] = (i < tot && r < rc && c < n) ? G[(int64_t)(r0 + r) * n + c] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = b0 + tid + 256 * u;
-            const int r = i / ncp, c = i - r * ncp;
-            if (i < tot) T[r * ld + c] = v[u];
-        }
+    for (int u = 0; u < R / 2; ++u) {
+        const int i = tid + 256 * u;
+        const int r = i / ncp, c = i - r * ncp;
+        if (i < tot) T[r * ld + c] = v[u];
     }
 }
 // the k-steps of one tile: acc += X'Y (and, SYM, += Y'X as well)
@@ -591,6 +596,14 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
     double* Kx = lh + 32 * ncp;
     __shared__ double red[4];
     if (n > 128) return;
+#ifdef BQP_RSTAMPS
+    // diagnostic build only: cycles of the row products, the assembly and the Cholesky tests
+    unsigned long long hst0 = __builtin_amdgcn_s_memtime(), hst1 = 0, hst2 = 0;
+    int hatt = 0;
+#define HST_ATT() (++hatt)
+#else
+#define HST_ATT() do { } while (0)
+#endif
     const double* J2 = a.Jr2 + (int64_t)b * nr2 * n;
     const double* T2 = a.Tr2 + (int64_t)b * nr2 * n;
     // S = Jr2'Tr2 + Tr2'Jr2 on the lower block triangle (lb_mfma_rows, two MFMAs per k-step)
@@ -598,14 +611,24 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
     lbd4 acc[LB_TPW];
 #pragma unroll
     for (int u = 0; u < LB_TPW; ++u) { lb_tile(wv, u, nbk, tI[u], tJ[u]); acc[u] = lbd4{0.0, 0.0, 0.0, 0.0}; }
+    double pa[8], pb[8];
+    lb_fetch_rows<16>(pa, J2, 0, min(16, nr2), n, ncp, tid);
+    lb_fetch_rows<16>(pb, T2, 0, min(16, nr2), n, ncp, tid);
     for (int r0 = 0; r0 < nr2; r0 += 16) {
-        const int rc = min(16, nr2 - r0);
         __syncthreads();
-        lb_load_rows<16>(TA, J2, r0, rc, n, ncp, ncp, tid);
-        lb_load_rows<16>(TB, T2, r0, rc, n, ncp, ncp, tid);
+        lb_put_rows<16>(TA, pa, ncp, ncp, tid);
+        lb_put_rows<16>(TB, pb, ncp, ncp, tid);
         __syncthreads();
+        if (r0 + 16 < nr2) {                       // the next tile's loads in flight during the MFMAs
+            lb_fetch_rows<16>(pa, J2, r0 + 16, min(16, nr2 - r0 - 16), n, ncp, tid);
+            lb_fetch_rows<16>(pb, T2, r0 + 16, min(16, nr2 - r0 - 16), n, ncp, tid);
+        }
         lb_mfma_rows<16, true>(acc, tI, tJ, TA, TB, ncp, lane);
     }
+#ifdef BQP_RSTAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    hst1 = __builtin_amdgcn_s_memtime();
+#endif
     // H_GN + the symmetric part S / 2 of Jr2'Tr2, both triangles, in LDS (column-major): each
     // entry (i >= j) belongs to one lane
     const double* H = a.H + (int64_t)b * n * n;
@@ -635,7 +658,12 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
     for (int j = tid; j < n; j += 256) dsave[j] = Kx[j * n + j];
     __syncthreads();
     // Cholesky test of H + sh I: lower triangle restored from the upper one, every pivot above tol
+#ifdef BQP_RSTAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    hst2 = __builtin_amdgcn_s_memtime();
+#endif
     auto attempt = [&](double sh) -> bool {
+        HST_ATT();
         for (int e = tid; e < n * n; e += 256) {
             const int i = e % n, j = e / n;
             if (i > j) Kx[e] = Kx[i * n + j];
@@ -676,6 +704,11 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
         }
         shift = ldexp(1e-12 * hd, 2 * hi);
     }
+#ifdef BQP_RSTAMPS
+    if ((b & 15) == 0 && tid == 0)
+        printf("HSTAMPS gemm %llu assembly %llu tests %llu attempts %d\n", hst1 - hst0, hst2 - hst1,
+               __builtin_amdgcn_s_memtime() - hst2, hatt);
+#endif
     double* Hw = a.H + (int64_t)b * n * n;
     for (int e = tid; e < n * n; e += 256) {
         const int i = e % n, j = e / n;
@@ -706,12 +739,16 @@ __global__ void __launch_bounds__(256) lbmpc_normal_kernel(LbmpcArgs a) {
 #pragma unroll
     for (int u = 0; u < LB_TPW; ++u) { lb_tile(wv, u, nbk, tI[u], tJ[u]); acc[u] = lbd4{0.0, 0.0, 0.0, 0.0}; }
     double fa = 0.0;
+    double pj[LB_RC / 2];
+    lb_fetch_rows<LB_RC>(pj, Jr, 0, min(LB_RC, nr), n, ncp, tid);
     for (int r0 = 0; r0 < nr; r0 += LB_RC) {
         const int rc = min(LB_RC, nr - r0);
         __syncthreads();
-        lb_load_rows<LB_RC>(T, Jr, r0, rc, n, ncp, LB_TS, tid);
+        lb_put_rows<LB_RC>(T, pj, ncp, LB_TS, tid);
         if (tid < LB_RC) E[tid] = tid < rc ? er[r0 + tid] : 0.0;
         __syncthreads();
+        if (r0 + LB_RC < nr)                       // the next tile's loads in flight during the MFMAs
+            lb_fetch_rows<LB_RC>(pj, Jr, r0 + LB_RC, min(LB_RC, nr - r0 - LB_RC), n, ncp, tid);
         lb_mfma_rows<LB_RC, false>(acc, tI, tJ, T, T, LB_TS, lane);
         if (tid < n)
             for (int r = 0; r < rc; ++r) fa += T[r * LB_TS + tid] * E[r];

@@ -32,7 +32,9 @@ namespace bqp {
 
 #define LB_WAVE 64
 #define LB_MAXQ 512      // NW window capacity (data points) held in LDS
-#define LB_CPL 4         // z columns per lane in the sensitivity recursion (n <= 256)
+#define LB_CPL 4         // z columns per lane of the update kernel's column table (n <= 256)
+#define LB_RCPL 2        // z columns per lane in the rollouts' sensitivity recursion: n <= LB_MAXN = 128
+                         // (lbmpc_supported); round 6 - with 4, half the recursion ran on columns past n
 
 // a readlane broadcast kept in vector registers (round 6): as scalar registers the 50 totals of
 // the Hessian rollout's NW sums outgrew the SGPR file and were spilled to and reloaded from VGPR
@@ -245,9 +247,9 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     const double alpha = gn ? 0.0 : ldexp(1.0, -t);
     const double* z = a.z + (int64_t)b * n;
     const double* dz = a.d + (int64_t)b * n;
-    // the trial point z + alpha d in LDS (n <= 4 x 64): one global load per stage put a memory
+    // the trial point z + alpha d in LDS (n <= 2 x 64): one global load per stage put a memory
     // round trip at the head of every stage's chain
-    __shared__ double zsh[LB_WAVE * LB_CPL];
+    __shared__ double zsh[LB_WAVE * LB_RCPL];
     for (int j = lane; j < n; j += LB_WAVE) zsh[j] = gn ? z[j] : z[j] + alpha * dz[j];
     wave_sync();
     auto zv = [&](int j) __attribute__((always_inline)) -> double { return zsh[j]; };
@@ -283,9 +285,9 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
 #pragma unroll
     for (int i = 0; i < NX; ++i) { x[i] = x0[i]; xn[i] = x0[i]; }
     // sensitivities of the learned (SL) and nominal (SN) states w.r.t. z, columns j = lane + 64 c
-    double SL[LB_CPL][NX], SN[LB_CPL][NX];
+    double SL[LB_RCPL][NX], SN[LB_RCPL][NX];
 #pragma unroll
-    for (int c = 0; c < LB_CPL; ++c)
+    for (int c = 0; c < LB_RCPL; ++c)
 #pragma unroll
         for (int i = 0; i < NX; ++i) { SL[c][i] = 0.0; SN[c][i] = 0.0; }
     double* Jr = gn ? a.Jr + (int64_t)b * nr * n : nullptr;
@@ -312,7 +314,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
             if (gn) {
                 if (lane == 0) er[row + r] = e;
 #pragma unroll
-                for (int c = 0; c < LB_CPL; ++c) {
+                for (int c = 0; c < LB_RCPL; ++c) {
                     const int j = lane + LB_WAVE * c;
                     if (j < n) {
                         double acc = 0.0;
@@ -336,10 +338,10 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
 #pragma unroll
         for (int i = 0; i < NX; ++i) { u += Km(0, i) * x[i]; un += Km(0, i) * xn[i]; }
         // input sensitivities U = K S + e_k
-        double UL[LB_CPL], UN[LB_CPL];
+        double UL[LB_RCPL], UN[LB_RCPL];
         if (gn) {
 #pragma unroll
-            for (int c = 0; c < LB_CPL; ++c) {
+            for (int c = 0; c < LB_RCPL; ++c) {
                 const int j = lane + LB_WAVE * c;
                 double ul = (j == k) ? 1.0 : 0.0, unn = ul;
 #pragma unroll
@@ -386,7 +388,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         }
         if (gn) {
 #pragma unroll
-            for (int c = 0; c < LB_CPL; ++c) {
+            for (int c = 0; c < LB_RCPL; ++c) {
                 double sl[NX], sn[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) {
@@ -468,7 +470,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
     double* J2 = a.Jr2 + (int64_t)b * 3 * N * n;
     double* T2 = a.Tr2 + (int64_t)b * 3 * N * n;
 #pragma unroll
-    for (int c = 0; c < LB_CPL; ++c)
+    for (int c = 0; c < LB_RCPL; ++c)
 #pragma unroll
         for (int i = 0; i < NX; ++i) SL[c][i] = 0.0;
     for (int k = 0; k < N; ++k) {
@@ -476,7 +478,7 @@ __global__ void __launch_bounds__(64) lbmpc_rollout_kernel(LbmpcArgs a, int gn) 
         const double* st = SS + (int64_t)k * LB_SS;
         const double w00 = st[12], w01 = st[13], w02 = st[14], w11 = st[15], w12 = st[16], w22 = st[17];
 #pragma unroll
-        for (int c = 0; c < LB_CPL; ++c) {
+        for (int c = 0; c < LB_RCPL; ++c) {
             const int j = lane + LB_WAVE * c;
             double ul = (j == k) ? 1.0 : 0.0;
 #pragma unroll
@@ -908,7 +910,7 @@ hipError_t launch_nw_oracle(int batch, int q, const double* data, int64_t sdata,
 }
 
 bool lbmpc_supported(int nx, int nu, int np, int n, int q) {
-    return nx == 4 && nu == 1 && np == 1 && n <= LB_MAXN && n <= LB_WAVE * LB_CPL && q >= 1 &&
+    return nx == 4 && nu == 1 && np == 1 && n <= LB_MAXN && n <= LB_WAVE * LB_RCPL && q >= 1 &&
            q <= LB_MAXQ;
 }
 
@@ -922,8 +924,8 @@ hipError_t launch_lbmpc_rollout(const LbmpcArgs& a, int gn, hipStream_t st) {
     const int grid = a.batch * (gn ? 1 : a.ntrial);
     const size_t lds = lbmpc_rollout_lds(a, gn);
     auto k = (gn && a.hess) ? lbmpc_rollout_kernel<4, 1, 1, true> : lbmpc_rollout_kernel<4, 1, 1, false>;
-    // z columns: LB_CPL per lane (the sensitivities and the LDS trial point); static LDS ~2.4 KB
-    if (a.n > LB_WAVE * LB_CPL || lds > 156 * 1024) return hipErrorInvalidValue;
+    // z columns: LB_RCPL per lane (the sensitivities and the LDS trial point); static LDS ~1.4 KB
+    if (a.n > LB_WAVE * LB_RCPL || lds > 156 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;

@@ -672,19 +672,35 @@ __global__ void __launch_bounds__(256) lbmpc_hess_kernel(LbmpcArgs a) {
             else if (i == j) Kx[e] = dsave[i] + sh;
         }
         __syncthreads();
+        // two pivots per pair of barriers (round 6): pivot j + 1 and column j + 1 after pivot j's
+        // update are formed from the unscaled values (every thread the pivot, each row's thread its
+        // entry), then one pass applies both rank-1 updates.  Each entry receives the same
+        // operations in the same order as one pivot at a time - the scaled column, K -= L L per
+        // pivot - so the outcome of the test is bitwise the one-pivot form's.
         bool pd = true;
-        for (int j = 0; j < n; ++j) {
-            const double d = Kx[j * n + j];
-            if (!(d > tol)) { pd = false; break; }      // uniform: every thread reads the same pivot
-            const double sq = sqrt(d);
-            for (int i = j + 1 + tid; i < n; i += 256) Kx[j * n + i] /= sq;
+        for (int j = 0; j < n; j += 2) {
+            const double d0 = Kx[j * n + j];
+            if (!(d0 > tol)) { pd = false; break; }     // uniform: every thread reads the same pivot
+            if (j + 1 == n) break;
+            const double sq0 = sqrt(d0);
+            const double l10 = Kx[j * n + j + 1] / sq0;                  // L(j + 1, j)
+            const double d1 = Kx[(j + 1) * n + j + 1] - l10 * l10;
+            if (!(d1 > tol)) { pd = false; break; }
+            const double sq1 = sqrt(d1);
+            for (int i = j + 2 + tid; i < n; i += 256) {
+                const double a0 = Kx[j * n + i] / sq0;
+                Kx[j * n + i] = a0;
+                Kx[(j + 1) * n + i] = (Kx[(j + 1) * n + i] - a0 * l10) / sq1;
+            }
             __syncthreads();
-            // trailing update over a 16 x 16 thread grid (ty: columns c, tx: rows i >= c) - each
-            // entry gets the same update as before, in the same order; one thread per column c
-            // ran the c loop serially (~5k cycles per pivot, ~0.5M per test at n = 101)
-            for (int c = j + 1 + ty; c < n; c += 16) {
-                const double lc = Kx[j * n + c];
-                for (int i = c + tx; i < n; i += 16) Kx[c * n + i] -= Kx[j * n + i] * lc;
+            // trailing update over a 16 x 16 thread grid (ty: columns c, tx: rows i >= c); one
+            // thread per column c ran the c loop serially (~5k cycles per pivot, round 4)
+            for (int c = j + 2 + ty; c < n; c += 16) {
+                const double lc0 = Kx[j * n + c], lc1 = Kx[(j + 1) * n + c];
+                for (int i = c + tx; i < n; i += 16) {
+                    const double v = Kx[c * n + i] - Kx[j * n + i] * lc0;
+                    Kx[c * n + i] = v - Kx[(j + 1) * n + i] * lc1;
+                }
             }
             __syncthreads();
         }
